@@ -1,0 +1,165 @@
+/*
+ * lcrc.h -- C ABI of the MI355X (gfx950) block/record checksum engine for leveldb-rust.
+ *
+ * This is the drop-in boundary for the checksum path of FateTHarlaown/leveldb-rust. The reference
+ * computes every block-trailer and WAL-record checksum with the external crate `crc32fast`
+ * (Cargo.toml:11, "1.2.0") through a stack-local `crc32fast::Hasher` at four call sites:
+ *   (1) LogWriter::emit_physical_record   src/db/log.rs:61-64    crc over type_u8 || payload
+ *   (2) LogReader::read_physical_record   src/db/log.rs:261-264  same, verified against header[0..4]
+ *   (3) write_raw_block                   src/sstable/table.rs:519-522  crc over content || type_u8
+ *   (4) BlockContent::read_block_from_file src/sstable/format.rs:164-166 verify data[0..n+1]
+ * The masked CRC-32C named by the project metric appears only inside the `snap` crate's framing
+ * (Cargo.toml:15; used at src/sstable/table.rs:486, src/sstable/format.rs:196).
+ *
+ * Entry points, and the reference interface each replaces:
+ *   lcrc_hasher_{init,update,finalize}  <- crc32fast::Hasher::{new, update, finalize} (call sites 1-4)
+ *   lcrc32_value / lcrc32_extend        <- Hasher::new().update(p).finalize() /
+ *                                          Hasher::new_with_initial(crc).update(p).finalize()
+ *   lcrc32c_{value,extend,mask,unmask}  <- the crc32c value/extend/mask surface (north star; the
+ *                                          snap framing's masked CRC-32C)
+ *   lcrc_combine                        <- crc32fast::Hasher::combine (zlib crc32_combine)
+ *   lcrc_batch / lcrc_batch_uniform     <- N independent calls of (3)/(4): one launch checksums and
+ *                                          optionally verifies thousands of device-resident blocks
+ *   lcrc_batch_host_uniform             <- the same starting and ending in host memory (pinned H2D,
+ *                                          kernel, D2H, double-buffered)
+ *   lcrc_wal_scan                       <- the header parse + CRC verify of (2) for every physical record
+ *                                          of a device-resident log file, 32 KiB block by block
+ *
+ * Conventions: plain pointers and sizes, no exceptions cross the boundary, every call returns an int
+ * status (LCRC_OK = 0). Buffers are owned by the caller. A context is bound to one device and one mode;
+ * calls on one context must not race each other (use one context per host thread). `stream` is a
+ * hipStream_t (NULL = the context's own stream). The batched calls are GPU-only: when no device or
+ * kernel image is available they return LCRC_ENODEV and compute nothing -- there is no CPU fallback.
+ */
+#ifndef LCRC_H
+#define LCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define LCRC_OK 0
+#define LCRC_EINVAL (-1)  /* bad argument */
+#define LCRC_ENODEV (-2)  /* no HIP device / kernel image unavailable */
+#define LCRC_EHIP (-3)    /* HIP runtime error (see lcrc_last_error) */
+#define LCRC_ENOMEM (-4)  /* device or pinned allocation failed */
+
+/* ---- CRC modes ---- */
+#define LCRC_MODE_REF 0 /* CRC-32/ISO-HDLC, refl. poly 0xEDB88320: bit-exact with crc32fast::Hasher */
+#define LCRC_MODE_C 1   /* CRC-32C (Castagnoli), refl. poly 0x82F63B78 */
+
+/* ---- flags ---- */
+#define LCRC_FLAG_MASK 0x1u   /* outputs (and expected values) are LevelDB-masked: rotr15(crc)+0xa282ead8 */
+#define LCRC_FLAG_DIRECT 0x2u /* lcrc_batch: skip the window pass, walk every block directly (sparse sets) */
+
+/* ---- scalar host API (drop-in for crc32fast::Hasher at the four call sites) ---- */
+uint32_t lcrc32_value(const uint8_t* p, size_t n);
+uint32_t lcrc32_extend(uint32_t crc, const uint8_t* p, size_t n);
+uint32_t lcrc32c_value(const uint8_t* p, size_t n);
+uint32_t lcrc32c_extend(uint32_t crc, const uint8_t* p, size_t n);
+uint32_t lcrc32c_mask(uint32_t crc);
+uint32_t lcrc32c_unmask(uint32_t masked);
+uint32_t lcrc_extend(int mode, uint32_t crc, const uint8_t* p, size_t n);
+uint32_t lcrc_combine(int mode, uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+typedef struct lcrc_hasher {
+  uint32_t state;  /* finalized CRC of the bytes seen so far */
+  int32_t mode;    /* LCRC_MODE_* */
+  uint64_t amount; /* bytes seen */
+} lcrc_hasher;
+void lcrc_hasher_init(lcrc_hasher* h, int mode);
+void lcrc_hasher_update(lcrc_hasher* h, const uint8_t* p, size_t n);
+uint32_t lcrc_hasher_finalize(const lcrc_hasher* h);
+
+/* ---- batched device API ---- */
+typedef struct lcrc_ctx lcrc_ctx;
+
+/* One checksummed byte range. The covered bytes are base[offset, offset+length). If expect_rel !=
+ * LCRC_NO_EXPECT the expected CRC is the little-endian u32 at base[offset + expect_rel]:
+ *   SSTable block with handle (off, n):  {off, n + 1, n + 1}   (table.rs:507-529, format.rs:162-171)
+ *   WAL physical record with header at h: {h + 6, 1 + len, -6}  (log.rs:58-80, log.rs:233-273)   */
+typedef struct lcrc_desc {
+  uint64_t offset;
+  uint32_t length;
+  int32_t expect_rel;
+} lcrc_desc;
+#define LCRC_NO_EXPECT ((int32_t)0x80000000)
+
+/* WAL physical record as parsed on the device by lcrc_wal_scan (one per record, in file order). */
+typedef struct lcrc_wal_rec {
+  uint64_t header;   /* file offset of the 7-byte header */
+  uint32_t length;   /* payload length (header bytes 4..6) */
+  uint8_t type;      /* header byte 6 */
+  uint8_t status;    /* LCRC_WAL_OK / LCRC_WAL_CRC_MISMATCH */
+  uint16_t block_end; /* 1 if this is the last record parsed in its 32 KiB block (see stop) */
+  uint32_t crc;      /* computed crc over type || payload */
+  uint32_t stop;     /* for the last record of a block: why parsing stopped (LCRC_WAL_STOP_*) */
+} lcrc_wal_rec;
+#define LCRC_WAL_OK 0
+#define LCRC_WAL_CRC_MISMATCH 1
+#define LCRC_WAL_STOP_TRAILER 0    /* < 7 bytes left in the block */
+#define LCRC_WAL_STOP_BAD_LENGTH 1 /* 7 + length exceeds the bytes left in the block */
+#define LCRC_WAL_STOP_ZERO 2       /* type == 0 && length == 0 (zero fill) */
+#define LCRC_WAL_STOP_MISMATCH 3   /* checksum mismatch: the reader drops the rest of the block */
+
+int lcrc_device_count(int* n);
+int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags);
+int lcrc_ctx_destroy(lcrc_ctx* ctx);
+/* Pre-allocate the device workspace for spans up to max_span bytes (so later calls allocate nothing
+ * and can be captured in a hipGraph). */
+int lcrc_ctx_reserve(lcrc_ctx* ctx, uint64_t max_span);
+/* hipStream_t owned by the context (for callers that want to enqueue around it). */
+void* lcrc_ctx_stream(lcrc_ctx* ctx);
+int lcrc_ctx_sync(lcrc_ctx* ctx);
+
+/* CRC of n ranges of the device buffer base[0, base_len). out_crc[i] (device) gets the CRC (masked if
+ * LCRC_FLAG_MASK). out_mismatch (device, nullable, ceil(n/32) u32 words, zeroed by the call) gets bit i
+ * set when descriptor i has an expected value and it differs. Ranges may be in any order and may
+ * overlap; every byte of [0, base_len) is streamed once unless LCRC_FLAG_DIRECT is given. */
+int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
+               uint32_t* out_crc, uint32_t* out_mismatch, void* stream);
+
+/* n blocks of `length` bytes, block i at base + i*stride (device). expected (device, nullable):
+ * per-block expected CRCs. The 4 KiB / stride 4 KiB case is the single-pass fast path. */
+int lcrc_batch_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
+                       const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch, void* stream);
+
+/* Same as lcrc_batch_uniform but base / expected / out_crc / out_mismatch are HOST pointers. Data is
+ * staged through pinned buffers in chunks of chunk_bytes (0 = default) with H2D copies overlapping
+ * the kernels. Synchronous. */
+int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
+                            const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch,
+                            size_t chunk_bytes);
+
+/* Parse and verify every physical record of a device-resident log file (file_len bytes, 32 KiB
+ * blocks, layout of src/db/log.rs). Records are written in file order to recs (device, capacity
+ * max_recs); *n_recs (host) receives the count. Returns LCRC_EINVAL if max_recs is too small. */
+int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs,
+                  size_t max_recs, size_t* n_recs, void* stream);
+
+/* ---- device memory helpers (so a binding needs nothing but this library) ---- */
+int lcrc_dev_alloc(int device, size_t bytes, void** out);
+int lcrc_dev_free(void* p);
+int lcrc_host_alloc_pinned(size_t bytes, void** out);
+int lcrc_host_free_pinned(void* p);
+int lcrc_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int lcrc_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int lcrc_memset_d(void* dst, int value, size_t bytes);
+int lcrc_device_sync(void);
+/* Event timing on the context stream (milliseconds between two recorded events). */
+int lcrc_timer_start(lcrc_ctx* ctx);
+int lcrc_timer_stop(lcrc_ctx* ctx, float* ms);
+
+/* Last HIP error string for this thread ("" if none). */
+const char* lcrc_last_error(void);
+/* Library build identification (kernel arch, version). */
+const char* lcrc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LCRC_H */

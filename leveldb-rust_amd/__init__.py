@@ -1,0 +1,554 @@
+"""leveldb-rust_amd -- MI355X-native block/record checksum engine for leveldb-rust (Python host mirror).
+
+This package is loaded under the importable name ``leveldb_rust_amd`` (the directory name has a hyphen;
+see ``load()`` in ``__graft_entry__.py``). It binds ``_build/liblcrc.so`` (built by ``build.py``) through
+ctypes and mirrors the reference's interfaces for the checksum path:
+
+* ``Hasher`` / ``value`` / ``extend``   -- ``crc32fast::Hasher::{new, update, finalize}`` as used at
+  src/db/log.rs:61-64, :261-264, src/sstable/table.rs:519-522, src/sstable/format.rs:164-166
+* ``crc32c_value`` / ``crc32c_extend`` / ``mask`` / ``unmask`` -- the crc32c value/extend/mask surface
+* ``Engine`` -- the batched device API (``lcrc_batch*``, ``lcrc_wal_scan``); GPU only, raises
+  ``NoDeviceError`` when no gfx950 device/kernel image is available (there is no CPU fallback)
+* ``LogWriter`` / ``LogReader`` / ``BatchLogReader`` -- src/db/log.rs LogWriter / LogReader
+* ``TableFile`` -- write_raw_block (table.rs:507-529) and read_block_from_file (format.rs:146-213)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "liblcrc.so")
+
+MODE_REF = 0  # CRC-32/ISO-HDLC (crc32fast)
+MODE_C = 1  # CRC-32C
+FLAG_MASK = 0x1
+FLAG_DIRECT = 0x2
+NO_EXPECT = -0x80000000
+
+OK, EINVAL, ENODEV, EHIP, ENOMEM = 0, -1, -2, -3, -4
+
+WAL_OK, WAL_CRC_MISMATCH = 0, 1
+WAL_STOP_TRAILER, WAL_STOP_BAD_LENGTH, WAL_STOP_ZERO = 0, 1, 2
+
+BLOCK_SIZE = 32768  # src/db/mod.rs:45
+HEADER_SIZE = 7  # src/db/mod.rs:48
+BLOCK_TRAILER_SIZE = 5  # src/sstable/format.rs:22
+
+
+class LcrcError(RuntimeError):
+    pass
+
+
+class NoDeviceError(LcrcError):
+    pass
+
+
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("expect_rel", "<i4")])
+WAL_REC_DTYPE = np.dtype([("header", "<u8"), ("length", "<u4"), ("type", "u1"), ("status", "u1"),
+                          ("block_end", "<u2"), ("crc", "<u4"), ("stop", "<u4")])
+
+
+class _Desc(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("length", ctypes.c_uint32), ("expect_rel", ctypes.c_int32)]
+
+
+class _WalRec(ctypes.Structure):
+    _fields_ = [("header", ctypes.c_uint64), ("length", ctypes.c_uint32), ("type", ctypes.c_uint8),
+                ("status", ctypes.c_uint8), ("block_end", ctypes.c_uint16), ("crc", ctypes.c_uint32),
+                ("stop", ctypes.c_uint32)]
+
+
+class _Hasher(ctypes.Structure):
+    _fields_ = [("state", ctypes.c_uint32), ("mode", ctypes.c_int32), ("amount", ctypes.c_uint64)]
+
+
+_lib = None
+
+# every symbol declared in include/lcrc.h (tests check the library exports all of them)
+ABI_SYMBOLS = [
+    "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
+    "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
+    "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
+    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_host_uniform", "lcrc_wal_scan",
+    "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
+    "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
+    "lcrc_last_error", "lcrc_version",
+]
+
+
+def lib():
+    """Load the native library (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LcrcError(f"{LIB_PATH} missing: run build() (leveldb-rust_amd/build.py) first")
+    L = ctypes.CDLL(LIB_PATH)
+    u32, u64, sz, vp, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+    cp = ctypes.c_char_p
+
+    def sig(name, res, *args):
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = list(args)
+
+    sig("lcrc32_value", u32, vp, sz)
+    sig("lcrc32_extend", u32, u32, vp, sz)
+    sig("lcrc32c_value", u32, vp, sz)
+    sig("lcrc32c_extend", u32, u32, vp, sz)
+    sig("lcrc32c_mask", u32, u32)
+    sig("lcrc32c_unmask", u32, u32)
+    sig("lcrc_extend", u32, i32, u32, vp, sz)
+    sig("lcrc_combine", u32, i32, u32, u32, u64)
+    sig("lcrc_hasher_init", None, ctypes.POINTER(_Hasher), i32)
+    sig("lcrc_hasher_update", None, ctypes.POINTER(_Hasher), vp, sz)
+    sig("lcrc_hasher_finalize", u32, ctypes.POINTER(_Hasher))
+    sig("lcrc_device_count", i32, ctypes.POINTER(ctypes.c_int))
+    sig("lcrc_ctx_create", i32, ctypes.POINTER(vp), i32, i32, u32)
+    sig("lcrc_ctx_destroy", i32, vp)
+    sig("lcrc_ctx_reserve", i32, vp, u64)
+    sig("lcrc_ctx_stream", vp, vp)
+    sig("lcrc_ctx_sync", i32, vp)
+    sig("lcrc_batch", i32, vp, vp, u64, vp, sz, vp, vp, vp)
+    sig("lcrc_batch_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, vp)
+    sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
+    sig("lcrc_wal_scan", i32, vp, vp, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp)
+    sig("lcrc_dev_alloc", i32, i32, sz, ctypes.POINTER(vp))
+    sig("lcrc_dev_free", i32, vp)
+    sig("lcrc_host_alloc_pinned", i32, sz, ctypes.POINTER(vp))
+    sig("lcrc_host_free_pinned", i32, vp)
+    sig("lcrc_memcpy_h2d", i32, vp, vp, sz)
+    sig("lcrc_memcpy_d2h", i32, vp, vp, sz)
+    sig("lcrc_memset_d", i32, vp, i32, sz)
+    sig("lcrc_device_sync", i32)
+    sig("lcrc_timer_start", i32, vp)
+    sig("lcrc_timer_stop", i32, vp, ctypes.POINTER(ctypes.c_float))
+    sig("lcrc_last_error", cp)
+    sig("lcrc_version", cp)
+    # C++ restatement of the reference call sites (lcrc_leveldb.cpp)
+    sig("lcrc_logw_create", vp, u64)
+    sig("lcrc_logw_destroy", None, vp)
+    sig("lcrc_logw_add", None, vp, vp, sz)
+    sig("lcrc_logw_size", sz, vp)
+    sig("lcrc_logw_data", vp, vp)
+    sig("lcrc_logw_prepend", None, vp, vp, sz)
+    sig("lcrc_logr_create", vp, vp, sz)
+    sig("lcrc_logr_create_batch", vp, vp, sz, vp, sz)
+    sig("lcrc_logr_destroy", None, vp)
+    sig("lcrc_logr_force_error", None, vp)
+    sig("lcrc_logr_read", i32, vp)
+    sig("lcrc_logr_record", sz, vp, ctypes.POINTER(vp))
+    sig("lcrc_logr_dropped", sz, vp)
+    sig("lcrc_logr_message", cp, vp)
+    sig("lcrc_logr_consistency_errors", i32, vp)
+    sig("lcrc_tbl_create", vp)
+    sig("lcrc_tbl_destroy", None, vp)
+    sig("lcrc_tbl_write_raw_block", None, vp, vp, sz, ctypes.c_uint8, ctypes.POINTER(u64), ctypes.POINTER(u64))
+    sig("lcrc_tbl_size", sz, vp)
+    sig("lcrc_tbl_data", vp, vp)
+    sig("lcrc_tbl_append", None, vp, vp, sz)
+    sig("lcrc_tbl_read_block", cp, vp, sz, u64, u64, i32, ctypes.POINTER(ctypes.c_uint8))
+    _lib = L
+    return L
+
+
+def _buf(data):
+    """(pointer, length, keepalive) for bytes / bytearray / numpy array."""
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data)
+        return a.ctypes.data_as(ctypes.c_void_p), a.nbytes, a
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(bytes(data) if isinstance(data, memoryview) else data, dtype=np.uint8)
+        return a.ctypes.data_as(ctypes.c_void_p), a.nbytes, a
+    raise TypeError(type(data))
+
+
+def _check(rc, what):
+    if rc == OK:
+        return
+    msg = f"{what} failed ({rc}): {lib().lcrc_last_error().decode(errors='replace')}"
+    if rc == ENODEV:
+        raise NoDeviceError(msg)
+    raise LcrcError(msg)
+
+
+# ---------------------------------------------------------------------------------------------------
+# scalar API (host)
+# ---------------------------------------------------------------------------------------------------
+def value(data, mode=MODE_REF):
+    p, n, _k = _buf(data)
+    return lib().lcrc_extend(mode, 0, p, n)
+
+
+def extend(crc, data, mode=MODE_REF):
+    p, n, _k = _buf(data)
+    return lib().lcrc_extend(mode, crc, p, n)
+
+
+def crc32c_value(data):
+    return value(data, MODE_C)
+
+
+def crc32c_extend(crc, data):
+    return extend(crc, data, MODE_C)
+
+
+def mask(crc):
+    return lib().lcrc32c_mask(crc)
+
+
+def unmask(m):
+    return lib().lcrc32c_unmask(m)
+
+
+def combine(crc_a, crc_b, len_b, mode=MODE_REF):
+    return lib().lcrc_combine(mode, crc_a, crc_b, len_b)
+
+
+class Hasher:
+    """Mirror of ``crc32fast::Hasher``: ``Hasher()``, ``update(bytes)``, ``finalize() -> int``."""
+
+    def __init__(self, mode=MODE_REF, initial=0):
+        self._h = _Hasher()
+        lib().lcrc_hasher_init(ctypes.byref(self._h), mode)
+        self._h.state = initial
+
+    @classmethod
+    def new_with_initial(cls, crc, mode=MODE_REF):
+        return cls(mode, crc)
+
+    def update(self, data):
+        p, n, _k = _buf(data)
+        lib().lcrc_hasher_update(ctypes.byref(self._h), p, n)
+
+    def finalize(self):
+        return lib().lcrc_hasher_finalize(ctypes.byref(self._h))
+
+    @property
+    def amount(self):
+        return self._h.amount
+
+
+# ---------------------------------------------------------------------------------------------------
+# device memory + batched engine
+# ---------------------------------------------------------------------------------------------------
+def device_count():
+    n = ctypes.c_int(0)
+    lib().lcrc_device_count(ctypes.byref(n))
+    return n.value
+
+
+class DeviceBuffer:
+    """Raw device allocation owned by Python (freed on close/GC)."""
+
+    def __init__(self, nbytes, device=0):
+        self.nbytes = int(nbytes)
+        self.device = device
+        p = ctypes.c_void_p()
+        _check(lib().lcrc_dev_alloc(device, self.nbytes, ctypes.byref(p)), "lcrc_dev_alloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_host(cls, data, device=0, pad=0):
+        p, n, _k = _buf(data)
+        b = cls(n + pad, device)
+        if n:
+            _check(lib().lcrc_memcpy_h2d(b.ptr, p, n), "lcrc_memcpy_h2d")
+        return b
+
+    def upload(self, data, offset=0):
+        p, n, _k = _buf(data)
+        assert offset + n <= self.nbytes
+        if n:
+            _check(lib().lcrc_memcpy_h2d(self.ptr + offset, p, n), "lcrc_memcpy_h2d")
+
+    def download(self, dtype=np.uint8, count=None, offset=0):
+        dtype = np.dtype(dtype)
+        if count is None:
+            count = (self.nbytes - offset) // dtype.itemsize
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            _check(lib().lcrc_memcpy_d2h(out.ctypes.data_as(ctypes.c_void_p), self.ptr + offset, out.nbytes),
+                   "lcrc_memcpy_d2h")
+        return out
+
+    def zero(self):
+        _check(lib().lcrc_memset_d(self.ptr, 0, self.nbytes), "lcrc_memset_d")
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            lib().lcrc_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PinnedBuffer:
+    def __init__(self, nbytes):
+        p = ctypes.c_void_p()
+        _check(lib().lcrc_host_alloc_pinned(int(nbytes), ctypes.byref(p)), "lcrc_host_alloc_pinned")
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            lib().lcrc_host_free_pinned(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, (DeviceBuffer, PinnedBuffer)):
+        return x.ptr
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):  # torch tensor
+        return x.data_ptr()
+    raise TypeError(type(x))
+
+
+class Engine:
+    """One device + one CRC mode (``lcrc_ctx``). All batched calls are GPU-only."""
+
+    def __init__(self, device=0, mode=MODE_C, flags=0):
+        self.device, self.mode, self.flags = device, mode, flags
+        ctx = ctypes.c_void_p()
+        _check(lib().lcrc_ctx_create(ctypes.byref(ctx), device, mode, flags), "lcrc_ctx_create")
+        self.ctx = ctx.value
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            lib().lcrc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return lib().lcrc_ctx_stream(self.ctx)
+
+    def sync(self):
+        _check(lib().lcrc_ctx_sync(self.ctx), "lcrc_ctx_sync")
+
+    def reserve(self, max_span):
+        _check(lib().lcrc_ctx_reserve(self.ctx, int(max_span)), "lcrc_ctx_reserve")
+
+    def batch(self, base, base_len, descs, n, out_crc, out_mismatch=None, stream=None):
+        _check(lib().lcrc_batch(self.ctx, _ptr(base), int(base_len), _ptr(descs), int(n), _ptr(out_crc),
+                                _ptr(out_mismatch), stream), "lcrc_batch")
+
+    def batch_uniform(self, base, n, length, stride, out_crc, expected=None, out_mismatch=None, stream=None):
+        _check(lib().lcrc_batch_uniform(self.ctx, _ptr(base), int(n), int(length), int(stride), _ptr(expected),
+                                        _ptr(out_crc), _ptr(out_mismatch), stream), "lcrc_batch_uniform")
+
+    def batch_host_uniform(self, base, n, length, stride, expected=None, chunk_bytes=0):
+        """Host-resident input (numpy / PinnedBuffer). Returns (crc array, mismatch bitmap)."""
+        bp, _nb, keep = (base.ptr, base.nbytes, base) if isinstance(base, PinnedBuffer) else _buf(base)
+        out = np.empty(n, np.uint32)
+        mm = np.empty((n + 31) // 32, np.uint32)
+        ep, _, keep2 = _buf(np.ascontiguousarray(expected, np.uint32)) if expected is not None else (None, 0, None)
+        _check(lib().lcrc_batch_host_uniform(self.ctx, bp, int(n), int(length), int(stride), ep,
+                                             out.ctypes.data_as(ctypes.c_void_p), mm.ctypes.data_as(ctypes.c_void_p),
+                                             int(chunk_bytes)), "lcrc_batch_host_uniform")
+        del keep, keep2
+        return out, mm
+
+    def wal_scan(self, file_dev, file_len, max_recs=None, recs_dev=None):
+        """Parse + verify every physical record of a device-resident log. Returns a WAL_REC_DTYPE array."""
+        if max_recs is None:
+            max_recs = max(1, file_len // HEADER_SIZE + 1)
+        own = recs_dev is None
+        if own:
+            recs_dev = DeviceBuffer(max_recs * WAL_REC_DTYPE.itemsize, self.device)
+        n = ctypes.c_size_t(0)
+        _check(lib().lcrc_wal_scan(self.ctx, _ptr(file_dev), int(file_len), _ptr(recs_dev), int(max_recs),
+                                   ctypes.byref(n), None), "lcrc_wal_scan")
+        self.sync()
+        out = recs_dev.download(WAL_REC_DTYPE, n.value)
+        if own:
+            recs_dev.close()
+        return out
+
+    def timer_start(self):
+        _check(lib().lcrc_timer_start(self.ctx), "lcrc_timer_start")
+
+    def timer_stop(self):
+        ms = ctypes.c_float(0)
+        _check(lib().lcrc_timer_stop(self.ctx, ctypes.byref(ms)), "lcrc_timer_stop")
+        return ms.value
+
+    # convenience: host numpy in, host numpy out (copies; for tests)
+    def crc_ranges(self, data, offsets, lengths, expect_rel=None):
+        data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data)
+        n = len(offsets)
+        d = np.zeros(n, DESC_DTYPE)
+        d["offset"] = offsets
+        d["length"] = lengths
+        d["expect_rel"] = NO_EXPECT if expect_rel is None else expect_rel
+        base = DeviceBuffer.from_host(data, self.device)
+        dd = DeviceBuffer.from_host(d.view(np.uint8), self.device)
+        out = DeviceBuffer(max(4 * n, 4), self.device)
+        mm = DeviceBuffer(max(4 * ((n + 31) // 32), 4), self.device)
+        self.batch(base, data.nbytes, dd, n, out, mm)
+        self.sync()
+        crcs = out.download(np.uint32, n)
+        bits = mm.download(np.uint32, (n + 31) // 32)
+        return crcs, unpack_bits(bits, n)
+
+
+def unpack_bits(words, n):
+    w = np.asarray(words, np.uint32)
+    bits = (w[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1
+    return bits.reshape(-1)[:n].astype(bool)
+
+
+# ---------------------------------------------------------------------------------------------------
+# reference call-site mirrors (C++ restatement in csrc/lcrc_leveldb.cpp)
+# ---------------------------------------------------------------------------------------------------
+class LogWriter:
+    """src/db/log.rs LogWriter over an in-memory file. ``offset`` = dest length (new_with_dest_len)."""
+
+    def __init__(self, offset=0, existing=b""):
+        self._w = lib().lcrc_logw_create(offset)
+        if existing:
+            p, n, _k = _buf(existing)
+            lib().lcrc_logw_prepend(self._w, p, n)
+
+    def add_record(self, data):
+        p, n, _k = _buf(data)
+        lib().lcrc_logw_add(self._w, p, n)
+
+    def contents(self):
+        n = lib().lcrc_logw_size(self._w)
+        if n == 0:
+            return b""
+        return ctypes.string_at(lib().lcrc_logw_data(self._w), n)
+
+    def __len__(self):
+        return lib().lcrc_logw_size(self._w)
+
+    def __del__(self):
+        try:
+            lib().lcrc_logw_destroy(self._w)
+        except Exception:
+            pass
+
+
+class EofError(Exception):
+    """StatusError::Eof("meet a eof")"""
+
+    def __str__(self):
+        return "meet a eof"
+
+
+class _ReaderBase:
+    def read_record(self):
+        rc = lib().lcrc_logr_read(self._r)
+        if rc != 0:
+            raise EofError()
+        p = ctypes.c_void_p()
+        n = lib().lcrc_logr_record(self._r, ctypes.byref(p))
+        return ctypes.string_at(p, n) if n else b""
+
+    def records(self):
+        out = []
+        while True:
+            try:
+                out.append(self.read_record())
+            except EofError:
+                return out
+
+    @property
+    def dropped_bytes(self):
+        return lib().lcrc_logr_dropped(self._r)
+
+    @property
+    def report_message(self):
+        return lib().lcrc_logr_message(self._r).decode()
+
+    def __del__(self):
+        try:
+            lib().lcrc_logr_destroy(self._r)
+        except Exception:
+            pass
+
+
+class LogReader(_ReaderBase):
+    """src/db/log.rs LogReader; per-record host checksum (call site 2)."""
+
+    def __init__(self, data):
+        p, n, _k = _buf(data)
+        self._r = lib().lcrc_logr_create(p, n)
+
+    def force_error(self):
+        lib().lcrc_logr_force_error(self._r)
+
+
+class BatchLogReader(_ReaderBase):
+    """Same reader contract; all physical-record checksums of the file verified in one device scan."""
+
+    def __init__(self, data, engine):
+        arr = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+        dev = DeviceBuffer.from_host(arr, engine.device)
+        self.records_scanned = engine.wal_scan(dev, arr.nbytes)
+        dev.close()
+        p, n, _k = _buf(arr)
+        rp, rn, _k2 = _buf(self.records_scanned.view(np.uint8))
+        self._r = lib().lcrc_logr_create_batch(p, n, rp, len(self.records_scanned))
+
+    @property
+    def consistency_errors(self):
+        return lib().lcrc_logr_consistency_errors(self._r)
+
+
+class TableFile:
+    """SSTable block trailers: write_raw_block (table.rs:507-529) / read_block (format.rs:146-213)."""
+
+    def __init__(self):
+        self._t = lib().lcrc_tbl_create()
+
+    def write_raw_block(self, content, block_type):
+        p, n, _k = _buf(content)
+        off, size = ctypes.c_uint64(), ctypes.c_uint64()
+        lib().lcrc_tbl_write_raw_block(self._t, p, n, block_type, ctypes.byref(off), ctypes.byref(size))
+        return off.value, size.value
+
+    def append(self, data):
+        p, n, _k = _buf(data)
+        lib().lcrc_tbl_append(self._t, p, n)
+
+    def contents(self):
+        n = lib().lcrc_tbl_size(self._t)
+        return ctypes.string_at(lib().lcrc_tbl_data(self._t), n) if n else b""
+
+    @staticmethod
+    def read_block(file_bytes, offset, size, verify_checksum):
+        """Returns (block_type, None) or (None, error string) exactly as format.rs:146-213."""
+        p, n, _k = _buf(file_bytes)
+        t = ctypes.c_uint8()
+        err = lib().lcrc_tbl_read_block(p, n, offset, size, 1 if verify_checksum else 0, ctypes.byref(t))
+        return (None, err.decode()) if err else (t.value, None)
+
+    def __del__(self):
+        try:
+            lib().lcrc_tbl_destroy(self._t)
+        except Exception:
+            pass

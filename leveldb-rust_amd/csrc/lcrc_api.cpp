@@ -1,0 +1,449 @@
+// C ABI of the batched device engine (include/lcrc.h). Host-side only: contexts, table upload,
+// workspace, launch sequencing, the host-resident pipeline and the WAL scan driver. All checksum
+// arithmetic on the batched path runs in the gfx950 kernels of lcrc_kernels.hip; when no device is
+// present every batched call returns LCRC_ENODEV.
+#include <hip/hip_runtime_api.h>
+
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/lcrc.h"
+#include "lcrc_device.h"
+#include "lcrc_math.h"
+
+extern "C" {
+hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
+                               uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
+                               const uint32_t* expected, uint32_t* mismatch, hipStream_t st);
+hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
+                              const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
+                              const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
+                              uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch, hipStream_t st);
+hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
+                                 const uint64_t* offsets, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
+                                 hipStream_t st);
+hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, uint64_t n, const uint32_t* crcs, const uint32_t* mismatch,
+                                  hipStream_t st);
+}
+
+static_assert(sizeof(lcrc_desc) == sizeof(lcrc_desc_dev), "desc layout");
+static_assert(sizeof(lcrc_wal_rec) == sizeof(lcrc_wal_rec_dev), "wal rec layout");
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail_hip(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  if (e == hipErrorOutOfMemory) return LCRC_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorNoBinaryForGpu ||
+      e == hipErrorInvalidDeviceFunction)
+    return LCRC_ENODEV;
+  return LCRC_EHIP;
+}
+
+#define HIPCHK(expr)                                  \
+  do {                                                \
+    hipError_t _e = (expr);                           \
+    if (_e != hipSuccess) return fail_hip(_e, #expr); \
+  } while (0)
+
+// Device buffer that grows on demand (reserve() up front keeps the hot calls allocation-free).
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  int ensure(size_t n) {
+    if (n <= cap) return LCRC_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 1024);
+    HIPCHK(hipMalloc(&p, want * sizeof(T)));
+    cap = want;
+    return LCRC_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct lcrc_ctx {
+  int device = 0;
+  int mode = LCRC_MODE_C;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  uint32_t* d_tab = nullptr;
+  uint32_t init = lcrc::CRC_INIT, xorout = lcrc::CRC_XOROUT, fin4096 = 0;
+  int grid_a = 256, grid_b = 1024;
+  DevBuf<uint32_t> win;       // window partials for the general path
+  DevBuf<uint8_t> chunk[2];   // host-resident pipeline staging
+  DevBuf<uint32_t> hexp[2];   // expected values per chunk
+  hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  DevBuf<uint32_t> wal_counts;
+  DevBuf<uint64_t> wal_offsets;
+  DevBuf<lcrc_desc_dev> wal_descs;
+  DevBuf<uint32_t> wal_crcs, wal_mm;
+};
+
+namespace {
+
+int set_device(lcrc_ctx* ctx) {
+  HIPCHK(hipSetDevice(ctx->device));
+  return LCRC_OK;
+}
+
+hipStream_t pick_stream(lcrc_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+}  // namespace
+
+extern "C" {
+
+const char* lcrc_last_error(void) { return g_last_error.c_str(); }
+const char* lcrc_version(void) { return "lcrc 0.1 (gfx950: k_windows slice4x32-LDS + DPP16 transpose, k_blocks row16)"; }
+
+int lcrc_device_count(int* n) {
+  if (!n) return LCRC_EINVAL;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail_hip(e, "hipGetDeviceCount");
+  }
+  *n = c;
+  return c > 0 ? LCRC_OK : LCRC_ENODEV;
+}
+
+int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
+  if (!out || (mode != LCRC_MODE_REF && mode != LCRC_MODE_C)) return LCRC_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  int rc = lcrc_device_count(&ndev);
+  if (rc != LCRC_OK) return LCRC_ENODEV;
+  if (device < 0 || device >= ndev) return LCRC_EINVAL;
+  lcrc_ctx* ctx = new lcrc_ctx();
+  ctx->device = device;
+  ctx->mode = mode;
+  ctx->flags = flags;
+  auto bail = [&](int code) {
+    lcrc_ctx_destroy(ctx);
+    return code;
+  };
+  if ((rc = set_device(ctx)) != LCRC_OK) return bail(rc);
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) return bail(fail_hip(e, "hipGetDeviceProperties"));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    g_last_error = std::string("kernels are built for gfx950 only; device is ") + prop.gcnArchName;
+    return bail(LCRC_ENODEV);
+  }
+  ctx->grid_a = prop.multiProcessorCount;      // k_windows: 144 KiB LDS -> 1 workgroup per CU
+  ctx->grid_b = prop.multiProcessorCount * 4;  // k_blocks: 40 KiB LDS -> 4 workgroups per CU
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
+    return bail(fail_hip(e, "hipStreamCreate"));
+  if ((e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking)) != hipSuccess)
+    return bail(fail_hip(e, "hipStreamCreate"));
+  if ((e = hipEventCreate(&ctx->t0)) != hipSuccess || (e = hipEventCreate(&ctx->t1)) != hipSuccess)
+    return bail(fail_hip(e, "hipEventCreate"));
+  for (int i = 0; i < 2; ++i)
+    if ((e = hipEventCreateWithFlags(&ctx->ev_copied[i], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming)) != hipSuccess)
+      return bail(fail_hip(e, "hipEventCreate"));
+
+  // constant tables for this mode
+  const uint32_t poly = lcrc::poly_of(mode);
+  std::vector<uint32_t> tab(TAB_TOTAL);
+  lcrc::make_slice_tables(poly, tab.data() + TAB_SLICE, 4);
+  for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 16ull << m, tab.data() + TAB_ZPIECE + m * 1024);
+  for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 256ull << m, tab.data() + TAB_ZWIN + m * 1024);
+  lcrc::make_shift_tables(poly, 4096, tab.data() + TAB_Z4096);
+  if ((e = hipMalloc(&ctx->d_tab, TAB_TOTAL * sizeof(uint32_t))) != hipSuccess) return bail(fail_hip(e, "hipMalloc"));
+  if ((e = hipMemcpy(ctx->d_tab, tab.data(), TAB_TOTAL * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess)
+    return bail(fail_hip(e, "hipMemcpy"));
+  ctx->fin4096 = lcrc::zshift(ctx->init, 4096, poly) ^ ctx->xorout;
+  *out = ctx;
+  return LCRC_OK;
+}
+
+int lcrc_ctx_destroy(lcrc_ctx* ctx) {
+  if (!ctx) return LCRC_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+  ctx->win.release();
+  for (int i = 0; i < 2; ++i) {
+    ctx->chunk[i].release();
+    ctx->hexp[i].release();
+    if (ctx->ev_copied[i]) (void)hipEventDestroy(ctx->ev_copied[i]);
+    if (ctx->ev_done[i]) (void)hipEventDestroy(ctx->ev_done[i]);
+  }
+  ctx->wal_counts.release();
+  ctx->wal_offsets.release();
+  ctx->wal_descs.release();
+  ctx->wal_crcs.release();
+  ctx->wal_mm.release();
+  if (ctx->d_tab) (void)hipFree(ctx->d_tab);
+  if (ctx->t0) (void)hipEventDestroy(ctx->t0);
+  if (ctx->t1) (void)hipEventDestroy(ctx->t1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+  delete ctx;
+  return LCRC_OK;
+}
+
+void* lcrc_ctx_stream(lcrc_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int lcrc_ctx_sync(lcrc_ctx* ctx) {
+  if (!ctx) return LCRC_EINVAL;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return LCRC_OK;
+}
+
+static uint64_t window_words(uint64_t span) { return ((span + 16383) / 16384) * 64; }
+
+int lcrc_ctx_reserve(lcrc_ctx* ctx, uint64_t max_span) {
+  if (!ctx) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return ctx->win.ensure(window_words(max_span));
+}
+
+int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
+               uint32_t* out_crc, uint32_t* out_mismatch, void* stream) {
+  if (!ctx || (n && (!descs || !out_crc || !base))) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  if (out_mismatch && n) HIPCHK(hipMemsetAsync(out_mismatch, 0, ((n + 31) / 32) * sizeof(uint32_t), st));
+  if (n == 0) return LCRC_OK;
+  const bool direct = (ctx->flags & LCRC_FLAG_DIRECT) != 0;
+  const uint32_t* win = nullptr;
+  if (!direct && base_len) {
+    if ((rc = ctx->win.ensure(window_words(base_len))) != LCRC_OK) return rc;
+    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, base, base_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
+                               st));
+    win = ctx->win.p;
+  }
+  HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
+                            ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK, out_crc,
+                            out_mismatch, st));
+  return LCRC_OK;
+}
+
+static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
+                              const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch, hipStream_t st,
+                              bool clear_mismatch) {
+  if (out_mismatch && n && clear_mismatch)
+    HIPCHK(hipMemsetAsync(out_mismatch, 0, ((n + 31) / 32) * sizeof(uint32_t), st));
+  if (n == 0) return LCRC_OK;
+  const uint32_t mflags = ctx->flags & LCRC_FLAG_MASK;
+  if (length == 4096 && stride == 4096) {
+    // single pass: k_windows folds each 4 KiB block and writes the final CRC
+    HIPCHK(lcrc_launch_windows(true, ctx->grid_a, base, (uint64_t)n * 4096, ctx->d_tab, out_crc, n, ctx->fin4096,
+                               mflags, expected, out_mismatch, st));
+    return LCRC_OK;
+  }
+  const uint64_t span = (uint64_t)(n - 1) * stride + length;
+  const uint32_t* win = nullptr;
+  if (!(ctx->flags & LCRC_FLAG_DIRECT) && span) {
+    int rc = ctx->win.ensure(window_words(span));
+    if (rc) return rc;
+    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, base, span, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
+    win = ctx->win.p;
+  }
+  HIPCHK(lcrc_launch_blocks(true, ctx->grid_b, base, span, nullptr, n, stride, length, expected, win, ctx->d_tab,
+                            ctx->init, ctx->xorout, mflags, out_crc, out_mismatch, st));
+  return LCRC_OK;
+}
+
+int lcrc_batch_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
+                       const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch, void* stream) {
+  if (!ctx || (n && (!base || !out_crc))) return LCRC_EINVAL;
+  if (n > 1 && stride < length) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return batch_uniform_impl(ctx, base, n, length, stride, expected, out_crc, out_mismatch, pick_stream(ctx, stream),
+                            true);
+}
+
+int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
+                            const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch, size_t chunk_bytes) {
+  if (!ctx || (n && (!base || !out_crc))) return LCRC_EINVAL;
+  if (n > 1 && stride < length) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  if (n == 0) return LCRC_OK;
+  if (chunk_bytes == 0) chunk_bytes = 64ull << 20;
+  // blocks per chunk: a multiple of 32 so every chunk starts on a mismatch-bitmap word
+  size_t bpc = std::max<size_t>(chunk_bytes / std::max<uint64_t>(stride, 1), 1);
+  bpc = std::max<size_t>(32, bpc / 32 * 32);
+  bpc = std::min(bpc, ((n + 31) / 32) * 32);
+  const uint64_t chunk_span = (uint64_t)(bpc - 1) * stride + length;
+  uint32_t* d_out = nullptr;
+  uint32_t* d_mm = nullptr;
+  const size_t mm_words = (n + 31) / 32;
+  HIPCHK(hipMalloc(&d_out, n * sizeof(uint32_t)));
+  if (out_mismatch) {
+    hipError_t e = hipMalloc(&d_mm, mm_words * sizeof(uint32_t));
+    if (e != hipSuccess) {
+      (void)hipFree(d_out);
+      return fail_hip(e, "hipMalloc");
+    }
+  }
+  int result = LCRC_OK;
+  for (int i = 0; i < 2 && result == LCRC_OK; ++i) {
+    result = ctx->chunk[i].ensure(chunk_span);
+    if (result == LCRC_OK && expected) result = ctx->hexp[i].ensure(bpc);
+  }
+  if (result == LCRC_OK && !(length == 4096 && stride == 4096) && !(ctx->flags & LCRC_FLAG_DIRECT))
+    result = ctx->win.ensure(window_words(chunk_span));
+  if (result == LCRC_OK && d_mm) {
+    hipError_t e = hipMemsetAsync(d_mm, 0, mm_words * sizeof(uint32_t), ctx->stream);
+    if (e != hipSuccess) result = fail_hip(e, "hipMemsetAsync");
+  }
+  const size_t nchunks = (n + bpc - 1) / bpc;
+  for (size_t k = 0; k < nchunks && result == LCRC_OK; ++k) {
+    const int b = (int)(k & 1);
+    const size_t first = k * bpc;
+    const size_t cnt = std::min(bpc, n - first);
+    const uint64_t span = (uint64_t)(cnt - 1) * stride + length;
+    hipError_t e;
+    // the staging buffer is free once the kernel that read it two chunks ago has finished
+    if (k >= 2 && (e = hipStreamWaitEvent(ctx->copy_stream, ctx->ev_done[b], 0)) != hipSuccess) {
+      result = fail_hip(e, "hipStreamWaitEvent");
+      break;
+    }
+    if ((e = hipMemcpyAsync(ctx->chunk[b].p, base + first * stride, span, hipMemcpyHostToDevice,
+                            ctx->copy_stream)) != hipSuccess) {
+      result = fail_hip(e, "hipMemcpyAsync");
+      break;
+    }
+    if (expected && (e = hipMemcpyAsync(ctx->hexp[b].p, expected + first, cnt * sizeof(uint32_t),
+                                        hipMemcpyHostToDevice, ctx->copy_stream)) != hipSuccess) {
+      result = fail_hip(e, "hipMemcpyAsync");
+      break;
+    }
+    if ((e = hipEventRecord(ctx->ev_copied[b], ctx->copy_stream)) != hipSuccess ||
+        (e = hipStreamWaitEvent(ctx->stream, ctx->ev_copied[b], 0)) != hipSuccess) {
+      result = fail_hip(e, "hipEventRecord");
+      break;
+    }
+    result = batch_uniform_impl(ctx, ctx->chunk[b].p, cnt, length, stride, expected ? ctx->hexp[b].p : nullptr,
+                                d_out + first, d_mm ? d_mm + first / 32 : nullptr, ctx->stream, false);
+    if (result == LCRC_OK && (e = hipEventRecord(ctx->ev_done[b], ctx->stream)) != hipSuccess)
+      result = fail_hip(e, "hipEventRecord");
+  }
+  if (result == LCRC_OK) {
+    hipError_t e = hipMemcpyAsync(out_crc, d_out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && d_mm)
+      e = hipMemcpyAsync(out_mismatch, d_mm, mm_words * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) result = fail_hip(e, "D2H");
+  }
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->copy_stream);
+  (void)hipFree(d_out);
+  if (d_mm) (void)hipFree(d_mm);
+  return result;
+}
+
+int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs, size_t max_recs,
+                  size_t* n_recs, void* stream) {
+  if (!ctx || !n_recs || (file_len && !file)) return LCRC_EINVAL;
+  *n_recs = 0;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  const uint64_t nblocks = (file_len + 32767) / 32768;
+  if (nblocks == 0) return LCRC_OK;
+  if ((rc = ctx->wal_counts.ensure(nblocks)) || (rc = ctx->wal_offsets.ensure(nblocks))) return rc;
+  HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, nullptr, nullptr, nullptr, st));
+  std::vector<uint32_t> counts(nblocks);
+  HIPCHK(hipMemcpyAsync(counts.data(), ctx->wal_counts.p, nblocks * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<uint64_t> offs(nblocks);
+  uint64_t total = 0;
+  for (uint64_t b = 0; b < nblocks; ++b) {
+    offs[b] = total;
+    total += counts[b];
+  }
+  *n_recs = total;
+  if (total > max_recs || (total && !recs)) return LCRC_EINVAL;
+  if (total == 0) return LCRC_OK;
+  if ((rc = ctx->wal_descs.ensure(total)) || (rc = ctx->wal_crcs.ensure(total)) ||
+      (rc = ctx->wal_mm.ensure((total + 31) / 32)))
+    return rc;
+  HIPCHK(hipMemcpyAsync(ctx->wal_offsets.p, offs.data(), nblocks * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_offsets.p,
+                               (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, st));
+  const uint32_t saved = ctx->flags;
+  ctx->flags &= ~LCRC_FLAG_MASK;  // the log format stores the raw crc
+  rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->wal_descs.p, total, ctx->wal_crcs.p, ctx->wal_mm.p, st);
+  ctx->flags = saved;
+  if (rc) return rc;
+  HIPCHK(lcrc_launch_wal_finish((lcrc_wal_rec_dev*)recs, total, ctx->wal_crcs.p, ctx->wal_mm.p, st));
+  return LCRC_OK;
+}
+
+// ---- device memory helpers ----
+int lcrc_dev_alloc(int device, size_t bytes, void** out) {
+  if (!out) return LCRC_EINVAL;
+  *out = nullptr;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(out, bytes ? bytes : 1));
+  return LCRC_OK;
+}
+int lcrc_dev_free(void* p) {
+  if (p) HIPCHK(hipFree(p));
+  return LCRC_OK;
+}
+int lcrc_host_alloc_pinned(size_t bytes, void** out) {
+  if (!out) return LCRC_EINVAL;
+  HIPCHK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return LCRC_OK;
+}
+int lcrc_host_free_pinned(void* p) {
+  if (p) HIPCHK(hipHostFree(p));
+  return LCRC_OK;
+}
+int lcrc_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return LCRC_OK;
+}
+int lcrc_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return LCRC_OK;
+}
+int lcrc_memset_d(void* dst, int value, size_t bytes) {
+  HIPCHK(hipMemset(dst, value, bytes));
+  return LCRC_OK;
+}
+int lcrc_device_sync(void) {
+  HIPCHK(hipDeviceSynchronize());
+  return LCRC_OK;
+}
+int lcrc_timer_start(lcrc_ctx* ctx) {
+  if (!ctx) return LCRC_EINVAL;
+  HIPCHK(hipEventRecord(ctx->t0, ctx->stream));
+  return LCRC_OK;
+}
+int lcrc_timer_stop(lcrc_ctx* ctx, float* ms) {
+  if (!ctx || !ms) return LCRC_EINVAL;
+  HIPCHK(hipEventRecord(ctx->t1, ctx->stream));
+  HIPCHK(hipEventSynchronize(ctx->t1));
+  HIPCHK(hipEventElapsedTime(ms, ctx->t0, ctx->t1));
+  return LCRC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,40 @@
+// Layouts shared by the kernels (lcrc_kernels.hip) and the host launcher code (lcrc_api.cpp).
+#pragma once
+#include <stdint.h>
+
+#ifndef LCRC_LOAD_AUX
+#define LCRC_LOAD_AUX 0  // cache-policy bits of the streaming buffer loads (2 = nt)
+#endif
+
+#ifndef LCRC_FLAG_MASK
+#define LCRC_FLAG_MASK 0x1u
+#endif
+
+// Per-mode constant table image (uint32 words), uploaded once per context.
+enum : int {
+  TAB_SLICE = 0,      // T0..T3 slice-by-4, 4 x 256
+  TAB_ZPIECE = 1024,  // Z16, Z32, Z64, Z128 byte-sliced shift tables, 4 x (4 x 256)
+  TAB_ZWIN = 5120,    // Z256, Z512, Z1024, Z2048
+  TAB_Z4096 = 9216,   // Z4096
+  TAB_TOTAL = 10240,
+};
+
+struct lcrc_desc_dev {  // == lcrc_desc
+  uint64_t offset;
+  uint32_t length;
+  int32_t expect_rel;
+};
+#define LCRC_NO_EXPECT_DEV ((int32_t)0x80000000)
+
+struct lcrc_wal_rec_dev {  // == lcrc_wal_rec
+  uint64_t header;
+  uint32_t length;
+  uint8_t type;
+  uint8_t status;
+  uint16_t block_end;
+  uint32_t crc;
+  uint32_t stop;
+};
+#define LCRC_WAL_STOP_TRAILER_DEV 0
+#define LCRC_WAL_STOP_BAD_LENGTH_DEV 1
+#define LCRC_WAL_STOP_ZERO_DEV 2

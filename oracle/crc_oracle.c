@@ -1,0 +1,236 @@
+/*
+ * crc_oracle.c -- TEST INFRASTRUCTURE. CPU restatement of the checksum arithmetic on the leveldb-rust
+ * block/record path. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker or the CPU baseline -- never as the thing measured or shipped.
+ *
+ * What it restates:
+ *  - The reference's checksum is the external crate `crc32fast` ("1.2.0", Cargo.toml:11; source not in
+ *    /root/reference, Cargo.lock git-ignored -> patch version unpinned). crc32fast computes
+ *    CRC-32/ISO-HDLC (reflected poly 0xEDB88320, init 0xFFFFFFFF, xorout 0xFFFFFFFF). Its published
+ *    algorithm: a PCLMULQDQ 4x128-bit folding path on x86 (SSE4.1 + PCLMULQDQ detected at run time),
+ *    otherwise slice-by-16 tables. Call sites: src/db/log.rs:61-64, :261-264, :482-484 (test),
+ *    src/sstable/table.rs:519-522, src/sstable/format.rs:164-166.
+ *  - The masked CRC-32C of the `snap` crate ("1", Cargo.toml:15) framing: CRC-32C (reflected poly
+ *    0x82F63B78) masked as rotr15(crc) + 0xa282ead8 per chunk; snap's x86 path uses the SSE4.2 crc32
+ *    instruction, else slice-by-16.
+ *  - orc_crc_bitwise is the definition, bit by bit (the pinning reference for everything else).
+ *
+ * Parity pinning: the reference's own tests hold no CRC literal. The oracle is pinned
+ * by published check values (CRC-32 "123456789" = 0xCBF43926, CRC-32C = 0xE3069283, RFC 3720 B.4
+ * vectors) and cross-checked against Python's zlib.crc32 (tests/test_oracle.py).
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+#include <pthread.h>
+#include <time.h>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#include <nmmintrin.h>
+#include <wmmintrin.h>
+#endif
+
+#define ORC_POLY_REF 0xEDB88320u
+#define ORC_POLY_C 0x82F63B78u
+
+/* ---- definition: bitwise reflected CRC ---- */
+uint32_t orc_crc_bitwise(uint32_t poly, uint32_t init, uint32_t xorout, const uint8_t* p, size_t n) {
+  uint32_t c = init;
+  for (size_t i = 0; i < n; ++i) {
+    c ^= p[i];
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (poly & (0u - (c & 1u)));
+  }
+  return c ^ xorout;
+}
+
+uint32_t orc_mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
+uint32_t orc_unmask(uint32_t m) {
+  uint32_t rot = m - 0xa282ead8u;
+  return (rot >> 17) | (rot << 15);
+}
+
+/* ---- slice-by-16 (crc32fast's and snap's table fallback) ---- */
+static uint32_t s16_ref[16][256], s16_c[16][256];
+static int s16_ready = 0;
+static void s16_init(void) {
+  if (s16_ready) return;
+  for (int m = 0; m < 2; ++m) {
+    uint32_t(*T)[256] = m ? s16_c : s16_ref;
+    uint32_t poly = m ? ORC_POLY_C : ORC_POLY_REF;
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t c = b;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (poly & (0u - (c & 1u)));
+      T[0][b] = c;
+    }
+    for (int t = 1; t < 16; ++t)
+      for (int b = 0; b < 256; ++b) T[t][b] = (T[t - 1][b] >> 8) ^ T[0][T[t - 1][b] & 0xff];
+  }
+  s16_ready = 1;
+}
+
+/* crc = finalized crc of the previous bytes (0 for none), like Hasher::new_with_initial */
+uint32_t orc_crc_s16(int mode, uint32_t crc, const uint8_t* p, size_t n) {
+  s16_init();
+  uint32_t(*T)[256] = mode ? s16_c : s16_ref;
+  uint32_t c = ~crc;
+  while (n >= 16) {
+    uint32_t w0, w1, w2, w3;
+    memcpy(&w0, p, 4);
+    memcpy(&w1, p + 4, 4);
+    memcpy(&w2, p + 8, 4);
+    memcpy(&w3, p + 12, 4);
+    w0 ^= c;
+    c = T[15][w0 & 0xff] ^ T[14][(w0 >> 8) & 0xff] ^ T[13][(w0 >> 16) & 0xff] ^ T[12][w0 >> 24] ^
+        T[11][w1 & 0xff] ^ T[10][(w1 >> 8) & 0xff] ^ T[9][(w1 >> 16) & 0xff] ^ T[8][w1 >> 24] ^
+        T[7][w2 & 0xff] ^ T[6][(w2 >> 8) & 0xff] ^ T[5][(w2 >> 16) & 0xff] ^ T[4][w2 >> 24] ^
+        T[3][w3 & 0xff] ^ T[2][(w3 >> 8) & 0xff] ^ T[1][(w3 >> 16) & 0xff] ^ T[0][w3 >> 24];
+    p += 16;
+    n -= 16;
+  }
+  while (n--) c = (c >> 8) ^ T[0][(c ^ *p++) & 0xff];
+  return ~c;
+}
+
+#if defined(__x86_64__)
+/* ---- SSE4.2 crc32 instruction (snap's CRC-32C hardware path) ---- */
+__attribute__((target("sse4.2"))) uint32_t orc_crc_sse42(uint32_t crc, const uint8_t* p, size_t n) {
+  uint64_t c = ~crc;
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    c = _mm_crc32_u64(c, v);
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = _mm_crc32_u8((uint32_t)c, *p++);
+  return ~(uint32_t)c;
+}
+
+/* ---- PCLMULQDQ folding for CRC-32/ISO-HDLC (crc32fast's x86 path; Gopal et al., "Fast CRC
+ * computation for generic polynomials using PCLMULQDQ", fold-by-4 then Barrett reduction) ---- */
+#define K1 0x154442bd4ull
+#define K2 0x1c6e41596ull
+#define K3 0x1751997d0ull
+#define K4 0x0ccaa009eull
+#define K5 0x163cd6124ull
+#define P_X 0x1DB710641ull
+#define U_PRIME 0x1F7011641ull
+
+__attribute__((target("sse4.1,pclmul"))) static __m128i fold_16(__m128i x, __m128i data, __m128i k) {
+  __m128i h = _mm_clmulepi64_si128(x, k, 0x11);
+  __m128i l = _mm_clmulepi64_si128(x, k, 0x00);
+  return _mm_xor_si128(_mm_xor_si128(h, l), data);
+}
+
+__attribute__((target("sse4.1,pclmul"))) uint32_t orc_crc_pclmul(uint32_t crc, const uint8_t* p, size_t n) {
+  if (n < 128) return orc_crc_s16(0, crc, p, n);
+  uint32_t c = ~crc;
+  __m128i x0 = _mm_loadu_si128((const __m128i*)(p + 0x00));
+  __m128i x1 = _mm_loadu_si128((const __m128i*)(p + 0x10));
+  __m128i x2 = _mm_loadu_si128((const __m128i*)(p + 0x20));
+  __m128i x3 = _mm_loadu_si128((const __m128i*)(p + 0x30));
+  x0 = _mm_xor_si128(x0, _mm_cvtsi32_si128((int)c));
+  p += 64;
+  n -= 64;
+  __m128i k = _mm_set_epi64x((long long)K2, (long long)K1);
+  while (n >= 64) {
+    x0 = fold_16(x0, _mm_loadu_si128((const __m128i*)(p + 0x00)), k);
+    x1 = fold_16(x1, _mm_loadu_si128((const __m128i*)(p + 0x10)), k);
+    x2 = fold_16(x2, _mm_loadu_si128((const __m128i*)(p + 0x20)), k);
+    x3 = fold_16(x3, _mm_loadu_si128((const __m128i*)(p + 0x30)), k);
+    p += 64;
+    n -= 64;
+  }
+  k = _mm_set_epi64x((long long)K4, (long long)K3);
+  __m128i x = fold_16(x0, x1, k);
+  x = fold_16(x, x2, k);
+  x = fold_16(x, x3, k);
+  while (n >= 16) {
+    x = fold_16(x, _mm_loadu_si128((const __m128i*)p), k);
+    p += 16;
+    n -= 16;
+  }
+  /* 128 -> 64 bits */
+  const __m128i lo32 = _mm_set_epi32(0, 0, 0, -1);
+  x = _mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x10), _mm_srli_si128(x, 8));
+  x = _mm_xor_si128(_mm_clmulepi64_si128(_mm_and_si128(x, lo32), _mm_set_epi64x(0, (long long)K5), 0x00),
+                    _mm_srli_si128(x, 4));
+  /* Barrett reduction 64 -> 32 */
+  const __m128i pu = _mm_set_epi64x((long long)U_PRIME, (long long)P_X);
+  __m128i t1 = _mm_clmulepi64_si128(_mm_and_si128(x, lo32), pu, 0x10);
+  __m128i t2 = _mm_clmulepi64_si128(_mm_and_si128(t1, lo32), pu, 0x00);
+  c = (uint32_t)_mm_extract_epi32(_mm_xor_si128(x, t2), 1);
+  return orc_crc_s16(0, ~c, p, n);
+}
+#else
+uint32_t orc_crc_sse42(uint32_t crc, const uint8_t* p, size_t n) { return orc_crc_s16(1, crc, p, n); }
+uint32_t orc_crc_pclmul(uint32_t crc, const uint8_t* p, size_t n) { return orc_crc_s16(0, crc, p, n); }
+#endif
+
+/* ---- per-block batch (for golden vectors and the CPU baseline) ---- */
+/* algo: 0 = bitwise REF, 1 = bitwise C, 2 = slice16 REF, 3 = slice16 C, 4 = pclmul REF, 5 = sse42 C */
+static uint32_t crc_algo(int algo, const uint8_t* p, size_t n) {
+  switch (algo) {
+    case 0: return orc_crc_bitwise(ORC_POLY_REF, 0xFFFFFFFFu, 0xFFFFFFFFu, p, n);
+    case 1: return orc_crc_bitwise(ORC_POLY_C, 0xFFFFFFFFu, 0xFFFFFFFFu, p, n);
+    case 2: return orc_crc_s16(0, 0, p, n);
+    case 3: return orc_crc_s16(1, 0, p, n);
+    case 4: return orc_crc_pclmul(0, p, n);
+    default: return orc_crc_sse42(0, p, n);
+  }
+}
+
+/* CRC of ranges [offs[i], offs[i]+lens[i]) of base */
+void orc_crc_ranges(int algo, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, size_t n, uint32_t* out) {
+  for (size_t i = 0; i < n; ++i) out[i] = crc_algo(algo, base + offs[i], lens[i]);
+}
+
+typedef struct {
+  int algo;
+  const uint8_t* base;
+  size_t first, count, blen, stride;
+  uint32_t* out;
+} job_t;
+
+static void* run_job(void* a) {
+  job_t* j = (job_t*)a;
+  for (size_t i = 0; i < j->count; ++i) j->out[j->first + i] = crc_algo(j->algo, j->base + (j->first + i) * j->stride, j->blen);
+  return 0;
+}
+
+/* Uniform blocks with `threads` POSIX threads, blocks partitioned evenly; returns wall seconds. */
+double orc_crc_uniform_mt(int algo, const uint8_t* base, size_t nblocks, size_t blen, size_t stride, int threads,
+                          uint32_t* out) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  job_t jobs[256];
+  s16_init(); /* tables built before any thread reads them */
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  size_t per = nblocks / (size_t)threads, rem = nblocks % (size_t)threads, first = 0;
+  for (int t = 0; t < threads; ++t) {
+    size_t cnt = per + ((size_t)t < rem ? 1 : 0);
+    jobs[t] = (job_t){algo, base, first, cnt, blen, stride, out};
+    first += cnt;
+    pthread_create(&th[t], 0, run_job, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* splitmix64 byte stream (SURVEY.md 8c/8d synthetic inputs): s += 0x9E3779B97F4A7C15, mix, 8 LE bytes */
+void orc_splitmix_fill(uint64_t seed, uint8_t* out, size_t n) {
+  uint64_t s = seed;
+  size_t i = 0;
+  while (i < n) {
+    s += 0x9E3779B97F4A7C15ull;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    for (int k = 0; k < 8 && i < n; ++k, ++i) out[i] = (uint8_t)(z >> (8 * k));
+  }
+}

@@ -1,0 +1,84 @@
+"""C ABI: the library loads, exports every symbol include/lcrc.h declares, the scalar host API (the
+crc32fast::Hasher drop-in) agrees with the oracle, and batched calls fail loudly without a device."""
+import os
+import re
+import zlib
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    with open(os.path.join(ROOT, "include", "lcrc.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(lcrc\w*)\s*\(", src))
+    return sorted(names)
+
+
+def test_exports_every_declared_symbol(lcrc):
+    L = lcrc.lib()
+    declared = _header_functions()
+    assert len(declared) >= 30
+    for name in declared:
+        assert hasattr(L, name), f"{name} declared in include/lcrc.h but not exported"
+    assert sorted(lcrc.ABI_SYMBOLS) == declared
+
+
+def test_kernel_image_is_gfx950(lcrc):
+    with open(lcrc.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle entry of the code object
+
+
+def test_struct_layouts(lcrc):
+    assert lcrc.DESC_DTYPE.itemsize == 16
+    assert lcrc.WAL_REC_DTYPE.itemsize == 24
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 7, 8, 9, 16, 100, 4096, 100003])
+def test_scalar_value(lcrc, orc, n):
+    d = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    assert lcrc.value(d) == zlib.crc32(d) == orc.crc(d, 0)
+    assert lcrc.crc32c_value(d) == orc.crc_bitwise(d, 1)
+    assert lcrc.lib().lcrc32_value(d, len(d)) == zlib.crc32(d)
+    assert lcrc.lib().lcrc32c_value(d, len(d)) == orc.crc(d, 1)
+
+
+def test_hasher_mirrors_crc32fast(lcrc):
+    # Hasher::new(); update([type]); update(data); finalize()  (log.rs:61-64)
+    h = lcrc.Hasher()
+    h.update(bytes([1]))
+    h.update(b"foo")
+    assert h.finalize() == zlib.crc32(b"\x01foo") == 0xEACA044A
+    assert h.amount == 4
+    h2 = lcrc.Hasher.new_with_initial(zlib.crc32(b"\x01f"))
+    h2.update(b"oo")
+    assert h2.finalize() == 0xEACA044A
+    assert lcrc.Hasher().finalize() == 0
+
+
+def test_extend_and_combine(lcrc, orc):
+    d = np.random.default_rng(5).integers(0, 256, 9000, dtype=np.uint8).tobytes()
+    for mode in (lcrc.MODE_REF, lcrc.MODE_C):
+        full = orc.crc(d, mode)
+        for cut in (0, 1, 4096, 8999, 9000):
+            a, b = d[:cut], d[cut:]
+            assert lcrc.extend(lcrc.value(a, mode), b, mode) == full
+            assert lcrc.combine(lcrc.value(a, mode), lcrc.value(b, mode), len(b), mode) == full
+
+
+def test_mask(lcrc, orc):
+    for v in (0, 1, 0xFFFFFFFF, 0xE3069283, 0xDEADBEEF):
+        assert lcrc.mask(v) == orc.mask(v)
+        assert lcrc.unmask(lcrc.mask(v)) == v
+
+
+def test_batched_api_fails_loudly_without_device(lcrc):
+    if lcrc.device_count() > 0:
+        pytest.skip("device present")
+    with pytest.raises(lcrc.NoDeviceError):
+        lcrc.Engine(0, lcrc.MODE_C)
+    assert lcrc.lib().lcrc_batch(None, None, 0, None, 0, None, None, None) == lcrc.EINVAL

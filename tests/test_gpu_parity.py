@@ -1,0 +1,212 @@
+"""Device parity: every batched path on the gfx950 kernels against the CPU oracle, bit-exact.
+Run on the MI355X box with `pytest -m gpu`."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import logtests
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+MODES = [0, 1]
+
+
+def _gold(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def _uniform(lcrc, eng, data, n, length, stride, expected=None):
+    base = lcrc.DeviceBuffer.from_host(data)
+    out = lcrc.DeviceBuffer(max(4 * n, 4))
+    mm = lcrc.DeviceBuffer(max(4 * ((n + 31) // 32), 4))
+    exp = lcrc.DeviceBuffer.from_host(np.asarray(expected, np.uint32)) if expected is not None else None
+    eng.batch_uniform(base, n, length, stride, out, expected=exp, out_mismatch=mm)
+    eng.sync()
+    return out.download(np.uint32, n), lcrc.unpack_bits(mm.download(np.uint32, (n + 31) // 32), n)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_config1_golden_fast_path(lcrc, orc, engines, mode):
+    g = _gold("config1_golden.json")
+    data = orc.splitmix_bytes(g["seed"], g["nblocks"] * g["block_len"])
+    got, mm = _uniform(lcrc, engines[mode], data, 1024, 4096, 4096)
+    want = [int(x, 16) for x in g["crc_c" if mode else "crc_ref"]]
+    assert got.tolist() == want
+    assert not mm.any()
+
+
+def test_config1_masked_and_verify(lcrc, orc):
+    g = _gold("config1_golden.json")
+    data = orc.splitmix_bytes(g["seed"], g["nblocks"] * g["block_len"])
+    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
+    exp = np.array([int(x, 16) for x in g["crc_c_masked"]], np.uint32)
+    bad = [0, 5, 31, 32, 1023]
+    exp2 = exp.copy()
+    exp2[bad] ^= 1
+    got, mm = _uniform(lcrc, eng, data, 1024, 4096, 4096, exp2)
+    assert np.array_equal(got, exp)
+    assert np.nonzero(mm)[0].tolist() == bad
+    eng.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_config2_full_size(lcrc, orc, engines, mode):
+    """64K x 4 KiB (BASELINE configs[1]) -- every CRC against the oracle."""
+    n = 65536
+    data = orc.splitmix_bytes(0x5EED0001, n * 4096)
+    got, _ = _uniform(lcrc, engines[mode], data, n, 4096, 4096)
+    want = orc.crc_ranges(data, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096), mode)
+    assert np.array_equal(got, want)
+    # size-independent property: xor of all block crcs
+    assert int(np.bitwise_xor.reduce(got)) == int(np.bitwise_xor.reduce(want))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 63, 64, 65, 1000, 4097])
+def test_fast_path_ragged_counts(lcrc, orc, engines, n):
+    data = orc.splitmix_bytes(n, n * 4096)
+    for mode in MODES:
+        got, _ = _uniform(lcrc, engines[mode], data, n, 4096, 4096)
+        assert np.array_equal(got, orc.crc_ranges(data, np.arange(n) * 4096, np.full(n, 4096), mode))
+
+
+@pytest.mark.parametrize("length,stride", [(1, 1), (1, 7), (3, 5), (16, 16), (100, 105), (255, 256), (256, 256),
+                                           (257, 300), (4095, 4100), (4096, 4101), (4097, 4097), (8192, 8192),
+                                           (20000, 20005), (65536, 65536)])
+def test_uniform_general(lcrc, orc, engines, length, stride):
+    n = max(1, min(3000, (4 << 20) // stride))
+    data = orc.splitmix_bytes(length * 31 + stride, (n - 1) * stride + length)
+    for mode in MODES:
+        got, _ = _uniform(lcrc, engines[mode], data, n, length, stride)
+        want = orc.crc_ranges(data, np.arange(n, dtype=np.uint64) * stride, np.full(n, length), mode)
+        assert np.array_equal(got, want), (mode, np.nonzero(got != want)[0][:10])
+
+
+def test_ranges_golden(lcrc, orc, engines):
+    g = _gold("ranges_golden.json")
+    data = orc.splitmix_bytes(g["seed"], g["buffer_len"])
+    offs = [r["offset"] for r in g["ranges"]]
+    lens = [r["length"] for r in g["ranges"]]
+    for mode, key in ((0, "crc_ref"), (1, "crc_c")):
+        crcs, _ = engines[mode].crc_ranges(data, offs, lens)
+        assert [f"{v:08x}" for v in crcs] == [r[key] for r in g["ranges"]]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_ranges(lcrc, orc, engines, seed):
+    rng = np.random.default_rng(seed)
+    total = 3 << 20
+    data = orc.splitmix_bytes(1000 + seed, total)
+    n = 3000
+    lens = np.minimum(rng.integers(0, 1 << rng.integers(1, 18, n)), total).astype(np.uint32)
+    offs = np.array([int(rng.integers(0, total - l + 1)) for l in lens], np.uint64)  # overlapping, unsorted
+    for mode in MODES:
+        crcs, _ = engines[mode].crc_ranges(data, offs, lens)
+        want = orc.crc_ranges(data, offs, lens, mode)
+        assert np.array_equal(crcs, want), np.nonzero(crcs != want)[0][:10]
+
+
+def test_direct_mode_matches(lcrc, orc):
+    rng = np.random.default_rng(9)
+    data = orc.splitmix_bytes(77, 1 << 20)
+    lens = rng.integers(0, 20000, 500).astype(np.uint32)
+    offs = np.array([int(rng.integers(0, (1 << 20) - l + 1)) for l in lens], np.uint64)
+    for mode in MODES:
+        eng = lcrc.Engine(0, mode, lcrc.FLAG_DIRECT)
+        crcs, _ = eng.crc_ranges(data, offs, lens)
+        assert np.array_equal(crcs, orc.crc_ranges(data, offs, lens, mode))
+        eng.close()
+
+
+def test_edges_at_buffer_bounds(lcrc, orc, engines):
+    data = orc.splitmix_bytes(5, 70000)
+    offs, lens = [], []
+    for l in range(0, 40):
+        offs += [0, 70000 - l]
+        lens += [l, l]
+    offs += [1, 15, 16, 17, 69999]
+    lens += [69999, 100, 69984, 5000, 1]
+    for mode in MODES:
+        crcs, _ = engines[mode].crc_ranges(data, offs, lens)
+        assert np.array_equal(crcs, orc.crc_ranges(data, offs, lens, mode))
+
+
+def _sstable(lcrc, orc, seed, nblocks):
+    rng = np.random.default_rng(seed)
+    t = lcrc.TableFile()
+    handles = []
+    for _ in range(nblocks):
+        n = int(rng.integers(0, 70000)) if rng.random() < 0.3 else int(rng.integers(3000, 5000))
+        handles.append(t.write_raw_block(rng.integers(0, 256, n, dtype=np.uint8).tobytes(), int(rng.integers(0, 2))))
+    return bytearray(t.contents()), handles
+
+
+def test_sstable_verify_batch(lcrc, orc, engines):
+    """Batched read_block_from_file verify (format.rs:162-171): desc {off, n+1, expect_rel n+1}."""
+    f, handles = _sstable(lcrc, orc, 3, 400)
+    bad = [0, 17, 200, 399]
+    for i in bad:
+        off, size = handles[i]
+        f[off + size // 2 if size else off] ^= 0x10  # corrupt content (or the type byte of an empty block)
+    offs = [h[0] for h in handles]
+    lens = [h[1] + 1 for h in handles]
+    crcs, mm = engines[0].crc_ranges(np.frombuffer(bytes(f), np.uint8), offs, lens, expect_rel=np.array(lens))
+    assert np.nonzero(mm)[0].tolist() == bad
+    assert np.array_equal(crcs, orc.crc_ranges(bytes(f), offs, lens, 0))
+    for i in range(len(handles)):
+        _, err = lcrc.TableFile.read_block(bytes(f), handles[i][0], handles[i][1], True)
+        assert (err == "block checksum mismatch") == (i in bad) or err == "bad block type"
+
+
+@pytest.mark.parametrize("length,stride", [(4096, 4096), (1000, 1024), (4096, 4101)])
+def test_host_resident_pipeline(lcrc, orc, engines, length, stride):
+    n = 20000
+    data = orc.splitmix_bytes(length + stride, (n - 1) * stride + length)
+    want = orc.crc_ranges(data, np.arange(n, dtype=np.uint64) * stride, np.full(n, length), 1)
+    exp = want.copy()
+    exp[[3, 9999]] ^= 0xFF
+    got, mm = engines[1].batch_host_uniform(data, n, length, stride, expected=exp, chunk_bytes=8 << 20)
+    assert np.array_equal(got, want)
+    assert np.nonzero(lcrc.unpack_bits(mm, n))[0].tolist() == [3, 9999]
+
+
+# ---- WAL path -------------------------------------------------------------------------------------
+def _batch_reader(lcrc, engines):
+    return lambda data: lcrc.BatchLogReader(data, engines[0])
+
+
+@pytest.mark.parametrize("scenario", [s for s in logtests.SCENARIOS], ids=lambda f: f.__name__)
+def test_wal_reference_scenarios_on_device(lcrc, engines, scenario):
+    scenario(logtests.Tester(lcrc, _batch_reader(lcrc, engines)))
+
+
+def test_wal_random_read_on_device(lcrc, engines):
+    logtests.t_random_read(logtests.Tester(lcrc, _batch_reader(lcrc, engines)), np.random.default_rng(5))
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_wal_batch_equals_host_reader_under_corruption(lcrc, orc, engines, seed):
+    rng = np.random.default_rng(500 + seed)
+    recs = []
+    for _ in range(400):
+        k = int(rng.integers(1, 17))
+        recs.append(rng.integers(0, 256, int(rng.integers(0, 1 << k)), dtype=np.uint8).tobytes())
+    data = bytearray(orc.log_write(recs))
+    for _ in range(int(rng.integers(0, 8))):
+        pos = int(rng.integers(0, len(data)))
+        data[pos] ^= 1 << int(rng.integers(0, 8))
+    if rng.random() < 0.5:
+        del data[len(data) - int(rng.integers(1, 200)):]
+    b = lcrc.BatchLogReader(bytes(data), engines[0])
+    got = (b.records(), b.dropped_bytes, b.report_message)
+    assert b.consistency_errors == 0
+    assert got == orc.log_read_all(bytes(data))
+    # per-record device crcs equal the oracle over type ++ payload
+    sc = b.records_scanned
+    for r in sc[:: max(1, len(sc) // 50)]:
+        h = int(r["header"])
+        body = bytes(data[h + 6:h + 7 + int(r["length"])])
+        assert int(r["crc"]) == orc.crc(body, 0)
+        assert int(r["status"]) == (int.from_bytes(data[h:h + 4], "little") != orc.crc(body, 0))
