@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "liblcrc.so")
+LIB_PATH = os.environ.get("LCRC_LIB_PATH") or os.path.join(_HERE, "_build", "liblcrc.so")
 
 MODE_REF = 0  # CRC-32/ISO-HDLC (crc32fast)
 MODE_C = 1  # CRC-32C

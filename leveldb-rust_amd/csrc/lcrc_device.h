@@ -3,7 +3,7 @@
 #include <stdint.h>
 
 #ifndef LCRC_LOAD_AUX
-#define LCRC_LOAD_AUX 0  // cache-policy bits of the streaming buffer loads (2 = nt)
+#define LCRC_LOAD_AUX 2  // cache-policy bits of the streaming buffer loads: 2 = nt (read-once stream)
 #endif
 
 #ifndef LCRC_FLAG_MASK

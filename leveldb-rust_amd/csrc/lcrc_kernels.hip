@@ -28,21 +28,32 @@ typedef u32x4 u32x4_ua __attribute__((aligned(1)));
 namespace lcrc_dev {
 
 // ---------------------------------------------------------------------------------------------------
-// k_windows LDS image (static, 144 KiB -> one 1024-thread workgroup per CU):
+// k_windows LDS image (static, 152 KiB -> one 1024-thread workgroup per CU):
 //   [0, 128 KiB): slice-by-4 tables T0..T3, 256 entries each, 32 replicas. Table t lives in region
 //                 t>>1 (64 KiB each); entry e of that region is a 256 B row holding table 2*region's
 //                 32 replicas in its first 128 B and table 2*region+1's in the second. Lane l reads
 //                 replica l&31 -> bank (l&31): the 32 lanes of each ds_read_b32 half-wave group never
 //                 conflict. The byte address of (t, e, l) = (t>>1)<<16 | e<<8 | (t&1)<<7 | (l&31)<<2,
 //                 built with ONE v_perm_b32 from a per-lane base and the data byte.
-//   [128 KiB, 144 KiB): Z256, Z512, Z1024, Z2048 byte-sliced shift tables (unreplicated, tree only).
-//   [144 KiB, 148 KiB): Z128 (joins the two 128 B chains of a window).
+//   [128 KiB, 152 KiB): byte-sliced shift tables Z64 (chain join), Z128 .. Z2048 (window tree),
+//                 unreplicated: they serve a few lookups per tile.
 // ---------------------------------------------------------------------------------------------------
 constexpr int A_SLICE_BYTES = 131072;
-constexpr int A_TREE_BYTES = 16384;
-constexpr int A_LDS_BYTES = A_SLICE_BYTES + A_TREE_BYTES + 4096;  // + Z128 (chain join)
-constexpr int A_THREADS = 1024;
-constexpr int TILE = 16384;  // bytes per wave tile (16 loads x 64 lanes x 16 B)
+constexpr int A_Z64 = A_SLICE_BYTES;       // Z64, then Z128, Z256, Z512, Z1024, Z2048 at +4 KiB steps
+constexpr int A_ZTREE = A_Z64 + 4096;      // Z128 .. Z2048: level m of the tree shifts 128 << m bytes
+constexpr int A_LDS_BYTES = A_Z64 + 6 * 4096;
+#ifndef LCRC_A_THREADS
+#define LCRC_A_THREADS 1024
+#endif
+constexpr int A_THREADS = LCRC_A_THREADS;
+constexpr int TILE = 8192;  // bytes per wave tile (8 loads x 64 lanes x 16 B)
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt(0)) but not for its
+// outstanding global loads -- __syncthreads() would add vmcnt(0) and expose the first tile's latency.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
 
 __device__ __forceinline__ uint32_t lds_u32(const void* lds_base, uint32_t byte_addr) {
   return *(const uint32_t*)((const char*)lds_base + byte_addr);
@@ -55,40 +66,43 @@ __device__ __forceinline__ uint32_t tab_addr(uint32_t base, uint32_t x) {
   return __builtin_amdgcn_perm(base, x, 0x0C060004u | (K << 8));
 }
 
-// one slice-by-4 step: r <- walk(r, 4 bytes w)
-__device__ __forceinline__ uint32_t step4_rep(const void* L, uint32_t r, uint32_t w, uint32_t b0, uint32_t b1,
-                                              uint32_t b2, uint32_t b3) {
-  uint32_t x = r ^ w;
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); gfx9 has no v_xor3
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// one slice-by-4 step on x = r ^ w (already folded); returns walk(r, w) ^ w_next
+__device__ __forceinline__ uint32_t step4x(const void* L, uint32_t x, uint32_t w_next, uint32_t b0, uint32_t b1,
+                                           uint32_t b2, uint32_t b3) {
   uint32_t t3 = lds_u32(L, tab_addr<0>(b3, x));
   uint32_t t2 = lds_u32(L, tab_addr<1>(b2, x));
   uint32_t t1 = lds_u32(L, tab_addr<2>(b1, x));
   uint32_t t0 = lds_u32(L, tab_addr<3>(b0, x));
-  return t0 ^ t1 ^ t2 ^ t3;
+  return xor3(xor3(t0, t1, w_next), t2, t3);
 }
 
-// In-register transpose. Lane l = 4*c + k (k = l & 3, c = l >> 2) loads, in instruction j, the 16 B
-// piece at tile byte 1024*j + 256*k + 16*c (each instruction still reads one contiguous 1 KiB). Within
-// each group k the 16 lanes c and 16 registers j form a 16x16 matrix of pieces; transposing it gives
-// lane (k, c) the pieces 1024*c + 256*k + 16*j', j' = 0..15: one contiguous 256 B window whose index
-// inside the tile is 4*c + k = l. The four butterfly stages run over lane bits 2..5:
-//   bit 2, bit 3: v_mov_b32_dpp row_shr/row_shl with a bank_mask -- disabled banks keep `old`, so the
-//                 DPP move is also the select (one instruction per register)
-//   bit 4: v_permlane16_swap (odd rows of a <-> even rows of b), bit 5: v_permlane32_swap
-//          (one instruction per register pair)
+// In-register transpose. Lane l = 8*c + k (k = l & 7, c = l >> 3) loads, in instruction j, the 16 B piece
+// at tile byte 1024*j + 128*k + 16*c (each instruction still reads one contiguous 1 KiB). Within each group
+// k the 8 lanes c and 8 registers j form an 8x8 matrix of pieces; transposing it gives lane (k, c) the
+// pieces at 1024*c + 128*k + 16*j', j' = 0..7: one contiguous 128 B window whose index inside the tile is
+// 8*c + k = l. The three butterfly stages run over lane bits 3..5:
+//   bit 3: v_mov_b32_dpp row_shr:8 / row_shl:8 with a bank_mask -- disabled banks keep `old`, so the DPP
+//          move is also the select (one instruction per register)
+//   bit 4: v_permlane16_swap (odd rows of a <-> even rows of b), bit 5: v_permlane32_swap (one
+//          instruction per register pair)
 template <int LB>
-__device__ __forceinline__ void transpose_stage(u32x4 (&v)[16]) {
-  constexpr int D = 1 << (LB - 2);  // register-index bit paired with lane bit LB
+__device__ __forceinline__ void transpose_stage(u32x4 (&v)[8]) {
+  constexpr int D = 1 << (LB - 3);  // register-index bit paired with lane bit LB
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < 8; ++j) {
     if (j & D) continue;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       uint32_t a = v[j][q], b = v[j + D][q];
-      if constexpr (LB == 2 || LB == 3) {
-        constexpr int S = 1 << LB;                            // lane distance 4 or 8
-        constexpr int HI = (LB == 2) ? 0xA : 0xC;             // banks whose lanes have bit LB set
-        uint32_t na = (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)b, 0x110 + S, 0xF, HI, false);
-        uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)a, 0x100 + S, 0xF, HI ^ 0xF, false);
+      if constexpr (LB == 3) {
+        // lanes 8..15 of each row (banks 2, 3) have bit 3 set
+        uint32_t na = (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)b, 0x118, 0xF, 0xC, false);
+        uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)a, 0x108, 0xF, 0x3, false);
         v[j][q] = na;
         v[j + D][q] = nb;
       } else if constexpr (LB == 4) {
@@ -110,12 +124,17 @@ __device__ __forceinline__ uint32_t zlook(const void* L, uint32_t tab_byte_off, 
          *(const uint32_t*)(z + 2048 + (((r >> 16) & 0xff) << 2)) ^ *(const uint32_t*)(z + 3072 + ((r >> 24) << 2));
 }
 
-// one level of the in-row window tree of k_windows: lane g (g % 2^(M+1) == 0) <- Z_{256*2^M}(p_g) ^ p_{g+2^M}
+// one level of the window tree: lane g (g % 2^(M+1) == 0) <- Z_{128*2^M}(p_g) ^ p_{g+2^M}. Only the
+// combining lanes look up (exec-masked ds_reads: fewer bank conflicts on the unreplicated tables).
 template <int M>
 __device__ __forceinline__ uint32_t tree_level(const void* L, uint32_t p, uint32_t lane) {
-  const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x100 + (1 << M), 0xF, 0xF, false);
-  const uint32_t sh = zlook(L, 131072 + M * 4096, p);
-  return ((lane & ((2u << M) - 1)) == 0) ? (sh ^ pn) : p;
+  uint32_t pn;
+  if constexpr (M < 4)
+    pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x100 + (1 << M), 0xF, 0xF, false);  // row_shl
+  else
+    pn = __shfl_down(p, 1 << M, 64);
+  if ((lane & ((2u << M) - 1)) == 0) p = zlook(L, A_ZTREE + M * 4096, p) ^ pn;
+  return p;
 }
 
 __device__ __forceinline__ uint32_t mask32c(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
@@ -123,22 +142,101 @@ __device__ __forceinline__ uint32_t mask32c(uint32_t crc) { return ((crc >> 15) 
 // wave-uniform descriptor for tile t: loads past the end of the span (or of a non-existent tile) return 0
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const uint8_t* base, uint64_t span, uint64_t t,
                                                             uint64_t ntiles) {
-  const uint64_t toff = t * (uint64_t)TILE;
   uint32_t nrec = 0;
+  uint64_t toff = 0;
+#ifdef LCRC_PROBE_NOLOAD  // ablation build: no memory traffic, loads return zeros
+  ntiles = 0;
+#endif
   if (t < ntiles) {
+#ifdef LCRC_PROBE_L2  // ablation build: every tile aliases one of the first 64 (512 KiB, L2-resident)
+    toff = (t & 63) * (uint64_t)TILE;
+#else
+    toff = t * (uint64_t)TILE;
+#endif
     const uint64_t rem = span - toff;
     nrec = rem < (uint64_t)TILE ? (uint32_t)rem : (uint32_t)TILE;
   }
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (t < ntiles ? toff : 0)), (short)0, (int)nrec, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + toff), (short)0, (int)nrec, 0x00020000);
 }
 
-template <int AUX>
-__device__ __forceinline__ u32x4 load_piece(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int j) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rs, voff + j * 1024, 0, AUX);
+#ifdef LCRC_PROBE_LDSDATA  // ablation build: random data from an 8 KiB LDS tile, no VMEM at all
+__shared__ u32x4 lcrc_probe_tile[512];
+#define LCRC_REFILL(rs, off) (lcrc_probe_tile[((off) >> 4) & 511])
+#else
+#define LCRC_REFILL(rs, off) __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LCRC_LOAD_AUX)
+#endif
+
+__device__ __forceinline__ void load_tile(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j * 1024);
 }
 
-// FINAL = false: out_win[t*64 + w] = walk(0, window w of tile t), w = 4*c + r (window at tile byte 256*w)
+// Transpose + walk one tile already in registers; returns walk(0, window l) of this lane (128 B).
+// As each register pair is consumed it is refilled from `rs` (the tile after next), so every wave keeps
+// between one and two tiles of loads in flight while it computes.
+__device__ __forceinline__ uint32_t walk_tile(const void* L, u32x4 (&v)[8], uint32_t b0, uint32_t b1, uint32_t b2,
+                                              uint32_t b3, __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+  transpose_stage<3>(v);
+  transpose_stage<4>(v);
+  transpose_stage<5>(v);
+#ifdef LCRC_PROBE_NOWALK  // ablation build: fold the data with xor only
+  uint32_t p = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    p ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+    v[j] = LCRC_REFILL(rs, voff + j * 1024);
+  }
+  return p;
+#else
+  // two independent chains over the 64 B halves (pieces 0..3 and 4..7); x carries the chain register
+  // already xored with its next data word
+  uint32_t xa = v[0].x, xb = v[4].x;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    xa = step4x(L, xa, v[j].y, b0, b1, b2, b3);
+    xb = step4x(L, xb, v[4 + j].y, b0, b1, b2, b3);
+    xa = step4x(L, xa, v[j].z, b0, b1, b2, b3);
+    xb = step4x(L, xb, v[4 + j].z, b0, b1, b2, b3);
+    xa = step4x(L, xa, v[j].w, b0, b1, b2, b3);
+    xb = step4x(L, xb, v[4 + j].w, b0, b1, b2, b3);
+    xa = step4x(L, xa, j < 3 ? v[j + 1].x : 0u, b0, b1, b2, b3);
+    xb = step4x(L, xb, j < 3 ? v[5 + j].x : 0u, b0, b1, b2, b3);
+    v[j] = LCRC_REFILL(rs, voff + j * 1024);
+    v[4 + j] = LCRC_REFILL(rs, voff + (4 + j) * 1024);
+    __builtin_amdgcn_sched_barrier(0);  // keep the refill here: hipcc would otherwise sink it past the walk
+  }
+  return zlook(L, A_Z64, xa) ^ xb;
+#endif
+}
+
+// FINAL = false: out[t*32 + w] = walk(0, 256 B window w of tile t) (raw partials for k_blocks)
 // FINAL = true : span = nblk * 4096; out[b] = crc of 4 KiB block b (xor fin, optional mask, verify)
+template <bool FINAL>
+__device__ __forceinline__ void finish_tile(const void* L, uint32_t p, uint64_t t, uint32_t lane,
+                                           uint32_t* __restrict__ out, uint64_t nblk, uint32_t fin, uint32_t flags,
+                                           const uint32_t* __restrict__ expected, uint32_t* __restrict__ mismatch) {
+  p = tree_level<0>(L, p, lane);  // 128 B windows -> 256 B windows
+  if (!FINAL) {
+    if ((lane & 1) == 0) out[t * 32 + (lane >> 1)] = p;
+    return;
+  }
+  p = tree_level<1>(L, p, lane);
+  p = tree_level<2>(L, p, lane);
+  p = tree_level<3>(L, p, lane);
+  p = tree_level<4>(L, p, lane);
+  const uint64_t blk = t * 2 + (lane >> 5);
+  if ((lane & 31) == 0 && blk < nblk) {
+    uint32_t crc = p ^ fin;
+    if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
+    out[blk] = crc;
+    if (expected && expected[blk] != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
+  }
+}
+
+#ifdef LCRC_PROBE_CLOCK  // diagnostic build: per-workgroup shader/real clock stamps around the tile loop
+__device__ unsigned long long lcrc_dbg_clock[4096];
+#endif
+
 template <bool FINAL>
 __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict__ base, uint64_t span,
                                                       uint64_t ntiles, const uint32_t* __restrict__ gtab,
@@ -150,83 +248,79 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * (A_THREADS / 64);
   uint64_t t = (uint64_t)blockIdx.x * (A_THREADS / 64) + wave;
-
-  // lane (k, c) = (lane & 3, lane >> 2) reads piece 16*k + c of every 1 KiB of the tile
-  const uint32_t voff = 16u * (16u * (lane & 3) + (lane >> 2));
-  u32x4 v[16];
-  {
-    // issue the first tile's loads before building the LDS tables so HBM streams during the fill
-    __amdgpu_buffer_rsrc_t rs = tile_rsrc(base, span, t, ntiles);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = load_piece<LCRC_LOAD_AUX>(rs, voff, j);
-  }
-
-  {
-    const uint32_t* gs = gtab + TAB_SLICE;
-    for (uint32_t i = threadIdx.x; i < A_SLICE_BYTES / 16; i += A_THREADS) {
-      const uint32_t off = i << 4;
-      const uint32_t tbl = ((off >> 16) << 1) | ((off >> 7) & 1);
-      const uint32_t e = (off >> 8) & 255;
-      const uint32_t val = gs[tbl * 256 + e];
-      *(u32x4*)((char*)L + off) = u32x4{val, val, val, val};
-    }
-    const u32x4* gz = (const u32x4*)(gtab + TAB_ZWIN);
-    for (uint32_t i = threadIdx.x; i < A_TREE_BYTES / 16; i += A_THREADS)
-      *(u32x4*)((char*)L + A_SLICE_BYTES + (i << 4)) = gz[i];
-    const u32x4* g128 = (const u32x4*)(gtab + TAB_ZPIECE + 3 * 1024);  // Z128 (chain join)
-    for (uint32_t i = threadIdx.x; i < 4096 / 16; i += A_THREADS)
-      *(u32x4*)((char*)L + A_SLICE_BYTES + A_TREE_BYTES + (i << 4)) = g128[i];
+#ifdef LCRC_PROBE_LDSDATA
+  for (uint32_t i = threadIdx.x; i < 512; i += A_THREADS) {
+    uint32_t h = i * 0x9E3779B9u + blockIdx.x * 0x85EBCA6Bu;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
+    lcrc_probe_tile[i] = u32x4{h, h * 0x27D4EB2Fu, h ^ 0x165667B1u, h * 0x94D049BBu};
   }
   __syncthreads();
+#endif
+  // lane (k, c) = (lane & 7, lane >> 3) reads piece 8*k + c of every 1 KiB of the tile
+  const uint32_t voff = 16u * (8u * (lane & 7) + (lane >> 3));
+
+  // two register tiles: while one is transposed and walked, the next one is in flight
+  u32x4 va[8], vb[8];
+  load_tile(va, tile_rsrc(base, span, t, ntiles), voff);  // before the LDS fill: HBM streams meanwhile
+
+  {
+    // Table image in one global round trip: every thread issues its loads up front.
+    //   slice T0..T3 (4 KiB)   -> staged in the Z-table area, then replicated 32x LDS->LDS
+    //   Z64, Z128..Z2048 (24 KiB) -> held in registers until the staging area is free again
+    const uint32_t tid = threadIdx.x;
+    const u32x4* gsl = (const u32x4*)(gtab + TAB_SLICE);
+    const u32x4* gz64 = (const u32x4*)(gtab + TAB_ZPIECE + 2 * 1024);  // Z64, Z128 (adjacent)
+    const u32x4* gzw = (const u32x4*)(gtab + TAB_ZWIN);                // Z256 .. Z2048
+    u32x4 sl = {0, 0, 0, 0}, za = {0, 0, 0, 0};
+    if (tid < 256) sl = gsl[tid];
+    if (tid < 512) za = gz64[tid];
+    const u32x4 zb = gzw[tid];
+    if (tid < 256) *(u32x4*)((char*)L + A_Z64 + (tid << 4)) = sl;
+    lds_barrier();
+    const uint32_t* stage = (const uint32_t*)((const char*)L + A_Z64);
+#pragma unroll
+    for (int k = 0; k < A_SLICE_BYTES / 16 / A_THREADS; ++k) {
+      const uint32_t off = (tid + k * A_THREADS) << 4;
+      const uint32_t tbl = ((off >> 16) << 1) | ((off >> 7) & 1);
+      const uint32_t val = stage[tbl * 256 + ((off >> 8) & 255)];
+      *(u32x4*)((char*)L + off) = u32x4{val, val, val, val};
+    }
+    lds_barrier();
+    if (tid < 512) *(u32x4*)((char*)L + A_Z64 + (tid << 4)) = za;
+    *(u32x4*)((char*)L + A_Z64 + 8192 + (tid << 4)) = zb;
+  }
+  lds_barrier();
 
   const uint32_t rep = (lane & 31) << 2;
   const uint32_t b0 = rep, b1 = (1u << 7) | rep, b2 = (1u << 16) | rep, b3 = (1u << 16) | (1u << 7) | rep;
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
-  while (t < ntiles) {
+  // va holds tile t, vb tile t + nwaves; walking a buffer refills it with the tile two steps ahead.
+  // The steady-state loop walks both buffers (no early exit inside, so the compiler's vmcnt bookkeeping
+  // sees one fixed issue order: each walk waits only for its own buffer); an odd tail tile follows.
+  load_tile(vb, tile_rsrc(base, span, t + nwaves, ntiles), voff);
+  for (; t + nwaves < ntiles; t += 2 * nwaves) {
     __builtin_amdgcn_sched_barrier(0);
-    transpose_stage<2>(v);
-    transpose_stage<3>(v);
-    transpose_stage<4>(v);
-    transpose_stage<5>(v);
-    // lane l now holds window l of the tile (256 B at tile offset 256*l) in v[0..15].
-    // Two independent chains (bytes 0..127 and 128..255) for ILP; as soon as a register has been
-    // walked it receives the next tile's piece, so the next tile streams in during this walk.
-    const uint64_t tcur = t;
-    t += nwaves;
-    __amdgpu_buffer_rsrc_t rsn = tile_rsrc(base, span, t, ntiles);
-    uint32_t pa = 0, pb = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      pa = step4_rep(L, pa, v[j].x, b0, b1, b2, b3);
-      pb = step4_rep(L, pb, v[j + 8].x, b0, b1, b2, b3);
-      pa = step4_rep(L, pa, v[j].y, b0, b1, b2, b3);
-      pb = step4_rep(L, pb, v[j + 8].y, b0, b1, b2, b3);
-      pa = step4_rep(L, pa, v[j].z, b0, b1, b2, b3);
-      pb = step4_rep(L, pb, v[j + 8].z, b0, b1, b2, b3);
-      pa = step4_rep(L, pa, v[j].w, b0, b1, b2, b3);
-      pb = step4_rep(L, pb, v[j + 8].w, b0, b1, b2, b3);
-      v[j] = load_piece<LCRC_LOAD_AUX>(rsn, voff, j);
-      v[j + 8] = load_piece<LCRC_LOAD_AUX>(rsn, voff, j + 8);
-    }
-    uint32_t p = zlook(L, A_SLICE_BYTES + A_TREE_BYTES, pa) ^ pb;
-
-    if (!FINAL) {
-      out[tcur * 64 + lane] = p;
-    } else {
-      // fold the 16 windows of each 4 KiB block (= one 16-lane row): level m joins lane g with g + 2^m
-      p = tree_level<0>(L, p, lane);
-      p = tree_level<1>(L, p, lane);
-      p = tree_level<2>(L, p, lane);
-      p = tree_level<3>(L, p, lane);
-      const uint64_t blk = tcur * 4 + (lane >> 4);
-      if ((lane & 15) == 0 && blk < nblk) {
-        uint32_t crc = p ^ fin;
-        if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
-        out[blk] = crc;
-        if (expected && expected[blk] != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
-      }
-    }
+    uint32_t p = walk_tile(L, va, b0, b1, b2, b3, tile_rsrc(base, span, t + 2 * nwaves, ntiles), voff);
+    finish_tile<FINAL>(L, p, t, lane, out, nblk, fin, flags, expected, mismatch);
+    __builtin_amdgcn_sched_barrier(0);
+    p = walk_tile(L, vb, b0, b1, b2, b3, tile_rsrc(base, span, t + 3 * nwaves, ntiles), voff);
+    finish_tile<FINAL>(L, p, t + nwaves, lane, out, nblk, fin, flags, expected, mismatch);
   }
+  if (t < ntiles) {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t p = walk_tile(L, va, b0, b1, b2, b3, tile_rsrc(base, span, ntiles, ntiles), voff);
+    finish_tile<FINAL>(L, p, t, lane, out, nblk, fin, flags, expected, mismatch);
+  }
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {
+    lcrc_dbg_clock[blockIdx.x * 4 + 0] = c1 - c0;
+    lcrc_dbg_clock[blockIdx.x * 4 + 1] = r1 - r0;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -470,6 +564,24 @@ __global__ void __launch_bounds__(256) k_wal_finish(lcrc_wal_rec_dev* __restrict
 // host-side launchers (called from lcrc_api.cpp)
 // ---------------------------------------------------------------------------------------------------
 extern "C" {
+
+#ifdef LCRC_PROBE_CLOCK
+// effective shader clock (MHz) of the last k_windows launch: median over workgroups of
+// d(s_memtime) / d(s_memrealtime) * 100 MHz
+double lcrc_probe_clock_mhz(int nwg) {
+  static unsigned long long h[4096];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(lcrc_dev::lcrc_dbg_clock), sizeof(h)) != hipSuccess) return -1;
+  double v[1024];
+  int n = 0;
+  for (int i = 0; i < nwg && i < 1024; ++i)
+    if (h[i * 4 + 1]) v[n++] = 100.0 * (double)h[i * 4] / (double)h[i * 4 + 1];
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && v[j - 1] > v[j]; --j) {
+      double t = v[j]; v[j] = v[j - 1]; v[j - 1] = t;
+    }
+  return n ? v[n / 2] : -1;
+}
+#endif
 
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
                                uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
