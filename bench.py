@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident CRC throughput for the leveldb-rust block/record checksum path.
+
+Metric (BASELINE.json): GiB/s of CRC32C over device-resident 4 KiB blocks, and the fraction of HBM3E read
+bandwidth. A "step" is one batched checksum pass over one 64K x 4 KiB batch (256 MiB, BASELINE.json
+configs[1]) already resident in HBM; four such batches rotate so every step reads from HBM rather than the
+256 MiB Infinity Cache. N>1: one process per GPU (torch.distributed.run), each rank checksums its own
+independent batches (no collective on the data path); `value` = all ranks' bytes / max-over-ranks time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed|mixed|wal] [--mode c|ref]
+
+Prints ONE JSON line on rank 0. `roofline.achieved` = payload bytes per launch / average launch time
+measured with HIP events on the engine's stream; `traffic` comes from the rocprofv3 PMC summary in
+profiles/ when one exists for this workload (tools/collect_traffic.py), else null. `cpu_baseline` times the
+oracle's restatement of the reference's CPU CRC on this host (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as entry  # noqa: E402
+
+METRIC = "GiB/s CRC32C over device-resident 4 KiB blocks; % of HBM3E read BW"
+PEAK_GBS = 8000.0  # MI355X HBM3E peak, GB/s (MI355X_MICROARCH.md chip table, spec)
+NBUF = 4
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", choices=["fixed", "mixed", "wal"], default="fixed")
+    p.add_argument("--mode", choices=["c", "ref"], default="c")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=1.0, help="wall seconds of the CPU baseline sample")
+    p.add_argument("--extra-out", default=None, help="also write the result dict to this file")
+    p.add_argument("--host-resident", action="store_true",
+                   help="fixed config starting and ending in (pinned) host memory: H2D + kernel + D2H per step "
+                        "(the PCIe-inclusive end-to-end rate reported in DESIGN.md, never the headline value)")
+    p.add_argument("--chunk-mib", type=int, default=32, help="host-resident pipeline chunk size")
+    return p.parse_args(argv)
+
+
+class Dist:
+    """torch.distributed wrapper (barrier + max-over-ranks); single-process when WORLD_SIZE is unset."""
+
+    def __init__(self, backend=None):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(self.local_rank)
+            dist.init_process_group(backend)
+            self.dist, self.torch, self.backend = dist, torch, backend
+
+    def barrier(self):
+        if self.dist is not None:
+            if self.backend == "nccl":
+                self.dist.barrier(device_ids=[self.local_rank])
+            else:
+                self.dist.barrier()
+
+    def max(self, x):
+        if self.dist is None:
+            return x
+        dev = f"cuda:{self.local_rank}" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def cuda_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except ImportError:
+        pass
+
+
+def timed_run(dist, step, steps, warmup, eng=None):
+    """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
+    Returns (max-over-ranks wall seconds, this rank's HIP-event milliseconds on the engine stream)."""
+    for i in range(warmup):
+        step(i)
+    if eng is not None:
+        eng.sync()
+    cuda_sync()
+    dist.barrier()
+    cuda_sync()
+    t0 = time.perf_counter()
+    if eng is not None:
+        eng.timer_start()
+    for i in range(steps):
+        step(warmup + i)
+    kernel_ms = eng.timer_stop() if eng is not None else None  # events bracketing the K launches
+    if eng is not None:
+        eng.sync()
+    cuda_sync()
+    dist.barrier()
+    cuda_sync()
+    elapsed = time.perf_counter() - t0
+    return dist.max(elapsed), kernel_ms
+
+
+def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
+    """Whole-job throughput: every rank processed bytes_per_step * steps in at most elapsed_max."""
+    return bytes_per_step * steps * world / elapsed_max / 2 ** 30
+
+
+# ---------------------------------------------------------------------------------------------------
+# workloads: each returns (step(i) callable, payload bytes per step, config dict, host sample for the CPU
+# baseline, verify(i) callable giving the device crcs of step i for the baseline cross-check)
+# ---------------------------------------------------------------------------------------------------
+def workload_fixed(m, synth, eng, rank, device):
+    nblk, blen = 65536, 4096
+    host = [synth.splitmix_bytes(synth.SEED_FIXED + rank * NBUF + i, nblk * blen) for i in range(NBUF)]
+    bufs = [m.DeviceBuffer.from_host(h, device) for h in host]
+    out = m.DeviceBuffer(nblk * 4, device)
+
+    def step(i):
+        eng.batch_uniform(bufs[i % NBUF], nblk, blen, blen, out)
+
+    def crcs():  # device result for batch 0 (the CPU baseline's sample)
+        step(0)
+        eng.sync()
+        return out.download(np.uint32, nblk)
+
+    cfg = {"workload": "64K x 4 KiB blocks, device-resident (BASELINE configs[1])", "blocks": nblk,
+           "block_bytes": blen, "batches_rotated": NBUF, "layout": "back-to-back"}
+    return step, nblk * blen, cfg, (host[0], nblk, blen), crcs
+
+
+def workload_host(m, synth, eng, rank, device, chunk_mib=32):
+    nblk, blen = 65536, 4096
+    pinned = m.PinnedBuffer(nblk * blen)
+    pinned.array[:] = synth.splitmix_bytes(synth.SEED_FIXED + rank * NBUF, nblk * blen)
+
+    def step(i):
+        eng.batch_host_uniform(pinned, nblk, blen, blen, chunk_bytes=chunk_mib << 20)
+
+    cfg = {"workload": "64K x 4 KiB blocks, HOST-resident pinned buffer: H2D + kernel + D2H (end-to-end)",
+           "blocks": nblk, "block_bytes": blen, "chunk_mib": chunk_mib}
+    return step, nblk * blen, cfg, None, None
+
+
+def workload_mixed(m, synth, eng, rank, device):
+    sizes = synth.mixed_sizes(256 << 20, seed=synth.SEED_MIXED + rank)
+    offs, total = synth.sstable_layout(sizes)
+    data = synth.splitmix_bytes(synth.SEED_MIXED + 1000 + rank, total)
+    d = np.zeros(len(sizes), m.DESC_DTYPE)
+    d["offset"], d["length"], d["expect_rel"] = offs, sizes.astype(np.uint64) + 1, m.NO_EXPECT
+    bufs = [m.DeviceBuffer.from_host(data, device) for _ in range(2)]
+    dd = m.DeviceBuffer.from_host(d.view(np.uint8), device)
+    out = m.DeviceBuffer(4 * len(sizes), device)
+    eng.reserve(total)
+
+    def step(i):
+        eng.batch(bufs[i % 2], total, dd, len(sizes), out)
+
+    cfg = {"workload": "SSTable file, block sizes 256 B-64 KiB zipf(1.1) (BASELINE configs[2])",
+           "blocks": int(len(sizes)), "file_bytes": int(total), "mean_block": float(sizes.mean())}
+    return step, int((sizes.astype(np.uint64) + 1).sum()), cfg, None, None
+
+
+def workload_wal(m, synth, eng, rank, device):
+    w = m.LogWriter()
+    payload = synth.splitmix_bytes(synth.SEED_WAL + 1000 + rank, 1 << 20)
+    for n in synth.wal_lengths(256 << 20, seed=synth.SEED_WAL + rank):
+        w.add_record(payload[: min(n, len(payload))] if n <= len(payload) else np.resize(payload, n))
+    data = np.frombuffer(w.contents(), np.uint8)
+    dev = m.DeviceBuffer.from_host(data, device)
+    maxr = len(data) // 7 + 1
+    recs = m.DeviceBuffer(maxr * m.WAL_REC_DTYPE.itemsize, device)
+    eng.reserve(len(data))
+    first = eng.wal_scan(dev, len(data), maxr, recs)
+    covered = int((first["length"].astype(np.uint64) + 1).sum())
+
+    def step(i):
+        eng.wal_scan(dev, len(data), maxr, recs)
+
+    cfg = {"workload": "WAL: 32 KiB log blocks, records n~U[1,2^k), k~U[1,16] (BASELINE configs[3])",
+           "file_bytes": int(len(data)), "records": int(len(first)), "bytes_counted": "sum(1+len)"}
+    return step, covered, cfg, None, None
+
+
+def load_traffic(config, mode):
+    path = os.path.join(ROOT, "profiles", f"traffic_{config}_{mode}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(orc, sample, mode, seconds, device_crcs):
+    """The reference's CPU CRC restated in oracle/ (snap's SSE4.2 CRC-32C path for mode c, crc32fast's
+    PCLMULQDQ path for mode ref), all usable host cores, repeated passes over the same 256 MiB batch."""
+    data, nblk, blen = sample
+    threads = min(16, os.cpu_count() or 1)
+    algo = orc.ALGO_SSE42_C if mode == "c" else orc.ALGO_PCLMUL_REF
+    crcs, secs = orc.crc_uniform_mt(data, nblk, blen, blen, threads, algo)  # warm + cross-check
+    match = None
+    if device_crcs is not None:
+        want = crcs if mode == "ref" else np.fromiter((orc.mask(int(c)) for c in crcs), np.uint32, len(crcs))
+        match = bool(np.array_equal(device_crcs(), want))
+    passes, total = 0, 0.0
+    while total < seconds or passes < 2:
+        _, s = orc.crc_uniform_mt(data, nblk, blen, blen, threads, algo)
+        total += s
+        passes += 1
+    gib = passes * nblk * blen / 2 ** 30
+    return {"value": round(gib / total, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{passes} passes over one 64K x 4 KiB batch ({gib:.1f} GiB), "
+                      f"{'snap SSE4.2 crc32c' if mode == 'c' else 'crc32fast PCLMULQDQ'} restated in oracle/, "
+                      f"{threads} threads",
+            "cpu_seconds": round(total * threads, 1), "matches_device": match}
+
+
+def main(argv=None):
+    args = parse(argv)
+    dist = Dist()
+    rank, world = dist.rank, dist.world
+    device = dist.local_rank
+    m = entry.load()
+    synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
+    mode = m.MODE_C if args.mode == "c" else m.MODE_REF
+    flags = m.FLAG_MASK if mode == m.MODE_C else 0
+    eng = m.Engine(device, mode, flags)
+    if args.host_resident:
+        step, nbytes, cfg, sample, crcs = workload_host(m, synth, eng, rank, device, args.chunk_mib)
+    else:
+        step, nbytes, cfg, sample, crcs = {"fixed": workload_fixed, "mixed": workload_mixed,
+                                           "wal": workload_wal}[args.config](m, synth, eng, rank, device)
+
+    elapsed_max, kernel_ms = timed_run(dist, step, args.steps, args.warmup, eng)
+    total_bytes = nbytes * args.steps * world
+    value = aggregate_gibs(nbytes, args.steps, world, elapsed_max)
+    per_launch_s = kernel_ms / 1e3 / args.steps
+    achieved = nbytes / per_launch_s / 1e9
+    traffic = load_traffic(args.config, args.mode)
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 bytes, seeds in leveldb-rust_amd/synth.py)",
+        "config": dict(cfg, crc="crc32c, LevelDB-masked" if mode == m.MODE_C else "crc-32/iso-hdlc (crc32fast)",
+                       parallelism=f"{world} independent shard(s), no collective"),
+        "pct_hbm_peak": round(100.0 * (total_bytes / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_GBS, 4),
+                     "traffic": traffic},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and sample is not None:
+        result["cpu_baseline"] = cpu_baseline(entry.load_oracle(), sample, args.mode, args.cpu_seconds, crcs)
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+        if args.extra_out:
+            with open(args.extra_out, "w") as f:
+                json.dump(result, f, indent=1)
+    eng.close()
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""Summarize a tools/profile_round.sh output directory into profiles/ (committed evidence).
+
+Writes:
+  profiles/<round>_<config>_<mode>_kernel_stats.csv   (rocprofv3 --stats table, verbatim)
+  profiles/<round>_<config>_<mode>_summary.json       (per-kernel avg duration, HBM bytes per launch)
+  profiles/traffic_<config>_<mode>.json               (read by bench.py for roofline.traffic)
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def find(d, pattern):
+    hits = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    return hits[0] if hits else None
+
+
+def counters(d, name):
+    f = find(d, "*counter_collection.csv")
+    per = {}
+    if not f:
+        return per
+    for row in csv.DictReader(open(f)):
+        if row.get("Counter_Name") != name:
+            continue
+        k = row["Kernel_Name"].split("(")[0]
+        per.setdefault(k, []).append(float(row["Counter_Value"]))
+    return per
+
+
+def main(outdir, rnd, config, mode):
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    tag = f"{rnd}_{config}_{mode}"
+    stats = find(os.path.join(outdir, "trace"), "*kernel_stats.csv")
+    summary = {"round": rnd, "config": config, "mode": mode, "kernels": {}}
+    if stats:
+        shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+        for row in csv.DictReader(open(stats)):
+            name = row["Name"].split("(")[0]
+            summary["kernels"][name] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+                                        "total_ns": float(row["TotalDurationNs"]),
+                                        "percent": float(row.get("Percentage", 0) or 0)}
+    fetch = counters(os.path.join(outdir, "fetch"), "FETCH_SIZE")
+    write = counters(os.path.join(outdir, "write"), "WRITE_SIZE")
+    traffic = {}
+    for k, vals in fetch.items():
+        # FETCH_SIZE is in KiB; gfx950 tallies 128-B streaming requests at 64 B -> x2 (MI355X_MICROARCH.md)
+        rd = sum(vals) / len(vals) * 1024 * 2
+        wr = (sum(write.get(k, [0])) / max(1, len(write.get(k, [0])))) * 1024
+        traffic[k] = {"hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                      "fetch_size_kib_raw": sum(vals) / len(vals), "launches_sampled": len(vals)}
+    summary["traffic"] = traffic
+    with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    # the dominant kernel's traffic for bench.py
+    dom = max(summary["kernels"].items(), key=lambda kv: kv[1]["total_ns"])[0] if summary["kernels"] else None
+    hot = None
+    for k in traffic:
+        if dom and dom.split("<")[0] in k:
+            hot = k
+    if hot is None and traffic:
+        hot = max(traffic, key=lambda k: traffic[k]["hbm_read_bytes_per_launch"])
+    if hot:
+        t = traffic[hot]
+        with open(os.path.join(prof, f"traffic_{config}_{mode}.json"), "w") as f:
+            json.dump({"kernel": hot, "hbm_bytes_per_launch": t["hbm_read_bytes_per_launch"] + t["hbm_write_bytes_per_launch"],
+                       "hbm_read_bytes_per_launch": t["hbm_read_bytes_per_launch"],
+                       "hbm_write_bytes_per_launch": t["hbm_write_bytes_per_launch"],
+                       "source": f"profiles/{tag}_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
+                                 "FETCH_SIZE KiB x1024 x2 per the gfx950 correction)"}, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:5])
