@@ -34,7 +34,10 @@ def build(force=False, verbose=False, extra_flags=()):
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
+    # the atomic optimizer would read the ticket atomic's result at once (readfirstlane + vmcnt(0)),
+    # stalling on every load issued before it; k_windows reads it one walk later instead
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
            "-Wall", "-Wno-unused-result", "-o", tmp] + list(extra_flags) + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

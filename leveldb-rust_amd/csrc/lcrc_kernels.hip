@@ -28,25 +28,31 @@ typedef u32x4 u32x4_ua __attribute__((aligned(1)));
 namespace lcrc_dev {
 
 // ---------------------------------------------------------------------------------------------------
-// k_windows LDS image (static, 152 KiB -> one 1024-thread workgroup per CU):
-//   [0, 128 KiB): slice-by-4 tables T0..T3, 256 entries each, 32 replicas. Table t lives in region
-//                 t>>1 (64 KiB each); entry e of that region is a 256 B row holding table 2*region's
-//                 32 replicas in its first 128 B and table 2*region+1's in the second. Lane l reads
-//                 replica l&31 -> bank (l&31): the 32 lanes of each ds_read_b32 half-wave group never
-//                 conflict. The byte address of (t, e, l) = (t>>1)<<16 | e<<8 | (t&1)<<7 | (l&31)<<2,
-//                 built with ONE v_perm_b32 from a per-lane base and the data byte.
-//   [128 KiB, 152 KiB): byte-sliced shift tables Z64 (chain join), Z128 .. Z2048 (window tree),
-//                 unreplicated: they serve a few lookups per tile.
+// k_windows LDS image (152 KiB -> one 1024-thread workgroup per CU)
+//
+// Four replicated "table sets" S0..S3 of four byte tables each: S0 = slice-by-4 T0..T3, S1 = Z64,
+// S2 = Z256, S3 = Z512 (Z_n[k][b] = byte b at position k advanced over n zero bytes). Set s occupies
+// 64 KiB region s >> 1, half s & 1 of every 256 B row, row e holding entry e. Inside a half-row
+// (32 dwords = the 32 LDS banks) dword 8*p + r is replica r (0..7) of the set's table at position p;
+// position p is indexed by data byte 3 - p (slice: T_p; shifts: Z[3 - p]).
+// Compact rotated lookups: lane l (r = l & 7, q = (l >> 3) & 3) performs the four lookups of one step
+// as instructions i = 0..3 on position (i + q) & 3, replica r. In every 32-lane ds_read group the banks
+// 8*((i + q) & 3) + r are pairwise distinct, so all lookups are conflict-free with 8 replicas per table
+// instead of 32 -- which is what makes room to replicate the shift tables as well. The address is one
+// v_perm_b32 of a per-lane base (byte 0: half/position/replica, byte 2: region) and the data byte.
+//   [128 KiB, 144 KiB): staging of the source tables during the fill.
+//   [144 KiB, 152 KiB): Z1024, Z2048 (unreplicated) for the two upper levels of the block tree.
 // ---------------------------------------------------------------------------------------------------
-constexpr int A_SLICE_BYTES = 131072;
-constexpr int A_Z64 = A_SLICE_BYTES;       // Z64, then Z128, Z256, Z512, Z1024, Z2048 at +4 KiB steps
-constexpr int A_ZTREE = A_Z64 + 4096;      // Z128 .. Z2048: level m of the tree shifts 128 << m bytes
-constexpr int A_LDS_BYTES = A_Z64 + 6 * 4096;
+constexpr int A_STAGE = 131072;             // fill staging: slice, Z64, Z256, Z512 (dead after the fill),
+constexpr int A_ZUP = A_STAGE + 16384;      // then Z1024, Z2048 (live)
+constexpr int A_LDS_BYTES = A_ZUP + 2 * 4096;
 #ifndef LCRC_A_THREADS
 #define LCRC_A_THREADS 1024
 #endif
 constexpr int A_THREADS = LCRC_A_THREADS;
-constexpr int TILE = 8192;  // bytes per wave tile (8 loads x 64 lanes x 16 B)
+static_assert(A_THREADS == 1024, "the table fill maps one 16 B source chunk per thread");
+constexpr int REGION = 16384;  // bytes per wave iteration: two 8 KiB half-tiles, 64 windows of 256 B
+constexpr uint32_t SET_S1 = 1u << 7, SET_S2 = 1u << 16, SET_S3 = (1u << 16) | (1u << 7);
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt(0)) but not for its
 // outstanding global loads -- __syncthreads() would add vmcnt(0) and expose the first tile's latency.
@@ -59,33 +65,61 @@ __device__ __forceinline__ uint32_t lds_u32(const void* lds_base, uint32_t byte_
   return *(const uint32_t*)((const char*)lds_base + byte_addr);
 }
 
-// v_perm_b32 selector building the table address from base (S0) and data byte k of x (S1):
-// out = { 0x00, base.b2, x.bk, base.b0 }
-template <int K>
-__device__ __forceinline__ uint32_t tab_addr(uint32_t base, uint32_t x) {
-  return __builtin_amdgcn_perm(base, x, 0x0C060004u | (K << 8));
-}
-
 // a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); gfx9 has no v_xor3
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// one slice-by-4 step on x = r ^ w (already folded); returns walk(r, w) ^ w_next
-__device__ __forceinline__ uint32_t step4x(const void* L, uint32_t x, uint32_t w_next, uint32_t b0, uint32_t b1,
-                                           uint32_t b2, uint32_t b3) {
-  uint32_t t3 = lds_u32(L, tab_addr<0>(b3, x));
-  uint32_t t2 = lds_u32(L, tab_addr<1>(b2, x));
-  uint32_t t1 = lds_u32(L, tab_addr<2>(b1, x));
-  uint32_t t0 = lds_u32(L, tab_addr<3>(b0, x));
-  return xor3(xor3(t0, t1, w_next), t2, t3);
+// per-lane lookup parameters of the rotated layout: base byte 0 and the v_perm selector of instruction i
+// (out = { 0x00, base.b2, x.b(3 - p), base.b0 })
+struct Rot {
+  uint32_t b[4], s[4];
+};
+
+__device__ __forceinline__ Rot make_rot(uint32_t lane) {
+  Rot R;
+  const uint32_t r = lane & 7, q = (lane >> 3) & 3;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t p = (i + q) & 3;
+    R.b[i] = (p << 5) | (r << 2);
+    R.s[i] = 0x0C060004u | ((3 - p) << 8);
+  }
+  return R;
 }
 
-// In-register transpose. Lane l = 8*c + k (k = l & 7, c = l >> 3) loads, in instruction j, the 16 B piece
-// at tile byte 1024*j + 128*k + 16*c (each instruction still reads one contiguous 1 KiB). Within each group
-// k the 8 lanes c and 8 registers j form an 8x8 matrix of pieces; transposing it gives lane (k, c) the
-// pieces at 1024*c + 128*k + 16*j', j' = 0..7: one contiguous 128 B window whose index inside the tile is
-// 8*c + k = l. The three butterfly stages run over lane bits 3..5:
+// one slice-by-4 step on x = r ^ w (already folded); returns walk(r, w) ^ w_next
+__device__ __forceinline__ uint32_t step4x(const void* L, const Rot& R, uint32_t x, uint32_t w_next) {
+  const uint32_t a0 = lds_u32(L, __builtin_amdgcn_perm(R.b[0], x, R.s[0]));
+  const uint32_t a1 = lds_u32(L, __builtin_amdgcn_perm(R.b[1], x, R.s[1]));
+  const uint32_t a2 = lds_u32(L, __builtin_amdgcn_perm(R.b[2], x, R.s[2]));
+  const uint32_t a3 = lds_u32(L, __builtin_amdgcn_perm(R.b[3], x, R.s[3]));
+  return xor3(xor3(a0, a1, w_next), a2, a3);
+}
+
+// Z_n(x) through replicated set SET (conflict-free)
+template <uint32_t SET>
+__device__ __forceinline__ uint32_t zrot(const void* L, const Rot& R, uint32_t x) {
+  const uint32_t a0 = lds_u32(L, __builtin_amdgcn_perm(R.b[0] | SET, x, R.s[0]));
+  const uint32_t a1 = lds_u32(L, __builtin_amdgcn_perm(R.b[1] | SET, x, R.s[1]));
+  const uint32_t a2 = lds_u32(L, __builtin_amdgcn_perm(R.b[2] | SET, x, R.s[2]));
+  const uint32_t a3 = lds_u32(L, __builtin_amdgcn_perm(R.b[3] | SET, x, R.s[3]));
+  return xor3(a0, a1, a2 ^ a3);
+}
+
+// Z_n(x) through an unreplicated byte-sliced table (4 x 256 entries at tab_byte_off)
+__device__ __forceinline__ uint32_t zlook(const void* L, uint32_t tab_byte_off, uint32_t r) {
+  const char* z = (const char*)L + tab_byte_off;
+  return *(const uint32_t*)(z + ((r & 0xff) << 2)) ^ *(const uint32_t*)(z + 1024 + (((r >> 8) & 0xff) << 2)) ^
+         *(const uint32_t*)(z + 2048 + (((r >> 16) & 0xff) << 2)) ^ *(const uint32_t*)(z + 3072 + ((r >> 24) << 2));
+}
+
+// In-register transpose. In half-tile h (0: bytes [0, 128) of every 256 B window, 1: [128, 256)), lane
+// l = 8*c + k (k = l & 7, c = l >> 3) loads in instruction j the 16 B piece at region byte
+// 2048*j + 256*k + 128*h + 16*c: each instruction reads eight full 128 B lines. Within each group k the
+// 8 lanes c and 8 registers j form an 8x8 matrix of pieces; transposing it leaves lane (k, c) with the
+// pieces 2048*c + 256*k + 128*h + 16*j', j' = 0..7: half h of window 8*c + k = l. The butterfly stages
+// run over lane bits 3..5:
 //   bit 3: v_mov_b32_dpp row_shr:8 / row_shl:8 with a bank_mask -- disabled banks keep `old`, so the DPP
 //          move is also the select (one instruction per register)
 //   bit 4: v_permlane16_swap (odd rows of a <-> even rows of b), bit 5: v_permlane32_swap (one
@@ -118,201 +152,261 @@ __device__ __forceinline__ void transpose_stage(u32x4 (&v)[8]) {
   }
 }
 
-__device__ __forceinline__ uint32_t zlook(const void* L, uint32_t tab_byte_off, uint32_t r) {
-  const char* z = (const char*)L + tab_byte_off;
-  return *(const uint32_t*)(z + ((r & 0xff) << 2)) ^ *(const uint32_t*)(z + 1024 + (((r >> 8) & 0xff) << 2)) ^
-         *(const uint32_t*)(z + 2048 + (((r >> 16) & 0xff) << 2)) ^ *(const uint32_t*)(z + 3072 + ((r >> 24) << 2));
-}
-
-// one level of the window tree: lane g (g % 2^(M+1) == 0) <- Z_{128*2^M}(p_g) ^ p_{g+2^M}. Only the
-// combining lanes look up (exec-masked ds_reads: fewer bank conflicts on the unreplicated tables).
-template <int M>
-__device__ __forceinline__ uint32_t tree_level(const void* L, uint32_t p, uint32_t lane) {
-  uint32_t pn;
-  if constexpr (M < 4)
-    pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x100 + (1 << M), 0xF, 0xF, false);  // row_shl
-  else
-    pn = __shfl_down(p, 1 << M, 64);
-  if ((lane & ((2u << M) - 1)) == 0) p = zlook(L, A_ZTREE + M * 4096, p) ^ pn;
-  return p;
-}
-
 __device__ __forceinline__ uint32_t mask32c(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
 
-// wave-uniform descriptor for tile t: loads past the end of the span (or of a non-existent tile) return 0
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const uint8_t* base, uint64_t span, uint64_t t,
-                                                            uint64_t ntiles) {
+// wave-uniform descriptor for region t: loads past the end of the span (or of a non-existent region)
+// return 0 without touching memory
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t region_rsrc(const uint8_t* base, uint64_t span, uint64_t t,
+                                                              uint64_t nreg) {
   uint32_t nrec = 0;
   uint64_t toff = 0;
 #ifdef LCRC_PROBE_NOLOAD  // ablation build: no memory traffic, loads return zeros
-  ntiles = 0;
+  nreg = 0;
 #endif
-  if (t < ntiles) {
-#ifdef LCRC_PROBE_L2  // ablation build: every tile aliases one of the first 64 (512 KiB, L2-resident)
-    toff = (t & 63) * (uint64_t)TILE;
+  if (t < nreg) {
+#ifdef LCRC_PROBE_L2  // ablation build: every region aliases one of the first 32 (512 KiB, L2-resident)
+    toff = (t & 31) * (uint64_t)REGION;
 #else
-    toff = t * (uint64_t)TILE;
+    toff = t * (uint64_t)REGION;
 #endif
     const uint64_t rem = span - toff;
-    nrec = rem < (uint64_t)TILE ? (uint32_t)rem : (uint32_t)TILE;
+    nrec = rem < (uint64_t)REGION ? (uint32_t)rem : (uint32_t)REGION;
   }
   return __builtin_amdgcn_make_buffer_rsrc((void*)(base + toff), (short)0, (int)nrec, 0x00020000);
 }
 
 #ifdef LCRC_PROBE_LDSDATA  // ablation build: random data from an 8 KiB LDS tile, no VMEM at all
-__shared__ u32x4 lcrc_probe_tile[512];
-#define LCRC_REFILL(rs, off) (lcrc_probe_tile[((off) >> 4) & 511])
+__shared__ u32x4 lcrc_probe_tile[256];
+#define LCRC_REFILL(rs, off) (lcrc_probe_tile[((off) >> 4) & 255])
 #else
 #define LCRC_REFILL(rs, off) __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LCRC_LOAD_AUX)
 #endif
 
-__device__ __forceinline__ void load_tile(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+__device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j * 1024);
+  for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j * 2048);
 }
 
-// Transpose + walk one tile already in registers; returns walk(0, window l) of this lane (128 B).
-// As each register pair is consumed it is refilled from `rs` (the tile after next), so every wave keeps
-// between one and two tiles of loads in flight while it computes.
-__device__ __forceinline__ uint32_t walk_tile(const void* L, u32x4 (&v)[8], uint32_t b0, uint32_t b1, uint32_t b2,
-                                              uint32_t b3, __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+// Transpose + walk one half-tile already in registers, starting chain a from register value `init`:
+// returns walk(init, 128 B half of window l). As each register pair is consumed it is refilled from `rs`
+// (the same half of the next region), so every wave keeps between one and two half-tiles in flight.
+__device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4 (&v)[8], uint32_t init,
+                                              __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
   transpose_stage<3>(v);
   transpose_stage<4>(v);
   transpose_stage<5>(v);
 #ifdef LCRC_PROBE_NOWALK  // ablation build: fold the data with xor only
-  uint32_t p = 0;
+  uint32_t p = init;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     p ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-    v[j] = LCRC_REFILL(rs, voff + j * 1024);
+    v[j] = LCRC_REFILL(rs, voff + j * 2048);
   }
   return p;
 #else
-  // two independent chains over the 64 B halves (pieces 0..3 and 4..7); x carries the chain register
+  // two independent chains over the 64 B quarters (pieces 0..3 and 4..7); x carries the chain register
   // already xored with its next data word
-  uint32_t xa = v[0].x, xb = v[4].x;
+  uint32_t xa = v[0].x ^ init, xb = v[4].x;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    xa = step4x(L, xa, v[j].y, b0, b1, b2, b3);
-    xb = step4x(L, xb, v[4 + j].y, b0, b1, b2, b3);
-    xa = step4x(L, xa, v[j].z, b0, b1, b2, b3);
-    xb = step4x(L, xb, v[4 + j].z, b0, b1, b2, b3);
-    xa = step4x(L, xa, v[j].w, b0, b1, b2, b3);
-    xb = step4x(L, xb, v[4 + j].w, b0, b1, b2, b3);
-    xa = step4x(L, xa, j < 3 ? v[j + 1].x : 0u, b0, b1, b2, b3);
-    xb = step4x(L, xb, j < 3 ? v[5 + j].x : 0u, b0, b1, b2, b3);
-    v[j] = LCRC_REFILL(rs, voff + j * 1024);
-    v[4 + j] = LCRC_REFILL(rs, voff + (4 + j) * 1024);
+    xa = step4x(L, R, xa, v[j].y);
+    xb = step4x(L, R, xb, v[4 + j].y);
+    xa = step4x(L, R, xa, v[j].z);
+    xb = step4x(L, R, xb, v[4 + j].z);
+    xa = step4x(L, R, xa, v[j].w);
+    xb = step4x(L, R, xb, v[4 + j].w);
+    xa = step4x(L, R, xa, j < 3 ? v[j + 1].x : 0u);
+    xb = step4x(L, R, xb, j < 3 ? v[5 + j].x : 0u);
+    v[j] = LCRC_REFILL(rs, voff + j * 2048);
+    v[4 + j] = LCRC_REFILL(rs, voff + (4 + j) * 2048);
     __builtin_amdgcn_sched_barrier(0);  // keep the refill here: hipcc would otherwise sink it past the walk
   }
-  return zlook(L, A_Z64, xa) ^ xb;
+  return zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two quarters
 #endif
 }
 
-// FINAL = false: out[t*32 + w] = walk(0, 256 B window w of tile t) (raw partials for k_blocks)
+// one level of the block tree inside a 16-lane DPP row: lane g (g % 2^(M+1) == 0) <-
+// Z_{256*2^M}(p_g) ^ p_{g+2^M}. Only the combining lanes look up (exec-masked ds_reads).
+template <int M>
+__device__ __forceinline__ uint32_t tree_level(const void* L, const Rot& R, uint32_t p, uint32_t lane) {
+  const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x100 + (1 << M), 0xF, 0xF, false);
+  if ((lane & ((2u << M) - 1)) == 0) {
+    if constexpr (M == 0)
+      p = zrot<SET_S2>(L, R, p) ^ pn;
+    else if constexpr (M == 1)
+      p = zrot<SET_S3>(L, R, p) ^ pn;
+    else
+      p = zlook(L, A_ZUP + (M - 2) * 4096, p) ^ pn;
+  }
+  return p;
+}
+
+// FINAL = false: out[t*64 + l] = walk(0, 256 B window l of region t) (raw partials for k_blocks)
 // FINAL = true : span = nblk * 4096; out[b] = crc of 4 KiB block b (xor fin, optional mask, verify)
 template <bool FINAL>
-__device__ __forceinline__ void finish_tile(const void* L, uint32_t p, uint64_t t, uint32_t lane,
-                                           uint32_t* __restrict__ out, uint64_t nblk, uint32_t fin, uint32_t flags,
-                                           const uint32_t* __restrict__ expected, uint32_t* __restrict__ mismatch) {
-  p = tree_level<0>(L, p, lane);  // 128 B windows -> 256 B windows
+__device__ __forceinline__ void finish_region(const void* L, const Rot& R, uint32_t p, uint64_t t, uint32_t lane,
+                                              uint32_t* __restrict__ out, uint64_t nblk, uint32_t fin,
+                                              uint32_t flags, const uint32_t* __restrict__ expected, uint32_t ev,
+                                              uint32_t* __restrict__ mismatch) {
   if (!FINAL) {
-    if ((lane & 1) == 0) out[t * 32 + (lane >> 1)] = p;
+    out[t * 64 + lane] = p;
     return;
   }
-  p = tree_level<1>(L, p, lane);
-  p = tree_level<2>(L, p, lane);
-  p = tree_level<3>(L, p, lane);
-  p = tree_level<4>(L, p, lane);
-  const uint64_t blk = t * 2 + (lane >> 5);
-  if ((lane & 31) == 0 && blk < nblk) {
+  p = tree_level<0>(L, R, p, lane);
+  p = tree_level<1>(L, R, p, lane);
+  p = tree_level<2>(L, R, p, lane);
+  p = tree_level<3>(L, R, p, lane);
+  const uint64_t blk = t * 4 + (lane >> 4);
+  if ((lane & 15) == 0 && blk < nblk) {
     uint32_t crc = p ^ fin;
     if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
     out[blk] = crc;
-    if (expected && expected[blk] != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
+    if (expected && ev != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
   }
+}
+
+// Regions are dealt to the waves of a workgroup from a counter in LDS. Every CU gets a contiguous share
+// of the regions, but inside the CU the instruction arbiter favours older waves (the first wave of each
+// SIMD finishes its static share in ~60% of the time of the fourth), so a static per-wave split leaves
+// the CU waiting for its youngest waves. The counter is an LDS atomic: its return is counted in
+// lgkmcnt, never behind the wave's HBM loads. take_ticket leaves the result in a VGPR and
+// ticket_region reads it one walk later (reading it at once would drain every LDS read in flight).
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* ctr, uint32_t lane) {
+  uint32_t v = 0;
+  if (lane == 0) v = atomicAdd(ctr, 1u);
+  return v;
+}
+__device__ __forceinline__ uint64_t ticket_region(uint32_t v, uint64_t reg_lo) {
+  return reg_lo + __builtin_amdgcn_readfirstlane(v);
 }
 
 #ifdef LCRC_PROBE_CLOCK  // diagnostic build: per-workgroup shader/real clock stamps around the tile loop
 __device__ unsigned long long lcrc_dbg_clock[4096];
+__device__ unsigned long long lcrc_dbg_stamp[4096 * 8];  // per wave: entry, tables ready, first half, end,
+                                                         // table source loaded, staged
 #endif
 
 template <bool FINAL>
 __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict__ base, uint64_t span,
-                                                      uint64_t ntiles, const uint32_t* __restrict__ gtab,
+                                                      uint64_t nreg, const uint32_t* __restrict__ gtab,
                                                       uint32_t* __restrict__ out, uint64_t nblk, uint32_t fin,
                                                       uint32_t flags, const uint32_t* __restrict__ expected,
                                                       uint32_t* __restrict__ mismatch) {
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
+  __shared__ uint32_t wg_ticket;
   const uint32_t lane = __lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * (A_THREADS / 64);
-  uint64_t t = (uint64_t)blockIdx.x * (A_THREADS / 64) + wave;
+  const uint32_t tid = threadIdx.x;
+  // this workgroup's share of the regions: [reg_lo, reg_hi); wave w starts on reg_lo + w, the rest by ticket
+  const uint64_t per = (nreg + gridDim.x - 1) / gridDim.x;
+  const uint64_t reg_lo = (uint64_t)blockIdx.x * per;
+  const uint64_t reg_hi = reg_lo + per < nreg ? reg_lo + per : nreg;
+  uint64_t t = reg_lo + wave;
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long s_entry = __builtin_amdgcn_s_memrealtime();
+  unsigned long long s_first = 0;
+#endif
 #ifdef LCRC_PROBE_LDSDATA
-  for (uint32_t i = threadIdx.x; i < 512; i += A_THREADS) {
+  for (uint32_t i = tid; i < 256; i += A_THREADS) {
     uint32_t h = i * 0x9E3779B9u + blockIdx.x * 0x85EBCA6Bu;
     h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
     lcrc_probe_tile[i] = u32x4{h, h * 0x27D4EB2Fu, h ^ 0x165667B1u, h * 0x94D049BBu};
   }
   __syncthreads();
 #endif
-  // lane (k, c) = (lane & 7, lane >> 3) reads piece 8*k + c of every 1 KiB of the tile
-  const uint32_t voff = 16u * (8u * (lane & 7) + (lane >> 3));
 
-  // two register tiles: while one is transposed and walked, the next one is in flight
+  // Table image, step 1: coalesced 16 B loads of the 24 KiB of source tables (slice T0..T3, Z64, then
+  // Z256 .. Z2048 -- adjacent in the global image), completed BEFORE the first region's HBM loads are
+  // issued: vector-memory returns reach a CU in issue order across its waves, so a table load issued
+  // after other waves' HBM loads would wait for all of them. (Per-entry gathers from the image took
+  // ~10 us: every wave instruction touched 32 lines, and all 256 CUs hammered the same 320 lines.)
+  const u32x4* g_sl = (const u32x4*)(gtab + TAB_SLICE);
+  const u32x4* g_z64 = (const u32x4*)(gtab + TAB_ZPIECE + 2048);
+  const u32x4* g_zw = (const u32x4*)(gtab + TAB_ZWIN);
+  const u32x4 src0 = tid < 256 ? g_sl[tid] : (tid < 512 ? g_z64[tid - 256] : g_zw[tid - 512]);
+  u32x4 src1 = {0, 0, 0, 0};
+  if (tid < 512) src1 = g_zw[512 + tid];
+#ifndef LCRC_FILL_BEHIND  // ablation build: old order (fill behind the HBM loads)
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
+#endif
+
+  // lane (k, c) = (lane & 7, lane >> 3) reads piece 16*k + 8*h + c of every 2 KiB of the region
+  const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
   u32x4 va[8], vb[8];
-  load_tile(va, tile_rsrc(base, span, t, ntiles), voff);  // before the LDS fill: HBM streams meanwhile
-
   {
-    // Table image in one global round trip: every thread issues its loads up front.
-    //   slice T0..T3 (4 KiB)   -> staged in the Z-table area, then replicated 32x LDS->LDS
-    //   Z64, Z128..Z2048 (24 KiB) -> held in registers until the staging area is free again
-    const uint32_t tid = threadIdx.x;
-    const u32x4* gsl = (const u32x4*)(gtab + TAB_SLICE);
-    const u32x4* gz64 = (const u32x4*)(gtab + TAB_ZPIECE + 2 * 1024);  // Z64, Z128 (adjacent)
-    const u32x4* gzw = (const u32x4*)(gtab + TAB_ZWIN);                // Z256 .. Z2048
-    u32x4 sl = {0, 0, 0, 0}, za = {0, 0, 0, 0};
-    if (tid < 256) sl = gsl[tid];
-    if (tid < 512) za = gz64[tid];
-    const u32x4 zb = gzw[tid];
-    if (tid < 256) *(u32x4*)((char*)L + A_Z64 + (tid << 4)) = sl;
-    lds_barrier();
-    const uint32_t* stage = (const uint32_t*)((const char*)L + A_Z64);
-#pragma unroll
-    for (int k = 0; k < A_SLICE_BYTES / 16 / A_THREADS; ++k) {
-      const uint32_t off = (tid + k * A_THREADS) << 4;
-      const uint32_t tbl = ((off >> 16) << 1) | ((off >> 7) & 1);
-      const uint32_t val = stage[tbl * 256 + ((off >> 8) & 255)];
-      *(u32x4*)((char*)L + off) = u32x4{val, val, val, val};
-    }
-    lds_barrier();
-    if (tid < 512) *(u32x4*)((char*)L + A_Z64 + (tid << 4)) = za;
-    *(u32x4*)((char*)L + A_Z64 + 8192 + (tid << 4)) = zb;
+    const __amdgpu_buffer_rsrc_t rs = region_rsrc(base, span, t, reg_hi);
+    load_half(va, rs, voff_a);
+    __builtin_amdgcn_sched_barrier(0);  // issue order va, vb: the loop's vmcnt bookkeeping assumes it
+    load_half(vb, rs, voff_b);
   }
+  __builtin_amdgcn_sched_barrier(0);
+  // step 2: stage [slice | Z64 | Z256 | Z512 | Z1024 | Z2048] at A_STAGE (Z1024/Z2048 are already in their
+  // final place), then step 3: every thread writes 8 replicated 16 B chunks of the rotated sets
+  *(u32x4*)((char*)L + A_STAGE + (tid << 4)) = src0;
+  if (tid < 512) *(u32x4*)((char*)L + A_STAGE + 16384 + (tid << 4)) = src1;
   lds_barrier();
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
+#endif
+  {
+    constexpr int FILL = 131072 / 16 / A_THREADS;  // 16 B chunks of the replicated sets per thread
+    const uint32_t* stage = (const uint32_t*)((const char*)L + A_STAGE);
+#pragma unroll
+    for (int k = 0; k < FILL; ++k) {
+      const uint32_t off = (tid + k * A_THREADS) << 4;
+      const uint32_t set = ((off >> 16) << 1) | ((off >> 7) & 1), e = (off >> 8) & 255, p = (off >> 5) & 3;
+      // S0: T_p | S1: Z64[3-p] | S2: Z256[3-p] | S3: Z512[3-p]
+      const uint32_t v = stage[set * 1024 + (set == 0 ? p : 3 - p) * 256 + e];
+      *(u32x4*)((char*)L + off) = u32x4{v, v, v, v};
+    }
+  }
+  if (tid == 0) wg_ticket = A_THREADS / 64;
+  lds_barrier();
+#ifndef LCRC_STATIC_SCHED
+  uint32_t tk = take_ticket(&wg_ticket, lane);
+#endif
 
-  const uint32_t rep = (lane & 31) << 2;
-  const uint32_t b0 = rep, b1 = (1u << 7) | rep, b2 = (1u << 16) | rep, b3 = (1u << 16) | (1u << 7) | rep;
+  const Rot R = make_rot(lane);
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
-  // va holds tile t, vb tile t + nwaves; walking a buffer refills it with the tile two steps ahead.
-  // The steady-state loop walks both buffers (no early exit inside, so the compiler's vmcnt bookkeeping
-  // sees one fixed issue order: each walk waits only for its own buffer); an odd tail tile follows.
-  load_tile(vb, tile_rsrc(base, span, t + nwaves, ntiles), voff);
-  for (; t + nwaves < ntiles; t += 2 * nwaves) {
+  // tn = the region the refills load (ticket taken after the prologue or in the previous iteration);
+  // the ticket for the one after is taken between the two walks.
+  // va/vb hold the two halves of region t; walking a half refills it with the same half of region tn.
+  // Chain a of the second half continues from the first half's register value, so one Z64 join per
+  // half is the only recombination inside a window.
+  while (t < reg_hi) {
+#ifdef LCRC_STATIC_SCHED  // ablation build: wave w takes regions reg_lo + w, reg_lo + w + 16, ...
+    const uint64_t tn = t + A_THREADS / 64;
+#else
+    const uint64_t tn = ticket_region(tk, reg_lo);
+#endif
+    const __amdgpu_buffer_rsrc_t rsn = region_rsrc(base, span, tn, reg_hi);
+    // expected values of this region's blocks, loaded ahead of the refills so that the verify at the
+    // end of the iteration does not wait for them (vmcnt retires in issue order)
+    uint32_t ev = 0;
+    if (FINAL && expected) {
+      const uint64_t blk = t * 4 + (lane >> 4);
+      if ((lane & 15) == 0 && blk < nblk) ev = expected[blk];
+    }
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t p = walk_tile(L, va, b0, b1, b2, b3, tile_rsrc(base, span, t + 2 * nwaves, ntiles), voff);
-    finish_tile<FINAL>(L, p, t, lane, out, nblk, fin, flags, expected, mismatch);
+    const uint32_t x = walk_half(L, R, va, 0u, rsn, voff_a);
+#ifdef LCRC_PROBE_CLOCK
+    if (!s_first) s_first = __builtin_amdgcn_s_memrealtime();
+#endif
     __builtin_amdgcn_sched_barrier(0);
-    p = walk_tile(L, vb, b0, b1, b2, b3, tile_rsrc(base, span, t + 3 * nwaves, ntiles), voff);
-    finish_tile<FINAL>(L, p, t + nwaves, lane, out, nblk, fin, flags, expected, mismatch);
-  }
-  if (t < ntiles) {
-    __builtin_amdgcn_sched_barrier(0);
-    const uint32_t p = walk_tile(L, va, b0, b1, b2, b3, tile_rsrc(base, span, ntiles, ntiles), voff);
-    finish_tile<FINAL>(L, p, t, lane, out, nblk, fin, flags, expected, mismatch);
+#ifndef LCRC_STATIC_SCHED
+    tk = take_ticket(&wg_ticket, lane);
+#endif
+    const uint32_t p = walk_half(L, R, vb, x, rsn, voff_b);
+    finish_region<FINAL>(L, R, p, t, lane, out, nblk, fin, flags, expected, ev, mismatch);
+    t = tn;
   }
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -320,15 +414,28 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     lcrc_dbg_clock[blockIdx.x * 4 + 0] = c1 - c0;
     lcrc_dbg_clock[blockIdx.x * 4 + 1] = r1 - r0;
   }
+  const uint64_t gw = (uint64_t)blockIdx.x * (A_THREADS / 64) + wave;
+  if (lane == 0 && gw < 4096) {
+    lcrc_dbg_stamp[gw * 8 + 0] = s_entry;
+    lcrc_dbg_stamp[gw * 8 + 1] = r0;
+    lcrc_dbg_stamp[gw * 8 + 2] = s_first;
+    lcrc_dbg_stamp[gw * 8 + 3] = r1;
+    lcrc_dbg_stamp[gw * 8 + 4] = s_src;
+    lcrc_dbg_stamp[gw * 8 + 5] = s_staged;
+  }
 #endif
 }
 
 // ---------------------------------------------------------------------------------------------------
 // k_blocks: one 16-lane row per range. LDS (40 KiB): T0..T3 [4 KiB], Z16..Z128 [16 KiB],
 // Z256..Z2048 [16 KiB], Z4096 [4 KiB], unreplicated (the hot loop is in k_windows).
+// The kernel is latency-bound (a few dependent memory round trips per range), so every load a range
+// needs -- head and tail pieces, the first batch of window values -- is issued before any of them is
+// used, and 512-thread workgroups (4 per CU by LDS) keep 32 waves per CU in flight.
 // ---------------------------------------------------------------------------------------------------
-constexpr int B_THREADS = 256;
+constexpr int B_THREADS = 512;
 constexpr int B_LDS_DWORDS = TAB_TOTAL;
+constexpr int B_BATCH = 8;  // window values per lane loaded ahead of the fold
 
 __device__ __forceinline__ uint32_t byte_step(const uint32_t* L, uint32_t r, uint32_t b) {
   return (r >> 8) ^ L[TAB_SLICE + ((r ^ b) & 0xff)];
@@ -343,33 +450,60 @@ __device__ __forceinline__ uint32_t zl(const uint32_t* L, int off, uint32_t r) {
          L[off + 768 + (r >> 24)];
 }
 
-// Returns walk(R0, base[a, e)) for 0 <= e - a <= 256 to every lane of the 16-lane row (g = lane in row).
-// Pieces are aligned to END at e: piece g covers [e - 16*(16-g), e - 16*(15-g)).
-// Must be called by all 64 lanes (contains cross-lane ops).
-__device__ uint32_t row_walk(const uint32_t* L, const uint8_t* __restrict__ base, uint64_t a, uint64_t e,
-                             uint32_t R0, uint32_t g, uint32_t lane) {
+// Lane g's share of a row walk over [a, e) (0 <= e - a <= 256): the 16 B piece ending at
+// e - 16*(15-g). kind 0: empty, 1: whole piece inside [a, e), 2: straddles a (bytes [first, 16) only,
+// gathered bytewise so nothing before a -- possibly before the buffer -- is read).
+struct RowPiece {
+  u32x4 w;
+  uint32_t kind, first, at_a;
+};
+
+__device__ __forceinline__ RowPiece row_load(const uint8_t* __restrict__ base, uint64_t a, uint64_t e, uint32_t g) {
+  RowPiece p;
+  p.w = u32x4{0, 0, 0, 0};
+  p.kind = 0;
+  p.first = 0;
+  p.at_a = 0;
   const int64_t pe = (int64_t)e - 16 * (15 - (int)g);
   const int64_t ps = pe - 16;
-  uint32_t cv = 0;
   if (pe > (int64_t)a) {
     if (ps >= (int64_t)a) {
-      u32x4 w = *(const u32x4_ua*)(base + ps);
-      uint32_t rr = (ps == (int64_t)a) ? R0 : 0u;
-      rr = step4(L, rr, w.x);
-      rr = step4(L, rr, w.y);
-      rr = step4(L, rr, w.z);
-      rr = step4(L, rr, w.w);
-      cv = rr;
+      p.kind = 1;
+      p.at_a = ps == (int64_t)a;
+      p.w = *(const u32x4_ua*)(base + ps);
     } else {
-      // straddle: bytes [a, pe) (1..15 of them), walked from R0 at a
-      uint32_t rr = R0;
-      const uint32_t first = (uint32_t)((int64_t)a - ps);
+      p.kind = 2;
+      p.first = (uint32_t)((int64_t)a - ps);
+      uint32_t b[16];
 #pragma unroll
-      for (int i = 1; i < 16; ++i) {
-        if ((uint32_t)i >= first) rr = byte_step(L, rr, base[ps + i]);
-      }
-      cv = rr;
+      for (int i = 0; i < 16; ++i) b[i] = (i >= 1 && (uint32_t)i >= p.first) ? base[ps + i] : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        p.w[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | (b[4 * q + 3] << 24);
     }
+  }
+  return p;
+}
+
+// walk(R0, base[a, e)) from the row's loaded pieces, returned to every lane of the row; a == e -> R0.
+// Must be called by all 64 lanes (contains cross-lane ops).
+__device__ uint32_t row_walk(const uint32_t* L, const RowPiece& p, bool empty_range, uint32_t R0, uint32_t g,
+                             uint32_t lane) {
+  uint32_t cv = 0;
+  if (p.kind == 1) {
+    uint32_t rr = p.at_a ? R0 : 0u;
+    rr = step4(L, rr, p.w.x);
+    rr = step4(L, rr, p.w.y);
+    rr = step4(L, rr, p.w.z);
+    rr = step4(L, rr, p.w.w);
+    cv = rr;
+  } else if (p.kind == 2) {
+    // bytes [first, 16) walked from R0 (1..15 of them)
+    uint32_t rr = R0;
+#pragma unroll
+    for (int i = 1; i < 16; ++i)
+      if ((uint32_t)i >= p.first) rr = byte_step(L, rr, (p.w[i >> 2] >> (8 * (i & 3))) & 0xff);
+    cv = rr;
   }
   // row tree: level m joins lane g with g + 2^m, shifting the left part by 16*2^m bytes
 #pragma unroll
@@ -379,7 +513,7 @@ __device__ uint32_t row_walk(const uint32_t* L, const uint8_t* __restrict__ base
     if ((g & ((2u << m) - 1)) == 0) cv = sh ^ pn;
   }
   uint32_t res = __shfl(cv, lane & ~15u, 64);
-  return (a == e) ? R0 : res;
+  return empty_range ? R0 : res;
 }
 
 __device__ __forceinline__ uint32_t load_le32(const uint8_t* p) {
@@ -394,8 +528,9 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
                                                      const uint32_t* __restrict__ win, const uint32_t* __restrict__ gtab,
                                                      uint32_t init, uint32_t xorout, uint32_t flags,
                                                      uint32_t* __restrict__ out, uint32_t* __restrict__ mismatch) {
-  __shared__ uint32_t L[B_LDS_DWORDS];
-  for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS; i += B_THREADS) L[i] = gtab[i];
+  __shared__ __attribute__((aligned(16))) uint32_t L[B_LDS_DWORDS];
+  for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS)
+    ((u32x4*)L)[i] = ((const u32x4*)gtab)[i];
   __syncthreads();
 
   const uint32_t lane = __lane_id();
@@ -424,26 +559,46 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
     const uint64_t e = s + len;
     uint32_t acc;
     if (use_win) {
+      // window indices: head = partial-or-full window ws, full windows (ws, wfull], tail = partial window wl
       const uint64_t ws = s >> 8;
       const uint64_t wl = len ? (e - 1) >> 8 : ws;
       const bool single = (ws == wl);
       const uint64_t head_end = single ? e : (ws + 1) << 8;
-      const uint32_t head = row_walk(L, base, s, head_end, init, g, lane);
-      // middle: virtual items [pad zeros..., head, win[ws+1 .. wfull]] folded 16 per round
+      const uint64_t ta = (single || (e & 255) == 0) ? e : (wl << 8);
       const uint64_t wfull = ((e & 255) == 0) ? wl : wl - 1;
+      // middle: virtual items [pad zeros..., head, win[ws+1 .. wfull]] folded 16 per round (Horner
+      // with Z4096 per lane, then a 4-level tree)
       const uint64_t items = single ? 0 : (wfull - ws) + 1;  // head + full windows
       const uint64_t npad = (16 - (items & 15)) & 15;
       const uint64_t rounds = single ? 0 : (npad + items) >> 4;
       uint32_t rmax = (uint32_t)rounds;
       rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 16, 64));
       rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 32, 64));
+
+      // every load this range needs first: head and tail pieces, the first batch of window values
+      const RowPiece ph = row_load(base, s, head_end, g);
+      const RowPiece pt = row_load(base, ta, e, g);
+      uint32_t vals[B_BATCH];
+#pragma unroll
+      for (int j = 0; j < B_BATCH; ++j) {
+        const uint64_t u = 16 * (uint64_t)j + g;
+        vals[j] = ((uint32_t)j < rounds && u > npad) ? win[ws + (u - npad)] : 0u;
+      }
+
+      const uint32_t head = row_walk(L, ph, s == head_end, init, g, lane);
       uint32_t a = 0;
-      for (uint32_t q = 0; q < rmax; ++q) {
-        const uint64_t u = 16 * q + g;
-        uint32_t val = 0;
-        if (q < rounds) {
-          if (u >= npad) val = (u == npad) ? head : win[ws + (u - npad)];
-          a = zl(L, TAB_Z4096, a) ^ val;
+      for (uint32_t q0 = 0; q0 < rmax; q0 += B_BATCH) {
+        if (q0) {
+#pragma unroll
+          for (int j = 0; j < B_BATCH; ++j) {
+            const uint64_t q = q0 + j, u = 16 * q + g;
+            vals[j] = (q < rounds && u > npad) ? win[ws + (u - npad)] : 0u;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < B_BATCH; ++j) {
+          const uint64_t q = q0 + j;
+          if (q < rounds) a = zl(L, TAB_Z4096, a) ^ (16 * q + g == npad ? head : vals[j]);
         }
       }
 #pragma unroll
@@ -455,8 +610,7 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
       const uint32_t mid = __shfl(a, lane & ~15u, 64);
       acc = single ? head : mid;
       // tail: the partial last window, walked from the folded value
-      const uint64_t ta = (single || (e & 255) == 0) ? e : (wl << 8);
-      acc = row_walk(L, base, ta, e, acc, g, lane);
+      acc = row_walk(L, pt, ta == e, acc, g, lane);
     } else {
       // direct: walk the whole range in 256 B chunks (sparse batches)
       uint32_t nch = (uint32_t)(((uint64_t)len + 255) >> 8);
@@ -464,11 +618,16 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
       cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, 16, 64));
       cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, 32, 64));
       acc = init;
+      RowPiece pc = row_load(base, s, s + 256 < e ? s + 256 : e, g);
       for (uint32_t k = 0; k < cmax; ++k) {
         uint64_t ca = s + 256 * k;
         uint64_t ce = ca + 256 < e ? ca + 256 : e;
         if (k >= nch) ca = ce = e;
-        acc = row_walk(L, base, ca, ce, acc, g, lane);
+        // next chunk's pieces in flight while this one is walked
+        const uint64_t na = ca + 256 < e ? ca + 256 : e, ne = na + 256 < e ? na + 256 : e;
+        const RowPiece pn = row_load(base, na, ne, g);
+        acc = row_walk(L, pc, ca == ce, acc, g, lane);
+        pc = pn;
       }
     }
     if (valid && g == 0) {
@@ -568,6 +727,13 @@ extern "C" {
 #ifdef LCRC_PROBE_CLOCK
 // effective shader clock (MHz) of the last k_windows launch: median over workgroups of
 // d(s_memtime) / d(s_memrealtime) * 100 MHz
+// raw per-wave s_memrealtime stamps (100 MHz) of the last k_windows launch: entry, tables ready,
+// first half-tile walked, end
+int lcrc_probe_stamps(unsigned long long* dst) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(lcrc_dev::lcrc_dbg_stamp), sizeof(unsigned long long) * 4096 * 8) ==
+                 hipSuccess ? 0 : -1;
+}
+
 double lcrc_probe_clock_mhz(int nwg) {
   static unsigned long long h[4096];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(lcrc_dev::lcrc_dbg_clock), sizeof(h)) != hipSuccess) return -1;
@@ -586,15 +752,15 @@ double lcrc_probe_clock_mhz(int nwg) {
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
                                uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
                                const uint32_t* expected, uint32_t* mismatch, hipStream_t st) {
-  const uint64_t ntiles = (span + lcrc_dev::TILE - 1) / lcrc_dev::TILE;
-  if (ntiles == 0) return hipSuccess;
-  uint64_t need = (ntiles + 15) / 16;
+  const uint64_t nreg = (span + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
+  if (nreg == 0) return hipSuccess;
+  uint64_t need = (nreg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
   int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   if (final_mode)
-    hipLaunchKernelGGL(lcrc_dev::k_windows<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, ntiles, gtab,
+    hipLaunchKernelGGL(lcrc_dev::k_windows<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg, gtab,
                        out, nblk, fin, flags, expected, mismatch);
   else
-    hipLaunchKernelGGL(lcrc_dev::k_windows<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, ntiles,
+    hipLaunchKernelGGL(lcrc_dev::k_windows<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg,
                        gtab, out, nblk, fin, flags, expected, mismatch);
   return hipGetLastError();
 }
@@ -604,7 +770,8 @@ hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint6
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
                               uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  uint64_t need = (n + 15) / 16;  // 16 ranges per 256-thread workgroup
+  const uint64_t per_wg = lcrc_dev::B_THREADS / 16;  // one range per 16-lane row
+  uint64_t need = (n + per_wg - 1) / per_wg;
   int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   if (uniform)
     hipLaunchKernelGGL(lcrc_dev::k_blocks<true>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs, n,

@@ -4,10 +4,13 @@ set -e
 cd "$(dirname "$0")/../.."
 mkdir -p tools/probe/variants
 SRC="leveldb-rust_amd/csrc/lcrc_kernels.hip leveldb-rust_amd/csrc/lcrc_api.cpp leveldb-rust_amd/csrc/lcrc_scalar.cpp leveldb-rust_amd/csrc/lcrc_leveldb.cpp"
-build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result "$@" $SRC; }
+build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -mllvm -amdgpu-atomic-optimizer-strategy=None -std=c++17 -fPIC -shared -Wno-unused-result "$@" $SRC; }
 build -DLCRC_PROBE_CLOCK -o tools/probe/variants/base.so &
 build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_L2 -o tools/probe/variants/l2.so &
 build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_LDSDATA -o tools/probe/variants/ldsdata.so &
 build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_NOLOAD -o tools/probe/variants/noload.so &
+build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_NOWALK -o tools/probe/variants/nowalk.so &
+build -DLCRC_PROBE_CLOCK -DLCRC_STATIC_SCHED -o tools/probe/variants/static.so &
+build -DLCRC_PROBE_CLOCK -DLCRC_FILL_BEHIND -o tools/probe/variants/fillbehind.so &
 wait
 ls tools/probe/variants
