@@ -9,10 +9,17 @@ independent batches (no collective on the data path); `value` = all ranks' bytes
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed|mixed|wal] [--mode c|ref]
 
-Prints ONE JSON line on rank 0. `roofline.achieved` = payload bytes per launch / average launch time
-measured with HIP events on the engine's stream; `traffic` comes from the rocprofv3 PMC summary in
-profiles/ when one exists for this workload (tools/collect_traffic.py), else null. `cpu_baseline` times the
-oracle's restatement of the reference's CPU CRC on this host (rank 0, N=1 only).
+Steps are submitted round-robin to --streams engines (default 2: two contexts, each with its own HIP
+stream and workspace), the way a storage server keeps more than one verify batch in flight: batch i+1's
+workgroups start on the CUs that batch i's tail has already left. Every step is a complete, independent
+launch over its own batch; nothing is skipped or cached.
+
+Prints ONE JSON line on rank 0. `roofline.achieved` = payload bytes per launch / average duration of the
+SAME launch run alone: a second timed phase launches it back to back on ONE stream, bracketed by HIP
+events on that stream (this is the figure the rocprofv3 kernel trace in profiles/ must agree with, taken
+with --streams 1). `traffic` comes from the rocprofv3 PMC summary in profiles/ when one exists for this
+workload (tools/profile_round.sh), else null. `cpu_baseline` times the oracle's restatement of the
+reference's CPU CRC on this host (rank 0, N=1 only).
 """
 import argparse
 import json
@@ -45,6 +52,7 @@ def parse(argv=None):
                    help="fixed config starting and ending in (pinned) host memory: H2D + kernel + D2H per step "
                         "(the PCIe-inclusive end-to-end rate reported in DESIGN.md, never the headline value)")
     p.add_argument("--chunk-mib", type=int, default=32, help="host-resident pipeline chunk size")
+    p.add_argument("--streams", type=int, default=2, help="engines (context + HIP stream) steps rotate over")
     return p.parse_args(argv)
 
 
@@ -95,29 +103,42 @@ def cuda_sync():
         pass
 
 
-def timed_run(dist, step, steps, warmup, eng=None):
+def timed_run(dist, step, steps, warmup, engines=()):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
-    Returns (max-over-ranks wall seconds, this rank's HIP-event milliseconds on the engine stream)."""
+    Returns the max-over-ranks wall seconds."""
     for i in range(warmup):
         step(i)
-    if eng is not None:
-        eng.sync()
+    for e in engines:
+        e.sync()
     cuda_sync()
     dist.barrier()
     cuda_sync()
     t0 = time.perf_counter()
-    if eng is not None:
-        eng.timer_start()
     for i in range(steps):
         step(warmup + i)
-    kernel_ms = eng.timer_stop() if eng is not None else None  # events bracketing the K launches
-    if eng is not None:
-        eng.sync()
+    for e in engines:
+        e.sync()
     cuda_sync()
     dist.barrier()
     cuda_sync()
     elapsed = time.perf_counter() - t0
-    return dist.max(elapsed), kernel_ms
+    return dist.max(elapsed), None
+
+
+def launch_ms(step_on, eng, reps, windows=3):
+    """Average duration of one launch run alone: `reps` launches back to back on ONE engine's stream,
+    bracketed by HIP events recorded on that stream; the median of `windows` such windows (the chip's
+    clock under this load wanders by ~10% from one window to the next)."""
+    step_on(0, eng)
+    eng.sync()
+    per = []
+    for _ in range(windows):
+        eng.timer_start()
+        for i in range(reps):
+            step_on(i, eng)
+        per.append(eng.timer_stop() / reps)
+        eng.sync()
+    return float(np.median(per))
 
 
 def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
@@ -129,39 +150,39 @@ def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
 # workloads: each returns (step(i) callable, payload bytes per step, config dict, host sample for the CPU
 # baseline, verify(i) callable giving the device crcs of step i for the baseline cross-check)
 # ---------------------------------------------------------------------------------------------------
-def workload_fixed(m, synth, eng, rank, device):
+def workload_fixed(m, synth, engs, rank, device):
     nblk, blen = 65536, 4096
     host = [synth.splitmix_bytes(synth.SEED_FIXED + rank * NBUF + i, nblk * blen) for i in range(NBUF)]
     bufs = [m.DeviceBuffer.from_host(h, device) for h in host]
-    out = m.DeviceBuffer(nblk * 4, device)
+    outs = [m.DeviceBuffer(nblk * 4, device) for _ in engs]
 
-    def step(i):
-        eng.batch_uniform(bufs[i % NBUF], nblk, blen, blen, out)
+    def step_on(i, eng):
+        eng.batch_uniform(bufs[i % NBUF], nblk, blen, blen, outs[engs.index(eng)])
 
     def crcs():  # device result for batch 0 (the CPU baseline's sample)
-        step(0)
-        eng.sync()
-        return out.download(np.uint32, nblk)
+        step_on(0, engs[0])
+        engs[0].sync()
+        return outs[0].download(np.uint32, nblk)
 
     cfg = {"workload": "64K x 4 KiB blocks, device-resident (BASELINE configs[1])", "blocks": nblk,
            "block_bytes": blen, "batches_rotated": NBUF, "layout": "back-to-back"}
-    return step, nblk * blen, cfg, (host[0], nblk, blen), crcs
+    return step_on, nblk * blen, cfg, (host[0], nblk, blen), crcs
 
 
-def workload_host(m, synth, eng, rank, device, chunk_mib=32):
+def workload_host(m, synth, engs, rank, device, chunk_mib=32):
     nblk, blen = 65536, 4096
     pinned = m.PinnedBuffer(nblk * blen)
     pinned.array[:] = synth.splitmix_bytes(synth.SEED_FIXED + rank * NBUF, nblk * blen)
 
-    def step(i):
+    def step_on(i, eng):
         eng.batch_host_uniform(pinned, nblk, blen, blen, chunk_bytes=chunk_mib << 20)
 
     cfg = {"workload": "64K x 4 KiB blocks, HOST-resident pinned buffer: H2D + kernel + D2H (end-to-end)",
            "blocks": nblk, "block_bytes": blen, "chunk_mib": chunk_mib}
-    return step, nblk * blen, cfg, None, None
+    return step_on, nblk * blen, cfg, None, None
 
 
-def workload_mixed(m, synth, eng, rank, device):
+def workload_mixed(m, synth, engs, rank, device):
     sizes = synth.mixed_sizes(256 << 20, seed=synth.SEED_MIXED + rank)
     offs, total = synth.sstable_layout(sizes)
     data = synth.splitmix_bytes(synth.SEED_MIXED + 1000 + rank, total)
@@ -169,18 +190,19 @@ def workload_mixed(m, synth, eng, rank, device):
     d["offset"], d["length"], d["expect_rel"] = offs, sizes.astype(np.uint64) + 1, m.NO_EXPECT
     bufs = [m.DeviceBuffer.from_host(data, device) for _ in range(2)]
     dd = m.DeviceBuffer.from_host(d.view(np.uint8), device)
-    out = m.DeviceBuffer(4 * len(sizes), device)
-    eng.reserve(total)
+    outs = [m.DeviceBuffer(4 * len(sizes), device) for _ in engs]
+    for e in engs:
+        e.reserve(total)
 
-    def step(i):
-        eng.batch(bufs[i % 2], total, dd, len(sizes), out)
+    def step_on(i, eng):
+        eng.batch(bufs[i % 2], total, dd, len(sizes), outs[engs.index(eng)])
 
     cfg = {"workload": "SSTable file, block sizes 256 B-64 KiB zipf(1.1) (BASELINE configs[2])",
            "blocks": int(len(sizes)), "file_bytes": int(total), "mean_block": float(sizes.mean())}
-    return step, int((sizes.astype(np.uint64) + 1).sum()), cfg, None, None
+    return step_on, int((sizes.astype(np.uint64) + 1).sum()), cfg, None, None
 
 
-def workload_wal(m, synth, eng, rank, device):
+def workload_wal(m, synth, engs, rank, device):
     w = m.LogWriter()
     payload = synth.splitmix_bytes(synth.SEED_WAL + 1000 + rank, 1 << 20)
     for n in synth.wal_lengths(256 << 20, seed=synth.SEED_WAL + rank):
@@ -188,17 +210,18 @@ def workload_wal(m, synth, eng, rank, device):
     data = np.frombuffer(w.contents(), np.uint8)
     dev = m.DeviceBuffer.from_host(data, device)
     maxr = len(data) // 7 + 1
-    recs = m.DeviceBuffer(maxr * m.WAL_REC_DTYPE.itemsize, device)
-    eng.reserve(len(data))
-    first = eng.wal_scan(dev, len(data), maxr, recs)
+    recs = [m.DeviceBuffer(maxr * m.WAL_REC_DTYPE.itemsize, device) for _ in engs]
+    for e in engs:
+        e.reserve(len(data))
+    first = engs[0].wal_scan(dev, len(data), maxr, recs[0])
     covered = int((first["length"].astype(np.uint64) + 1).sum())
 
-    def step(i):
-        eng.wal_scan(dev, len(data), maxr, recs)
+    def step_on(i, eng):  # wal_scan returns the record count to the host: it ends in a stream sync
+        eng.wal_scan(dev, len(data), maxr, recs[engs.index(eng)])
 
     cfg = {"workload": "WAL: 32 KiB log blocks, records n~U[1,2^k), k~U[1,16] (BASELINE configs[3])",
            "file_bytes": int(len(data)), "records": int(len(first)), "bytes_counted": "sum(1+len)"}
-    return step, covered, cfg, None, None
+    return step_on, covered, cfg, None, None
 
 
 def load_traffic(config, mode):
@@ -242,17 +265,20 @@ def main(argv=None):
     synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
     mode = m.MODE_C if args.mode == "c" else m.MODE_REF
     flags = m.FLAG_MASK if mode == m.MODE_C else 0
-    eng = m.Engine(device, mode, flags)
+    engs = [m.Engine(device, mode, flags) for _ in range(max(1, args.streams))]
     if args.host_resident:
-        step, nbytes, cfg, sample, crcs = workload_host(m, synth, eng, rank, device, args.chunk_mib)
+        step_on, nbytes, cfg, sample, crcs = workload_host(m, synth, engs, rank, device, args.chunk_mib)
     else:
-        step, nbytes, cfg, sample, crcs = {"fixed": workload_fixed, "mixed": workload_mixed,
-                                           "wal": workload_wal}[args.config](m, synth, eng, rank, device)
+        step_on, nbytes, cfg, sample, crcs = {"fixed": workload_fixed, "mixed": workload_mixed,
+                                              "wal": workload_wal}[args.config](m, synth, engs, rank, device)
 
-    elapsed_max, kernel_ms = timed_run(dist, step, args.steps, args.warmup, eng)
+    def step(i):
+        step_on(i, engs[i % len(engs)])
+
+    elapsed_max, _ = timed_run(dist, step, args.steps, args.warmup, engs)
     total_bytes = nbytes * args.steps * world
     value = aggregate_gibs(nbytes, args.steps, world, elapsed_max)
-    per_launch_s = kernel_ms / 1e3 / args.steps
+    per_launch_s = launch_ms(step_on, engs[0], args.steps) / 1e3
     achieved = nbytes / per_launch_s / 1e9
     traffic = load_traffic(args.config, args.mode)
     result = {
@@ -269,11 +295,13 @@ def main(argv=None):
         "dtype": "u8",
         "data": "synthetic (splitmix64 bytes, seeds in leveldb-rust_amd/synth.py)",
         "config": dict(cfg, crc="crc32c, LevelDB-masked" if mode == m.MODE_C else "crc-32/iso-hdlc (crc32fast)",
-                       parallelism=f"{world} independent shard(s), no collective"),
+                       parallelism=f"{world} independent shard(s), no collective",
+                       streams=len(engs)),
         "pct_hbm_peak": round(100.0 * (total_bytes / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_GBS, 4),
-                     "traffic": traffic},
+                     "traffic": traffic, "launch_us": round(per_launch_s * 1e6, 2),
+                     "timing": "one stream, launches back to back, HIP events on that stream, median of 3 windows"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and sample is not None:
         result["cpu_baseline"] = cpu_baseline(entry.load_oracle(), sample, args.mode, args.cpu_seconds, crcs)
@@ -284,7 +312,8 @@ def main(argv=None):
         if args.extra_out:
             with open(args.extra_out, "w") as f:
                 json.dump(result, f, indent=1)
-    eng.close()
+    for e in engs:
+        e.close()
     dist.close()
 
 

@@ -265,19 +265,19 @@ __device__ __forceinline__ void finish_region(const void* L, const Rot& R, uint3
   }
 }
 
-// Regions are dealt to the waves of a workgroup from a counter in LDS. Every CU gets a contiguous share
-// of the regions, but inside the CU the instruction arbiter favours older waves (the first wave of each
-// SIMD finishes its static share in ~60% of the time of the fourth), so a static per-wave split leaves
-// the CU waiting for its youngest waves. The counter is an LDS atomic: its return is counted in
-// lgkmcnt, never behind the wave's HBM loads. take_ticket leaves the result in a VGPR and
-// ticket_region reads it one walk later (reading it at once would drain every LDS read in flight).
-__device__ __forceinline__ uint32_t take_ticket(uint32_t* ctr, uint32_t lane) {
+// Region scheduler: the regions are split into equal contiguous shares, one per workgroup, and dealt to
+// the workgroup's waves from a counter in LDS. Inside a CU the instruction arbiter favours older waves
+// (with a fixed per-wave split the first wave of each SIMD finished in ~60% of the time of the fourth).
+// An LDS atomic returns through lgkmcnt, never behind the HBM loads. (A pool of regions dealt by global
+// atomics to balance CUs against each other cost more than it won: same-address device atomics
+// serialise at ~11 ns, and their returns queue behind the CU's HBM loads.)
+constexpr uint64_t NO_REGION = ~0ull;
+
+__device__ __forceinline__ uint64_t take_region(uint32_t* lctr, uint64_t reg_lo, uint64_t count, uint32_t lane) {
   uint32_t v = 0;
-  if (lane == 0) v = atomicAdd(ctr, 1u);
-  return v;
-}
-__device__ __forceinline__ uint64_t ticket_region(uint32_t v, uint64_t reg_lo) {
-  return reg_lo + __builtin_amdgcn_readfirstlane(v);
+  if (lane == 0) v = atomicAdd(lctr, 1u);
+  v = __builtin_amdgcn_readfirstlane(v);
+  return v < count ? reg_lo + v : NO_REGION;
 }
 
 #ifdef LCRC_PROBE_CLOCK  // diagnostic build: per-workgroup shader/real clock stamps around the tile loop
@@ -295,13 +295,11 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
   const uint32_t lane = __lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t tid = threadIdx.x;
-  // this workgroup's share of the regions: [reg_lo, reg_hi); wave w starts on reg_lo + w, the rest by ticket
+  // this workgroup's share of the regions: [reg_lo, reg_lo + count)
   const uint64_t per = (nreg + gridDim.x - 1) / gridDim.x;
   const uint64_t reg_lo = (uint64_t)blockIdx.x * per;
-  const uint64_t reg_hi = reg_lo + per < nreg ? reg_lo + per : nreg;
-  uint64_t t = reg_lo + wave;
+  const uint64_t count = reg_lo < nreg ? (nreg - reg_lo < per ? nreg - reg_lo : per) : 0;
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long s_first = 0;
@@ -318,19 +316,18 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   // Table image, step 1: coalesced 16 B loads of the 24 KiB of source tables (slice T0..T3, Z64, then
   // Z256 .. Z2048 -- adjacent in the global image), completed BEFORE the first region's HBM loads are
   // issued: vector-memory returns reach a CU in issue order across its waves, so a table load issued
-  // after other waves' HBM loads would wait for all of them. (Per-entry gathers from the image took
-  // ~10 us: every wave instruction touched 32 lines, and all 256 CUs hammered the same 320 lines.)
+  // after other waves' HBM loads would wait for all of them (measured: tables ready at ~10 us).
   const u32x4* g_sl = (const u32x4*)(gtab + TAB_SLICE);
   const u32x4* g_z64 = (const u32x4*)(gtab + TAB_ZPIECE + 2048);
   const u32x4* g_zw = (const u32x4*)(gtab + TAB_ZWIN);
   const u32x4 src0 = tid < 256 ? g_sl[tid] : (tid < 512 ? g_z64[tid - 256] : g_zw[tid - 512]);
   u32x4 src1 = {0, 0, 0, 0};
   if (tid < 512) src1 = g_zw[512 + tid];
-#ifndef LCRC_FILL_BEHIND  // ablation build: old order (fill behind the HBM loads)
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __builtin_amdgcn_sched_barrier(0);
-#endif
+  // step 2: stage [slice | Z64 | Z256 | Z512 | Z1024 | Z2048] at A_STAGE (Z1024/Z2048 are already in their
+  // final place).
+  *(u32x4*)((char*)L + A_STAGE + (tid << 4)) = src0;
+  if (tid < 512) *(u32x4*)((char*)L + A_STAGE + 16384 + (tid << 4)) = src1;
+  __syncthreads();
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -338,18 +335,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   // lane (k, c) = (lane & 7, lane >> 3) reads piece 16*k + 8*h + c of every 2 KiB of the region
   const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
   u32x4 va[8], vb[8];
-  {
-    const __amdgpu_buffer_rsrc_t rs = region_rsrc(base, span, t, reg_hi);
-    load_half(va, rs, voff_a);
-    __builtin_amdgcn_sched_barrier(0);  // issue order va, vb: the loop's vmcnt bookkeeping assumes it
-    load_half(vb, rs, voff_b);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  // step 2: stage [slice | Z64 | Z256 | Z512 | Z1024 | Z2048] at A_STAGE (Z1024/Z2048 are already in their
-  // final place), then step 3: every thread writes 8 replicated 16 B chunks of the rotated sets
-  *(u32x4*)((char*)L + A_STAGE + (tid << 4)) = src0;
-  if (tid < 512) *(u32x4*)((char*)L + A_STAGE + 16384 + (tid << 4)) = src1;
-  lds_barrier();
+  // step 3: every thread writes 8 replicated 16 B chunks of the rotated sets
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -365,11 +351,20 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
       *(u32x4*)((char*)L + off) = u32x4{v, v, v, v};
     }
   }
-  if (tid == 0) wg_ticket = A_THREADS / 64;
+  if (tid == 0) wg_ticket = 0;
   lds_barrier();
-#ifndef LCRC_STATIC_SCHED
-  uint32_t tk = take_ticket(&wg_ticket, lane);
-#endif
+  // the first region's loads go out only now: a wave blocks at VMEM issue once its CU's queue is full,
+  // and issued earlier they kept waves from the replication above (tables ready at ~9 us instead of ~2)
+  uint64_t t = take_region(&wg_ticket, reg_lo, count, lane);
+  {
+    const __amdgpu_buffer_rsrc_t rs0 = region_rsrc(base, span, t, nreg);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half(va, rs0, voff_a);
+    __builtin_amdgcn_sched_barrier(0);  // issue order va, vb: the loop's vmcnt bookkeeping assumes it
+    load_half(vb, rs0, voff_b);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  uint64_t tn = take_region(&wg_ticket, reg_lo, count, lane);
 
   const Rot R = make_rot(lane);
 #ifdef LCRC_PROBE_CLOCK
@@ -381,13 +376,8 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   // va/vb hold the two halves of region t; walking a half refills it with the same half of region tn.
   // Chain a of the second half continues from the first half's register value, so one Z64 join per
   // half is the only recombination inside a window.
-  while (t < reg_hi) {
-#ifdef LCRC_STATIC_SCHED  // ablation build: wave w takes regions reg_lo + w, reg_lo + w + 16, ...
-    const uint64_t tn = t + A_THREADS / 64;
-#else
-    const uint64_t tn = ticket_region(tk, reg_lo);
-#endif
-    const __amdgpu_buffer_rsrc_t rsn = region_rsrc(base, span, tn, reg_hi);
+  while (t != NO_REGION) {
+    const __amdgpu_buffer_rsrc_t rsn = region_rsrc(base, span, tn, nreg);
     // expected values of this region's blocks, loaded ahead of the refills so that the verify at the
     // end of the iteration does not wait for them (vmcnt retires in issue order)
     uint32_t ev = 0;
@@ -401,12 +391,11 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     if (!s_first) s_first = __builtin_amdgcn_s_memrealtime();
 #endif
     __builtin_amdgcn_sched_barrier(0);
-#ifndef LCRC_STATIC_SCHED
-    tk = take_ticket(&wg_ticket, lane);
-#endif
+    const uint64_t tnn = take_region(&wg_ticket, reg_lo, count, lane);
     const uint32_t p = walk_half(L, R, vb, x, rsn, voff_b);
     finish_region<FINAL>(L, R, p, t, lane, out, nblk, fin, flags, expected, ev, mismatch);
     t = tn;
+    tn = tnn;
   }
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -414,7 +403,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     lcrc_dbg_clock[blockIdx.x * 4 + 0] = c1 - c0;
     lcrc_dbg_clock[blockIdx.x * 4 + 1] = r1 - r0;
   }
-  const uint64_t gw = (uint64_t)blockIdx.x * (A_THREADS / 64) + wave;
+  const uint64_t gw = (uint64_t)blockIdx.x * (A_THREADS / 64) + (threadIdx.x >> 6);
   if (lane == 0 && gw < 4096) {
     lcrc_dbg_stamp[gw * 8 + 0] = s_entry;
     lcrc_dbg_stamp[gw * 8 + 1] = r0;

@@ -1,3 +1,5 @@
 set -e
 export TMPDIR=/tmp
-for v in base; do echo "== $v"; LCRC_LIB_PATH=$PWD/tools/probe/variants/$v.so timeout -k 10 200 python tools/probe/stamps.py 65536 4096 | grep -v "xcd\|wave\|by "; done
+for s in 1 2; do LCRC_BENCH_PRE=1 timeout -k 10 200 python bench.py --config fixed --steps 50 --warmup 5 --no-cpu-baseline --streams $s | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('fixed streams', d['config']['streams'], d['value'], 'GiB/s', d['ms_per_step'], 'ms/step; roofline', d['roofline']['achieved'], d['roofline']['frac'], d['roofline']['launch_us'])"; done
+LCRC_BENCH_PRE=1 timeout -k 10 200 python bench.py --config fixed --steps 200 --warmup 5 --no-cpu-baseline --streams 1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('fixed streams', d['config']['streams'], d['value'], 'GiB/s', d['ms_per_step'], 'ms/step; roofline', d['roofline']['achieved'], d['roofline']['frac'], d['roofline']['launch_us'])"
+timeout -k 10 200 python tools/probe/size_sweep.py

@@ -13,7 +13,7 @@ MODE=${3:-c}
 OUT=gpurun_out/prof_${ROUND}_${CONFIG}_${MODE}
 rm -rf "$OUT"
 mkdir -p "$OUT" profiles
-BENCH="bench.py --config $CONFIG --mode $MODE --steps 20 --warmup 3 --no-cpu-baseline"
+BENCH="bench.py --config $CONFIG --mode $MODE --steps 20 --warmup 3 --no-cpu-baseline --streams 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH > "$OUT/write.log" 2>&1
