@@ -148,7 +148,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
     g_last_error = std::string("kernels are built for gfx950 only; device is ") + prop.gcnArchName;
     return bail(LCRC_ENODEV);
   }
-  ctx->grid_a = prop.multiProcessorCount;      // k_windows: 152 KiB LDS -> 1 workgroup per CU
+  ctx->grid_a = prop.multiProcessorCount;      // k_windows: CUs (the launcher scales by workgroups per CU)
   ctx->grid_b = prop.multiProcessorCount * 4;  // k_blocks: 40 KiB LDS -> 4 x 512-thread workgroups per CU
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return bail(fail_hip(e, "hipStreamCreate"));

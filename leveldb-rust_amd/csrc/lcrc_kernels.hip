@@ -43,16 +43,28 @@ namespace lcrc_dev {
 //   [128 KiB, 144 KiB): staging of the source tables during the fill.
 //   [144 KiB, 152 KiB): Z1024, Z2048 (unreplicated) for the two upper levels of the block tree.
 // ---------------------------------------------------------------------------------------------------
+#ifndef LCRC_WG1
+// Two 512-thread workgroups per CU (76 KiB each): only S0 and S1 are replicated (region 0); the tree's
+// Z256, Z512, Z1024 are unreplicated at A_ZT (its top level applies Z1024 twice). While one workgroup of
+// a CU is in its prologue or its tail, the other one computes -- also across consecutive launches.
+constexpr int A_WG_PER_CU = 2;
+constexpr int A_THREADS = 512;
+constexpr int A_REP_BYTES = 65536;
+constexpr int A_ZT = A_REP_BYTES;           // Z256, Z512, Z1024; fill staging (slice, Z64) before that
+constexpr int A_STAGE = A_ZT;
+constexpr int A_LDS_BYTES = A_ZT + 3 * 4096;
+#else
+// One 1024-thread workgroup per CU (152 KiB): S0..S3 replicated, staging, Z1024/Z2048 unreplicated.
+constexpr int A_WG_PER_CU = 1;
+constexpr int A_THREADS = 1024;
+constexpr int A_REP_BYTES = 131072;
 constexpr int A_STAGE = 131072;             // fill staging: slice, Z64, Z256, Z512 (dead after the fill),
 constexpr int A_ZUP = A_STAGE + 16384;      // then Z1024, Z2048 (live)
 constexpr int A_LDS_BYTES = A_ZUP + 2 * 4096;
-#ifndef LCRC_A_THREADS
-#define LCRC_A_THREADS 1024
+constexpr uint32_t SET_S2 = 1u << 16, SET_S3 = (1u << 16) | (1u << 7);
 #endif
-constexpr int A_THREADS = LCRC_A_THREADS;
-static_assert(A_THREADS == 1024, "the table fill maps one 16 B source chunk per thread");
 constexpr int REGION = 16384;  // bytes per wave iteration: two 8 KiB half-tiles, 64 windows of 256 B
-constexpr uint32_t SET_S1 = 1u << 7, SET_S2 = 1u << 16, SET_S3 = (1u << 16) | (1u << 7);
+constexpr uint32_t SET_S1 = 1u << 7;
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt(0)) but not for its
 // outstanding global loads -- __syncthreads() would add vmcnt(0) and expose the first tile's latency.
@@ -231,12 +243,19 @@ template <int M>
 __device__ __forceinline__ uint32_t tree_level(const void* L, const Rot& R, uint32_t p, uint32_t lane) {
   const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x100 + (1 << M), 0xF, 0xF, false);
   if ((lane & ((2u << M) - 1)) == 0) {
+#ifndef LCRC_WG1
+    if constexpr (M < 3)
+      p = zlook(L, A_ZT + M * 4096, p) ^ pn;
+    else
+      p = zlook(L, A_ZT + 2 * 4096, zlook(L, A_ZT + 2 * 4096, p)) ^ pn;  // Z2048 = Z1024 o Z1024
+#else
     if constexpr (M == 0)
       p = zrot<SET_S2>(L, R, p) ^ pn;
     else if constexpr (M == 1)
       p = zrot<SET_S3>(L, R, p) ^ pn;
     else
       p = zlook(L, A_ZUP + (M - 2) * 4096, p) ^ pn;
+#endif
   }
   return p;
 }
@@ -320,6 +339,16 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   const u32x4* g_sl = (const u32x4*)(gtab + TAB_SLICE);
   const u32x4* g_z64 = (const u32x4*)(gtab + TAB_ZPIECE + 2048);
   const u32x4* g_zw = (const u32x4*)(gtab + TAB_ZWIN);
+#ifndef LCRC_WG1
+  static_assert(A_THREADS == 512, "the table fill maps one 16 B source chunk per thread");
+  const u32x4 src0 = tid < 256 ? g_sl[tid] : g_z64[tid - 256];  // slice, Z64
+  const u32x4 zs0 = g_zw[tid];                                   // Z256, Z512
+  u32x4 zs1 = {0, 0, 0, 0};
+  if (tid < 256) zs1 = g_zw[512 + tid];                          // Z1024
+  // step 2: stage [slice | Z64] at A_STAGE
+  *(u32x4*)((char*)L + A_STAGE + (tid << 4)) = src0;
+#else
+  static_assert(A_THREADS == 1024, "the table fill maps one 16 B source chunk per thread");
   const u32x4 src0 = tid < 256 ? g_sl[tid] : (tid < 512 ? g_z64[tid - 256] : g_zw[tid - 512]);
   u32x4 src1 = {0, 0, 0, 0};
   if (tid < 512) src1 = g_zw[512 + tid];
@@ -327,6 +356,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   // final place).
   *(u32x4*)((char*)L + A_STAGE + (tid << 4)) = src0;
   if (tid < 512) *(u32x4*)((char*)L + A_STAGE + 16384 + (tid << 4)) = src1;
+#endif
   __syncthreads();
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
@@ -340,7 +370,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
 #endif
   {
-    constexpr int FILL = 131072 / 16 / A_THREADS;  // 16 B chunks of the replicated sets per thread
+    constexpr int FILL = A_REP_BYTES / 16 / A_THREADS;  // 16 B chunks of the replicated sets per thread
     const uint32_t* stage = (const uint32_t*)((const char*)L + A_STAGE);
 #pragma unroll
     for (int k = 0; k < FILL; ++k) {
@@ -351,6 +381,11 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
       *(u32x4*)((char*)L + off) = u32x4{v, v, v, v};
     }
   }
+#ifndef LCRC_WG1
+  lds_barrier();  // the staging area becomes the tree's tables
+  *(u32x4*)((char*)L + A_ZT + (tid << 4)) = zs0;
+  if (tid < 256) *(u32x4*)((char*)L + A_ZT + 8192 + (tid << 4)) = zs1;
+#endif
   if (tid == 0) wg_ticket = 0;
   lds_barrier();
   // the first region's loads go out only now: a wave blocks at VMEM issue once its CU's queue is full,
@@ -743,6 +778,7 @@ hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, u
                                const uint32_t* expected, uint32_t* mismatch, hipStream_t st) {
   const uint64_t nreg = (span + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
   if (nreg == 0) return hipSuccess;
+  grid *= lcrc_dev::A_WG_PER_CU;  // `grid` = CUs
   uint64_t need = (nreg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
   int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   if (final_mode)
