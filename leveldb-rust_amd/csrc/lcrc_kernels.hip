@@ -289,7 +289,9 @@ __device__ __forceinline__ void finish_region(const void* L, const Rot& R, uint3
 // (with a fixed per-wave split the first wave of each SIMD finished in ~60% of the time of the fourth).
 // An LDS atomic returns through lgkmcnt, never behind the HBM loads. (A pool of regions dealt by global
 // atomics to balance CUs against each other cost more than it won: same-address device atomics
-// serialise at ~11 ns, and their returns queue behind the CU's HBM loads.)
+// serialise at ~11 ns, and their returns queue behind the CU's HBM loads. Raising the issue priority of
+// the workgroup that is further behind, with s_setprio, evened out the two workgroups of a CU without
+// shortening the launch.)
 constexpr uint64_t NO_REGION = ~0ull;
 
 __device__ __forceinline__ uint64_t take_region(uint32_t* lctr, uint64_t reg_lo, uint64_t count, uint32_t lane) {
