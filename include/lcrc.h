@@ -24,6 +24,12 @@
  *                                          kernel, D2H, double-buffered)
  *   lcrc_wal_scan                       <- the header parse + CRC verify of (2) for every physical record
  *                                          of a device-resident log file, 32 KiB block by block
+ *   lcrc_table_scan                     <- Table::open with paranoid_checks (table.rs:39-103) followed by
+ *                                          read_block_from_file(verify_checksum) (format.rs:146-171) of
+ *                                          every data, filter, metaindex and index block: one batched verify
+ *   lcrc_batch_seal                     <- (1)/(3) for a batch: the trailer CRCs of write_raw_block
+ *                                          (table.rs:519-527) or the header CRCs of emit_physical_record
+ *                                          (log.rs:61-70), computed and stored in place on the device
  *
  * Conventions: plain pointers and sizes, no exceptions cross the boundary, every call returns an int
  * status (LCRC_OK = 0). Buffers are owned by the caller. A context is bound to one device and one mode;
@@ -47,6 +53,8 @@ extern "C" {
 #define LCRC_ENODEV (-2)  /* no HIP device / kernel image unavailable */
 #define LCRC_EHIP (-3)    /* HIP runtime error (see lcrc_last_error) */
 #define LCRC_ENOMEM (-4)  /* device or pinned allocation failed */
+#define LCRC_ECORRUPT (-5) /* lcrc_table_scan: the table structure is corrupt (message in err) */
+#define LCRC_ERANGE (-6)  /* output capacity too small; the count needed is returned */
 
 /* ---- CRC modes ---- */
 #define LCRC_MODE_REF 0 /* CRC-32/ISO-HDLC, refl. poly 0xEDB88320: bit-exact with crc32fast::Hasher */
@@ -140,6 +148,44 @@ int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32
  * max_recs); *n_recs (host) receives the count. Returns LCRC_EINVAL if max_recs is too small. */
 int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs,
                   size_t max_recs, size_t* n_recs, void* stream);
+
+/* One block of an SSTable located by lcrc_table_scan (host struct, 24 B). */
+typedef struct lcrc_tblk {
+  uint64_t offset;  /* BlockHandle offset */
+  uint64_t size;    /* BlockHandle size n; the 5-byte trailer [type][crc] follows */
+  uint32_t crc;     /* computed CRC of data[0..n+1] (masked if LCRC_FLAG_MASK) */
+  uint8_t kind;     /* LCRC_TBLK_DATA / _FILTER / _METAINDEX / _INDEX */
+  uint8_t type;     /* stored type byte data[n] (0 raw, 1 snappy, other: "bad block type" on read) */
+  uint8_t status;   /* LCRC_TBLK_OK / _CRC_MISMATCH / _TRUNCATED */
+  uint8_t reserved;
+} lcrc_tblk;
+#define LCRC_TBLK_DATA 0
+#define LCRC_TBLK_FILTER 1
+#define LCRC_TBLK_METAINDEX 2
+#define LCRC_TBLK_INDEX 3
+#define LCRC_TBLK_OK 0
+#define LCRC_TBLK_CRC_MISMATCH 1 /* read_block_from_file(verify) -> "block checksum mismatch" */
+#define LCRC_TBLK_TRUNCATED 2    /* handle past the end of the file -> "truncated block read" */
+
+/* Whole-table verify scan of a device-resident SSTable file (file_len bytes). The host reads the footer
+ * and the index block (verified: paranoid_checks), and -- when filter_name is non-NULL, as read_meta does
+ * for a filter policy -- the metaindex block and the "filter" + filter_name entry; then ONE batched
+ * device pass checksums every data, filter, metaindex and index block. blocks (host, capacity
+ * max_blocks) receives them sorted by offset; *n_blocks the count (LCRC_ERANGE if it exceeds
+ * max_blocks; blocks may be NULL to query). Structural corruption returns LCRC_ECORRUPT with the
+ * reference's message ("file is too short to be an sstable", "not an sstable (bad magic number)",
+ * "block checksum mismatch", "bad block type", "corrupted compressed block content", "bad block
+ * contents", "bad entry in block", "truncated block read", "Error when decoding varint64") copied to
+ * err (capacity err_cap, may be NULL). Synchronous. */
+int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
+                    lcrc_tblk* blocks, size_t max_blocks, size_t* n_blocks, char* err, size_t err_cap);
+
+/* Writer side, for a batch: CRC of every descriptor (masked if LCRC_FLAG_MASK) stored little-endian at
+ * base[offset + expect_rel] in place (device). SSTable block: {off, n + 1, n + 1} writes the trailer crc;
+ * WAL record with header at h: {h + 6, 1 + len, -6} writes the header crc. out_crc (device, nullable)
+ * also receives the values. Covered ranges must not contain another descriptor's CRC slot. */
+int lcrc_batch_seal(lcrc_ctx* ctx, uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
+                    uint32_t* out_crc, void* stream);
 
 /* ---- device memory helpers (so a binding needs nothing but this library) ---- */
 int lcrc_dev_alloc(int device, size_t bytes, void** out);

@@ -11,6 +11,9 @@ ctypes and mirrors the reference's interfaces for the checksum path:
   ``NoDeviceError`` when no gfx950 device/kernel image is available (there is no CPU fallback)
 * ``LogWriter`` / ``LogReader`` / ``BatchLogReader`` -- src/db/log.rs LogWriter / LogReader
 * ``TableFile`` -- write_raw_block (table.rs:507-529) and read_block_from_file (format.rs:146-213)
+* ``Engine.table_scan`` -- Table::open(paranoid) + verify of every block (table.rs:39-103, format.rs:146-171)
+* ``Engine.batch_seal`` -- batched trailer / WAL-header CRCs stored in place (table.rs:519-527, log.rs:61-70)
+* ``snappy_frame_decode`` -- the Snappy framing decoder the table walk uses for compressed index blocks
 """
 import ctypes
 import os
@@ -26,7 +29,7 @@ FLAG_MASK = 0x1
 FLAG_DIRECT = 0x2
 NO_EXPECT = -0x80000000
 
-OK, EINVAL, ENODEV, EHIP, ENOMEM = 0, -1, -2, -3, -4
+OK, EINVAL, ENODEV, EHIP, ENOMEM, ECORRUPT, ERANGE = 0, -1, -2, -3, -4, -5, -6
 
 WAL_OK, WAL_CRC_MISMATCH = 0, 1
 WAL_STOP_TRAILER, WAL_STOP_BAD_LENGTH, WAL_STOP_ZERO = 0, 1, 2
@@ -40,11 +43,19 @@ class LcrcError(RuntimeError):
     pass
 
 
+class TableCorruption(LcrcError):
+    """lcrc_table_scan found the table structure corrupt; str() is the reference's message."""
+
+
 class NoDeviceError(LcrcError):
     pass
 
 
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("expect_rel", "<i4")])
+TBLK_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u8"), ("crc", "<u4"), ("kind", "u1"), ("type", "u1"),
+                       ("status", "u1"), ("reserved", "u1")])
+TBLK_DATA, TBLK_FILTER, TBLK_METAINDEX, TBLK_INDEX = 0, 1, 2, 3
+TBLK_OK, TBLK_CRC_MISMATCH, TBLK_TRUNCATED = 0, 1, 2
 WAL_REC_DTYPE = np.dtype([("header", "<u8"), ("length", "<u4"), ("type", "u1"), ("status", "u1"),
                           ("block_end", "<u2"), ("crc", "<u4"), ("stop", "<u4")])
 
@@ -71,6 +82,7 @@ ABI_SYMBOLS = [
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_host_uniform", "lcrc_wal_scan",
+    "lcrc_table_scan", "lcrc_batch_seal",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
     "lcrc_last_error", "lcrc_version",
@@ -114,6 +126,9 @@ def lib():
     sig("lcrc_batch_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, vp)
     sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
     sig("lcrc_wal_scan", i32, vp, vp, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp)
+    sig("lcrc_table_scan", i32, vp, vp, u64, cp, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp, sz)
+    sig("lcrc_batch_seal", i32, vp, vp, u64, vp, sz, vp, vp)
+    sig("lcrc_snappy_frame_decode", ctypes.c_int64, vp, sz, vp, sz)
     sig("lcrc_dev_alloc", i32, i32, sz, ctypes.POINTER(vp))
     sig("lcrc_dev_free", i32, vp)
     sig("lcrc_host_alloc_pinned", i32, sz, ctypes.POINTER(vp))
@@ -387,6 +402,30 @@ class Engine:
             recs_dev.close()
         return out
 
+    def table_scan(self, file_dev, file_len, filter_name=None):
+        """Whole-table verify scan of a device-resident SSTable. Returns a TBLK_DTYPE array sorted by
+        offset; raises TableCorruption(reference message) when the structure is corrupt."""
+        n = ctypes.c_size_t(0)
+        err = ctypes.create_string_buffer(256)
+        fname = filter_name.encode() if isinstance(filter_name, str) else filter_name
+        rc = lib().lcrc_table_scan(self.ctx, _ptr(file_dev), int(file_len), fname, None, 0, ctypes.byref(n), err, 256)
+        if rc == ECORRUPT:
+            raise TableCorruption(err.value.decode())
+        if rc != ERANGE:
+            _check(rc, "lcrc_table_scan")
+        out = np.zeros(n.value, TBLK_DTYPE)
+        rc = lib().lcrc_table_scan(self.ctx, _ptr(file_dev), int(file_len), fname,
+                                   out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n), err, 256)
+        if rc == ECORRUPT:
+            raise TableCorruption(err.value.decode())
+        _check(rc, "lcrc_table_scan")
+        return out
+
+    def batch_seal(self, base, base_len, descs, n, out_crc=None, stream=None):
+        """Compute each descriptor's CRC and store it at base[offset + expect_rel] (device, in place)."""
+        _check(lib().lcrc_batch_seal(self.ctx, _ptr(base), int(base_len), _ptr(descs), int(n), _ptr(out_crc), stream),
+               "lcrc_batch_seal")
+
     def timer_start(self):
         _check(lib().lcrc_timer_start(self.ctx), "lcrc_timer_start")
 
@@ -552,3 +591,15 @@ class TableFile:
             lib().lcrc_tbl_destroy(self._t)
         except Exception:
             pass
+
+
+def snappy_frame_decode(data):
+    """Snappy framing decoder of the table walk (host): bytes, or None when corrupt."""
+    data = bytes(data)
+    buf = ctypes.create_string_buffer(data, len(data)) if data else None
+    n = lib().lcrc_snappy_frame_decode(buf, len(data), None, 0)
+    if n < 0:
+        return None
+    out = ctypes.create_string_buffer(max(1, n))
+    lib().lcrc_snappy_frame_decode(buf, len(data), out, n)
+    return out.raw[:n]

@@ -15,6 +15,7 @@
 #include "../../include/lcrc.h"
 #include "lcrc_device.h"
 #include "lcrc_math.h"
+#include "lcrc_table.h"
 
 extern "C" {
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
@@ -26,6 +27,9 @@ hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint6
                               uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch, hipStream_t st);
 hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
                                  const uint64_t* offsets, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
+                                 hipStream_t st);
+hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
+hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
 hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, uint64_t n, const uint32_t* crcs, const uint32_t* mismatch,
                                   hipStream_t st);
@@ -95,6 +99,10 @@ struct lcrc_ctx {
   DevBuf<uint64_t> wal_offsets;
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs, wal_mm;
+  DevBuf<lcrc_desc_dev> tbl_descs;  // table scan / seal
+  DevBuf<uint32_t> tbl_crcs, tbl_mm;
+  DevBuf<uint64_t> tbl_pos;
+  DevBuf<uint8_t> tbl_types;
 };
 
 namespace {
@@ -193,6 +201,11 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->wal_descs.release();
   ctx->wal_crcs.release();
   ctx->wal_mm.release();
+  ctx->tbl_descs.release();
+  ctx->tbl_crcs.release();
+  ctx->tbl_mm.release();
+  ctx->tbl_pos.release();
+  ctx->tbl_types.release();
   if (ctx->d_tab) (void)hipFree(ctx->d_tab);
   if (ctx->t0) (void)hipEventDestroy(ctx->t0);
   if (ctx->t1) (void)hipEventDestroy(ctx->t1);
@@ -393,6 +406,147 @@ int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wa
   ctx->flags = saved;
   if (rc) return rc;
   HIPCHK(lcrc_launch_wal_finish((lcrc_wal_rec_dev*)recs, total, ctx->wal_crcs.p, ctx->wal_mm.p, st));
+  return LCRC_OK;
+}
+
+// ---- whole-table verify scan ----
+int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
+                    lcrc_tblk* blocks, size_t max_blocks, size_t* n_blocks, char* err, size_t err_cap) {
+  using namespace lcrc_tbl;
+  if (!ctx || !n_blocks || (file_len && !file)) return LCRC_EINVAL;
+  *n_blocks = 0;
+  if (err && err_cap) err[0] = 0;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  auto corrupt = [&](const char* msg) {
+    if (err && err_cap) {
+      strncpy(err, msg, err_cap - 1);
+      err[err_cap - 1] = 0;
+    }
+    return LCRC_ECORRUPT;
+  };
+  // the host reads only what locates the blocks: footer, index block, metaindex block
+  auto read_raw = [&](const Handle& h, std::vector<uint8_t>& raw) -> const char* {
+    if (h.offset > file_len || h.size + BLOCK_TRAILER_SIZE > file_len - h.offset) return "truncated block read";
+    raw.resize(h.size + BLOCK_TRAILER_SIZE);
+    if (hipMemcpy(raw.data(), file + h.offset, raw.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return "device read failed";
+    return nullptr;
+  };
+  if (file_len < FOOTER_ENCODED_LENGTH) return corrupt("file is too short to be an sstable");
+  uint8_t footer[FOOTER_ENCODED_LENGTH];
+  HIPCHK(hipMemcpy(footer, file + file_len - FOOTER_ENCODED_LENGTH, FOOTER_ENCODED_LENGTH, hipMemcpyDeviceToHost));
+  Handle meta_h, index_h;
+  if (const char* e = decode_footer(footer, meta_h, index_h)) return corrupt(e);
+
+  std::vector<lcrc_tblk> found;
+  auto add = [&](const Handle& h, uint8_t kind) {
+    lcrc_tblk b;
+    memset(&b, 0, sizeof(b));
+    b.offset = h.offset;
+    b.size = h.size;
+    b.kind = kind;
+    found.push_back(b);
+  };
+  // Table::open: the index block is read with verify_checksum = paranoid_checks (true here)
+  std::vector<uint8_t> raw, contents;
+  if (const char* e = read_raw(index_h, raw)) return corrupt(e);
+  if (const char* e = block_contents(raw.data(), index_h.size, true, ctx->mode, ctx->flags, contents))
+    return corrupt(e);
+  const char* herr = nullptr;
+  const char* berr = block_entries(contents, [&](const std::string&, const uint8_t* v, uint32_t vn) {
+    Handle h;
+    const uint8_t* p = v;
+    if ((herr = decode_handle(p, v + vn, h))) return false;
+    add(h, LCRC_TBLK_DATA);
+    return true;
+  });
+  if (berr) return corrupt(berr);
+  if (herr) return corrupt(herr);
+  // read_meta: only with a filter policy, and its errors are not propagated (table.rs:81-103)
+  if (filter_name && !read_raw(meta_h, raw) &&
+      !block_contents(raw.data(), meta_h.size, true, ctx->mode, ctx->flags, contents)) {
+    const std::string want = std::string("filter") + filter_name;
+    block_entries(contents, [&](const std::string& key, const uint8_t* v, uint32_t vn) {
+      if (key < want) return true;  // seek: first key >= want
+      Handle h;
+      const uint8_t* p = v;
+      if (key == want && !decode_handle(p, v + vn, h)) add(h, LCRC_TBLK_FILTER);
+      return false;
+    });
+  }
+  add(meta_h, LCRC_TBLK_METAINDEX);
+  add(index_h, LCRC_TBLK_INDEX);
+  std::stable_sort(found.begin(), found.end(),
+                   [](const lcrc_tblk& a, const lcrc_tblk& b) { return a.offset < b.offset; });
+  const size_t n = found.size();
+  *n_blocks = n;
+  if (!blocks || max_blocks < n) return LCRC_ERANGE;
+
+  // ONE batched pass over the file for every block in range
+  std::vector<lcrc_desc_dev> descs;
+  std::vector<uint64_t> pos;
+  std::vector<size_t> which;
+  for (size_t i = 0; i < n; ++i) {
+    lcrc_tblk& b = found[i];
+    if (b.offset > file_len || b.size + BLOCK_TRAILER_SIZE > file_len - b.offset || b.size + 1 > 0xFFFFFFFFull) {
+      b.status = LCRC_TBLK_TRUNCATED;
+      b.type = 0xFF;
+      continue;
+    }
+    lcrc_desc_dev d;
+    d.offset = b.offset;
+    d.length = (uint32_t)(b.size + 1);
+    d.expect_rel = (int32_t)(b.size + 1);
+    if ((uint64_t)d.expect_rel != b.size + 1) d.expect_rel = LCRC_NO_EXPECT_DEV;  // > 2 GiB block
+    descs.push_back(d);
+    pos.push_back(b.offset + b.size);
+    which.push_back(i);
+  }
+  const size_t m = descs.size();
+  if (m) {
+    if ((rc = ctx->tbl_descs.ensure(m)) || (rc = ctx->tbl_crcs.ensure(m)) || (rc = ctx->tbl_mm.ensure((m + 31) / 32)) ||
+        (rc = ctx->tbl_pos.ensure(m)) || (rc = ctx->tbl_types.ensure(m)))
+      return rc;
+    HIPCHK(hipMemcpyAsync(ctx->tbl_descs.p, descs.data(), m * sizeof(lcrc_desc_dev), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(ctx->tbl_pos.p, pos.data(), m * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    if ((rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->tbl_descs.p, m, ctx->tbl_crcs.p, ctx->tbl_mm.p,
+                         st)))
+      return rc;
+    HIPCHK(lcrc_launch_gather_u8(file, ctx->tbl_pos.p, m, ctx->tbl_types.p, st));
+    std::vector<uint32_t> crcs(m), mm((m + 31) / 32);
+    std::vector<uint8_t> types(m);
+    HIPCHK(hipMemcpyAsync(crcs.data(), ctx->tbl_crcs.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(mm.data(), ctx->tbl_mm.p, mm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(types.data(), ctx->tbl_types.p, m, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (size_t k = 0; k < m; ++k) {
+      lcrc_tblk& b = found[which[k]];
+      b.crc = crcs[k];
+      b.type = types[k];
+      b.status = ((mm[k >> 5] >> (k & 31)) & 1) ? LCRC_TBLK_CRC_MISMATCH : LCRC_TBLK_OK;
+    }
+  }
+  memcpy(blocks, found.data(), n * sizeof(lcrc_tblk));
+  return LCRC_OK;
+}
+
+// ---- writer side: batch seal ----
+int lcrc_batch_seal(lcrc_ctx* ctx, uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
+                    uint32_t* out_crc, void* stream) {
+  if (!ctx || (n && (!descs || !base))) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  if (n == 0) return LCRC_OK;
+  hipStream_t st = pick_stream(ctx, stream);
+  uint32_t* crc = out_crc;
+  if (!crc) {
+    if ((rc = ctx->tbl_crcs.ensure(n))) return rc;
+    crc = ctx->tbl_crcs.p;
+  }
+  if ((rc = lcrc_batch(ctx, base, base_len, descs, n, crc, nullptr, st))) return rc;
+  HIPCHK(lcrc_launch_store_crc(base, (const lcrc_desc_dev*)descs, crc, n, st));
   return LCRC_OK;
 }
 

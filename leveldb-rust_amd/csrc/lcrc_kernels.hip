@@ -280,7 +280,7 @@ __device__ __forceinline__ void finish_region(const void* L, const Rot& R, uint3
     uint32_t crc = p ^ fin;
     if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
     out[blk] = crc;
-    if (expected && ev != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
+    if (expected && mismatch && ev != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
   }
 }
 
@@ -524,11 +524,16 @@ __device__ uint32_t row_walk(const uint32_t* L, const RowPiece& p, bool empty_ra
     rr = step4(L, rr, p.w.w);
     cv = rr;
   } else if (p.kind == 2) {
-    // bytes [first, 16) walked from R0 (1..15 of them)
+    // bytes [first, 16) walked from R0 (1..15 of them): the bytes up to the next word boundary one at a
+    // time, then whole words -- at most 3 + 3 dependent steps instead of 15
     uint32_t rr = R0;
+    const uint32_t fw = (p.first + 3) >> 2;  // first whole word
 #pragma unroll
     for (int i = 1; i < 16; ++i)
-      if ((uint32_t)i >= p.first) rr = byte_step(L, rr, (p.w[i >> 2] >> (8 * (i & 3))) & 0xff);
+      if ((uint32_t)i >= p.first && (uint32_t)i < 4 * fw) rr = byte_step(L, rr, (p.w[i >> 2] >> (8 * (i & 3))) & 0xff);
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+      if ((uint32_t)q >= fw) rr = step4(L, rr, p.w[q]);
     cv = rr;
   }
   // row tree: level m joins lane g with g + 2^m, shifting the left part by 16*2^m bytes
@@ -667,7 +672,7 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
         const int64_t xp = (int64_t)s + xrel;
         bad = (xp < 0 || (uint64_t)xp + 4 > base_len) ? true : load_le32(base + xp) != crc;
       }
-      if (bad) atomicOr(&mismatch[i >> 5], 1u << (i & 31));
+      if (bad && mismatch) atomicOr(&mismatch[i >> 5], 1u << (i & 31));
     }
   }
 }
@@ -743,6 +748,32 @@ __global__ void __launch_bounds__(256) k_wal_finish(lcrc_wal_rec_dev* __restrict
   recs[i].status = (mismatch[i >> 5] >> (i & 31)) & 1;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// small helpers of the table scan and the writer-side seal
+// ---------------------------------------------------------------------------------------------------
+// out[i] = base[pos[i]] (the type bytes of a table's blocks)
+__global__ void __launch_bounds__(256) k_gather_u8(const uint8_t* __restrict__ base, const uint64_t* __restrict__ pos,
+                                                   uint64_t n, uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = base[pos[i]];
+}
+
+// base[offset_i + expect_rel_i .. +4) = crc_i, little-endian: the trailer of write_raw_block
+// (table.rs:519-527) or the header checksum of emit_physical_record (log.rs:61-70), in place
+__global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, const lcrc_desc_dev* __restrict__ descs,
+                                                   const uint32_t* __restrict__ crc, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const lcrc_desc_dev d = descs[i];
+  if (d.expect_rel == LCRC_NO_EXPECT_DEV) return;
+  uint8_t* p = base + (int64_t)d.offset + d.expect_rel;
+  const uint32_t c = crc[i];
+  p[0] = (uint8_t)c;
+  p[1] = (uint8_t)(c >> 8);
+  p[2] = (uint8_t)(c >> 16);
+  p[3] = (uint8_t)(c >> 24);
+}
+
 }  // namespace lcrc_dev
 
 // ---------------------------------------------------------------------------------------------------
@@ -816,6 +847,19 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
   int g = (int)((nblocks + 255) / 256);
   hipLaunchKernelGGL(lcrc_dev::k_wal_parse, dim3(g), dim3(256), 0, st, file, file_len, nblocks, counts, offsets, recs,
                      descs);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_gather_u8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, pos, n, out);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
+                                 hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_store_crc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, descs, crc, n);
   return hipGetLastError();
 }
 

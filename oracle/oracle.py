@@ -272,3 +272,355 @@ def read_block(file_bytes, offset, n, verify):
     if d[n] not in (0, 1):
         return None, "bad block type"
     return d[n], None
+
+
+# ---------------------------------------------------------------------------------------------------
+# SSTable files (test infrastructure): a restatement of the reference's table writer and the walk of
+# Table::open + read_meta + per-block verify, to generate scan inputs and the expected verdicts.
+#   BlockBuilder::add / finish      <- src/sstable/block.rs:320-370
+#   TableBuilder::add / flush / finish <- src/sstable/table.rs:315-454 (filter-type quirk :383-391)
+#   write_block / write_raw_block   <- src/sstable/table.rs:470-529 (snappy kept iff < raw - raw/8)
+#   Footer / BlockHandle            <- src/sstable/format.rs:24-118; varints util/coding.rs
+#   BitWiseComparator separators    <- the bytewise FindShortestSeparator / FindShortSuccessor contract
+#   Snappy framing + raw format     <- the published Snappy formats (snap crate absent)
+# ---------------------------------------------------------------------------------------------------
+TABLE_MAGIC = 0xdb4775248b80fb57
+FOOTER_LEN = 48
+
+
+def varint(v):
+    out = bytearray()
+    while v >= 128:
+        out.append((v & 127) | 128)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def block_build(entries, restart_interval=16):
+    """entries: [(key bytes, value bytes)] in key order -> block contents (block.rs:320-370)."""
+    buf, restarts, last, counter = bytearray(), [0], b"", 0
+    for key, value in entries:
+        shared = 0
+        if counter < restart_interval:
+            while shared < min(len(last), len(key)) and last[shared] == key[shared]:
+                shared += 1
+        else:
+            restarts.append(len(buf))
+            counter = 0
+        buf += varint(shared) + varint(len(key) - shared) + varint(len(value)) + key[shared:] + value
+        counter += 1
+        last = key
+    for r in restarts:
+        buf += _le32(r)
+    buf += _le32(len(restarts))
+    return bytes(buf)
+
+
+def shortest_separator(start, limit):
+    n = min(len(start), len(limit))
+    i = 0
+    while i < n and start[i] == limit[i]:
+        i += 1
+    if i < n:
+        b = start[i]
+        if b < 0xFF and b + 1 < limit[i]:
+            return start[:i] + bytes([b + 1])
+    return start
+
+
+def short_successor(key):
+    for i, b in enumerate(key):
+        if b != 0xFF:
+            return key[:i] + bytes([b + 1])
+    return key
+
+
+def snappy_compress_raw(data):
+    """A valid (greedy, 4-byte-hash) Snappy raw encoding: literals and 2-byte-offset copies."""
+    data = bytes(data)
+    out = bytearray(varint(len(data)))
+    table, i, lit = {}, 0, 0
+
+    def literal(a, b):
+        while a < b:
+            n = min(b - a, 1 << 16)
+            if n <= 60:
+                out.append((n - 1) << 2)
+            elif n <= 256:
+                out.extend([60 << 2, n - 1])
+            else:
+                out.extend([61 << 2, (n - 1) & 0xFF, (n - 1) >> 8])
+            out.extend(data[a:a + n])
+            a += n
+
+    while i + 4 <= len(data):
+        k = data[i:i + 4]
+        j = table.get(k)
+        table[k] = i
+        if j is not None and i - j < 65536:
+            n = 4
+            while i + n < len(data) and data[j + n] == data[i + n] and n < 64:
+                n += 1
+            literal(lit, i)
+            off = i - j
+            out.extend([((n - 1) << 2) | 2, off & 0xFF, off >> 8])
+            i += n
+            lit = i
+        else:
+            i += 1
+    literal(lit, len(data))
+    return bytes(out)
+
+
+def snappy_frame_encode(data):
+    """Snappy framing: stream identifier, then <= 64 KiB chunks [type][u24 len][masked crc32c][body]."""
+    out = bytearray(b"\xff\x06\x00\x00sNaPpY")
+    for a in range(0, len(data), 65536):
+        chunk = bytes(data[a:a + 65536])
+        c = _le32(mask(crc(chunk, 1)))
+        z = snappy_compress_raw(chunk)
+        typ, body = (0, c + z) if len(z) < len(chunk) - len(chunk) // 8 else (1, c + chunk)
+        out += bytes([typ, len(body) & 0xFF, (len(body) >> 8) & 0xFF, len(body) >> 16]) + body
+    return bytes(out)
+
+
+def table_build(kvs, block_size=4096, restart_interval=16, compression=0, filter_name=None, filter_block=b"",
+                mode=0, masked=False):
+    """TableBuilder over sorted kvs -> (file bytes, [(offset, size, kind)]); kind 0 data, 1 filter,
+    2 metaindex, 3 index. Trailer CRCs in `mode` (0 = crc32fast, the reference), optionally masked."""
+    f = bytearray()
+    blocks = []
+
+    def raw_write(content, typ, kind):
+        off = len(f)
+        c = crc(bytes(content) + bytes([typ]), mode)
+        if masked:
+            c = mask(c)
+        f.extend(content)
+        f.append(typ)
+        f.extend(_le32(c))
+        blocks.append((off, len(content), kind))
+        return off, len(content)
+
+    def write_block(raw, kind):
+        if compression == 1:
+            z = snappy_frame_encode(raw)
+            if len(z) < len(raw) - len(raw) // 8:
+                return raw_write(z, 1, kind)
+        return raw_write(raw, 0, kind)
+
+    data, index, pending, last_key = [], [], None, b""
+    for key, value in kvs:
+        if pending is not None:
+            index.append((shortest_separator(last_key, key), varint(pending[0]) + varint(pending[1])))
+            pending = None
+        data.append((key, value))
+        last_key = key
+        est = len(block_build(data, restart_interval))
+        if est >= block_size:
+            pending = write_block(block_build(data, restart_interval), 0)
+            data = []
+    if data:
+        pending = write_block(block_build(data, restart_interval), 0)
+    meta = []
+    if filter_name is not None:
+        fh = raw_write(filter_block, compression, 1)  # the reference's quirk: type = options.compression_type
+        meta.append((b"filter" + filter_name.encode(), varint(fh[0]) + varint(fh[1])))
+    mh = write_block(block_build(meta, restart_interval), 2)
+    if pending is not None:
+        index.append((short_successor(last_key), varint(pending[0]) + varint(pending[1])))
+    ih = write_block(block_build(index, restart_interval), 3)
+    foot = bytearray(varint(mh[0]) + varint(mh[1]) + varint(ih[0]) + varint(ih[1]))
+    foot += bytes(40 - len(foot)) + _le32(TABLE_MAGIC & 0xFFFFFFFF) + _le32(TABLE_MAGIC >> 32)
+    f += foot
+    return bytes(f), blocks
+
+
+def _get_varint(buf, p, limit, bits):
+    result, shift = 0, 0
+    while shift <= bits - 4:
+        if p >= limit:
+            return None, p
+        b = buf[p]
+        p += 1
+        result |= (b & 127) << shift
+        if not b & 128:
+            return result, p
+        shift += 7
+    return None, p
+
+
+def snappy_frame_decode(data):
+    """Pure-Python Snappy framing decode with chunk CRC check; None when corrupt."""
+    data, p, out, seen = bytes(data), 0, bytearray(), False
+    while p < len(data):
+        if len(data) - p < 4:
+            return None
+        typ, n = data[p], data[p + 1] | (data[p + 2] << 8) | (data[p + 3] << 16)
+        p += 4
+        if len(data) - p < n:
+            return None
+        body, p = data[p:p + n], p + n
+        if typ == 0xFF:
+            if body != b"sNaPpY":
+                return None
+            seen = True
+            continue
+        if not seen:
+            return None
+        if typ in (0, 1):
+            if n < 4:
+                return None
+            want = int.from_bytes(body[:4], "little")
+            chunk = body[4:] if typ == 1 else _snappy_raw(body[4:])
+            if chunk is None or len(chunk) > 65536 or mask(crc(chunk, 1)) != want:
+                return None
+            out += chunk
+        elif typ <= 0x7F:
+            return None
+    return bytes(out)
+
+
+def _snappy_raw(z):
+    ulen, p = _get_varint(z, 0, len(z), 32)
+    if ulen is None:
+        return None
+    out = bytearray()
+    while p < len(z):
+        tag = z[p]
+        p += 1
+        t = tag & 3
+        if t == 0:
+            n = tag >> 2
+            if n >= 60:
+                nb = n - 59
+                if len(z) - p < nb:
+                    return None
+                n = int.from_bytes(z[p:p + nb], "little")
+                p += nb
+            n += 1
+            if len(z) - p < n:
+                return None
+            out += z[p:p + n]
+            p += n
+            continue
+        if t == 1:
+            if p >= len(z):
+                return None
+            n, off = 4 + ((tag >> 2) & 7), ((tag >> 5) << 8) | z[p]
+            p += 1
+        elif t == 2:
+            if len(z) - p < 2:
+                return None
+            n, off = 1 + (tag >> 2), z[p] | (z[p + 1] << 8)
+            p += 2
+        else:
+            if len(z) - p < 4:
+                return None
+            n, off = 1 + (tag >> 2), int.from_bytes(z[p:p + 4], "little")
+            p += 4
+        if off == 0 or off > len(out):
+            return None
+        for _ in range(n):
+            out.append(out[-off])
+    return bytes(out) if len(out) == ulen else None
+
+
+def _block_entries(d):
+    """(entries [(key, value)], error) of block contents d (block.rs:21-41, :124-175)."""
+    if len(d) < 4:
+        return None, "bad block contents, size smaller than u32"
+    nr = int.from_bytes(d[-4:], "little")
+    if nr > (len(d) - 4) // 4:
+        return None, "bad block contents"
+    restarts = len(d) - (1 + nr) * 4
+    out, key, off = [], b"", 0
+    while off < restarts:
+        if restarts - off < 3:
+            return None, "bad entry in block"
+        p = off
+        shared, p = _get_varint(d, p, restarts, 32)
+        non_shared, p = _get_varint(d, p, restarts, 32) if shared is not None else (None, p)
+        vlen, p = _get_varint(d, p, restarts, 32) if non_shared is not None else (None, p)
+        if vlen is None or restarts - p < non_shared + vlen or len(key) < shared:
+            return None, "bad entry in block"
+        key = key[:shared] + d[p:p + non_shared]
+        out.append((key, d[p + non_shared:p + non_shared + vlen]))
+        off = p + non_shared + vlen
+    return out, None
+
+
+def table_scan_expect(f, filter_name=None, mode=0, masked=False):
+    """Expected lcrc_table_scan result: ([(offset, size, kind, type, status, crc)] sorted by offset, None)
+    or (None, reference error message)."""
+    f = bytes(f)
+
+    def trailer_crc(off, n):
+        c = crc(f[off:off + n + 1], mode)
+        return mask(c) if masked else c
+
+    def contents(off, n, verify):
+        if off > len(f) or n + 5 > len(f) - off:
+            return None, "truncated block read"
+        if verify and trailer_crc(off, n) != int.from_bytes(f[off + n + 1:off + n + 5], "little"):
+            return None, "block checksum mismatch"
+        t = f[off + n]
+        if t == 0:
+            return f[off:off + n], None
+        if t == 1:
+            d = snappy_frame_decode(f[off:off + n])
+            return (d, None) if d is not None else (None, "corrupted compressed block content")
+        return None, "bad block type"
+
+    def handle(v):
+        a, p = _get_varint(v, 0, len(v), 64)
+        b, p = _get_varint(v, p, len(v), 64) if a is not None else (None, p)
+        return (a, b) if b is not None else None
+
+    if len(f) < FOOTER_LEN:
+        return None, "file is too short to be an sstable"
+    foot = f[-FOOTER_LEN:]
+    if int.from_bytes(foot[40:48], "little") != TABLE_MAGIC:
+        return None, "not an sstable (bad magic number)"
+    mo, p = _get_varint(foot, 0, 48, 64)
+    ms, p = _get_varint(foot, p, 48, 64)
+    io_, p = _get_varint(foot, p, 48, 64)
+    is_, p = _get_varint(foot, p, 48, 64)
+    if None in (mo, ms, io_, is_):
+        return None, "Error when decoding varint64"
+    d, err = contents(io_, is_, True)
+    if err:
+        return None, err
+    ents, err = _block_entries(d)
+    if err:
+        return None, err
+    found = []
+    for _, v in ents:
+        h = handle(v)
+        if h is None:
+            return None, "Error when decoding varint64"
+        found.append((h[0], h[1], 0))
+    if filter_name is not None:
+        md, err = contents(mo, ms, True)
+        if not err:
+            mes, err = _block_entries(md)
+            if not err:
+                want = b"filter" + filter_name.encode()
+                for k, v in mes:
+                    if k < want:
+                        continue
+                    if k == want and handle(v) is not None:
+                        found.append((*handle(v), 1))
+                    break
+    found += [(mo, ms, 2), (io_, is_, 3)]
+    found.sort(key=lambda b: b[0])
+    out = []
+    for off, n, kind in found:
+        if off > len(f) or n + 5 > len(f) - off:
+            out.append((off, n, kind, 0xFF, 2, 0))
+            continue
+        c = trailer_crc(off, n)
+        st = 0 if c == int.from_bytes(f[off + n + 1:off + n + 5], "little") else 1
+        out.append((off, n, kind, f[off + n], st, c))
+    return out, None
