@@ -217,7 +217,12 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
   return p;
 #else
   // two independent chains over the 64 B quarters (pieces 0..3 and 4..7); x carries the chain register
-  // already xored with its next data word
+  // already xored with its next data word. Pair (j, 4 + j) is refilled REFILL_DELAY step groups after it
+  // was consumed (0: at once).
+#ifndef LCRC_REFILL_DELAY
+#define LCRC_REFILL_DELAY 0
+#endif
+  constexpr int D = LCRC_REFILL_DELAY;
   uint32_t xa = v[0].x ^ init, xb = v[4].x;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -229,11 +234,19 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     xb = step4x(L, R, xb, v[4 + j].w);
     xa = step4x(L, R, xa, j < 3 ? v[j + 1].x : 0u);
     xb = step4x(L, R, xb, j < 3 ? v[5 + j].x : 0u);
-    v[j] = LCRC_REFILL(rs, voff + j * 2048);
-    v[4 + j] = LCRC_REFILL(rs, voff + (4 + j) * 2048);
+    if (j - D >= 0) {
+      v[j - D] = LCRC_REFILL(rs, voff + (j - D) * 2048);
+      v[4 + j - D] = LCRC_REFILL(rs, voff + (4 + j - D) * 2048);
+    }
     __builtin_amdgcn_sched_barrier(0);  // keep the refill here: hipcc would otherwise sink it past the walk
   }
-  return zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two quarters
+  const uint32_t res = zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two quarters
+#pragma unroll
+  for (int j = 4 - D; j < 4; ++j) {
+    v[j] = LCRC_REFILL(rs, voff + j * 2048);
+    v[4 + j] = LCRC_REFILL(rs, voff + (4 + j) * 2048);
+  }
+  return res;
 #endif
 }
 
@@ -448,6 +461,9 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     lcrc_dbg_stamp[gw * 8 + 3] = r1;
     lcrc_dbg_stamp[gw * 8 + 4] = s_src;
     lcrc_dbg_stamp[gw * 8 + 5] = s_staged;
+    // where the wave ran: HW_ID (cu/sh/se fields) and XCC_ID
+    lcrc_dbg_stamp[gw * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    lcrc_dbg_stamp[gw * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 #endif
 }
