@@ -176,6 +176,13 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 16ull << m, tab.data() + TAB_ZPIECE + m * 1024);
   for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 256ull << m, tab.data() + TAB_ZWIN + m * 1024);
   lcrc::make_shift_tables(poly, 4096, tab.data() + TAB_Z4096);
+  // k_windows builds its LDS image from columns (entries 1, 2, 4, .., 128) of the byte tables it uses
+  for (int t = 0; t < 20; ++t) {
+    const uint32_t src = t < 4 ? TAB_SLICE + t * 256                    // S0: T_p
+                         : t < 8 ? TAB_ZPIECE + 2048 + (7 - t) * 256      // S1: Z64[3 - p], p = t - 4
+                                 : TAB_ZWIN + (t - 8) * 256;              // Z256, Z512, Z1024
+    for (int i = 0; i < 8; ++i) tab[TAB_COLS + t * 8 + i] = tab[src + (1u << i)];
+  }
   if ((e = hipMalloc(&ctx->d_tab, TAB_TOTAL * sizeof(uint32_t))) != hipSuccess) return bail(fail_hip(e, "hipMalloc"));
   if ((e = hipMemcpy(ctx->d_tab, tab.data(), TAB_TOTAL * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess)
     return bail(fail_hip(e, "hipMemcpy"));
@@ -272,7 +279,8 @@ static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint
   if (!(ctx->flags & LCRC_FLAG_DIRECT) && span) {
     int rc = ctx->win.ensure(window_words(span));
     if (rc) return rc;
-    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, base, span, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
+    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, base, span, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
+                               st));
     win = ctx->win.p;
   }
   HIPCHK(lcrc_launch_blocks(true, ctx->grid_b, base, span, nullptr, n, stride, length, expected, win, ctx->d_tab,

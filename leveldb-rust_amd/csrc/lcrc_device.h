@@ -16,7 +16,9 @@ enum : int {
   TAB_ZPIECE = 1024,  // Z16, Z32, Z64, Z128 byte-sliced shift tables, 4 x (4 x 256)
   TAB_ZWIN = 5120,    // Z256, Z512, Z1024, Z2048
   TAB_Z4096 = 9216,   // Z4096
-  TAB_TOTAL = 10240,
+  TAB_COLS = 10240,   // k_windows' LDS image as columns: 20 byte tables x 8 columns (table[1 << i]):
+                      // S0 T_p (p = 0..3), S1 Z64[3 - p], then Z256, Z512, Z1024 in TAB_ZWIN word order
+  TAB_TOTAL = 10400,
 };
 
 struct lcrc_desc_dev {  // == lcrc_desc

@@ -28,41 +28,35 @@ typedef u32x4 u32x4_ua __attribute__((aligned(1)));
 namespace lcrc_dev {
 
 // ---------------------------------------------------------------------------------------------------
-// k_windows LDS image (152 KiB -> one 1024-thread workgroup per CU)
+// k_windows LDS image (76 KiB -> two 512-thread workgroups per CU)
 //
-// Four replicated "table sets" S0..S3 of four byte tables each: S0 = slice-by-4 T0..T3, S1 = Z64,
-// S2 = Z256, S3 = Z512 (Z_n[k][b] = byte b at position k advanced over n zero bytes). Set s occupies
-// 64 KiB region s >> 1, half s & 1 of every 256 B row, row e holding entry e. Inside a half-row
-// (32 dwords = the 32 LDS banks) dword 8*p + r is replica r (0..7) of the set's table at position p;
-// position p is indexed by data byte 3 - p (slice: T_p; shifts: Z[3 - p]).
+// Two replicated "table sets" of four byte tables each: S0 = slice-by-4 T0..T3, S1 = Z64 (Z_n[k][b] =
+// byte b at position k advanced over n zero bytes). Set s occupies half s of every 256 B row of the first
+// 64 KiB, row e holding entry e. Inside a half-row (32 dwords = the 32 LDS banks) dword 8*p + r is replica
+// r (0..7) of the set's table at position p; position p is indexed by data byte 3 - p (slice: T_p;
+// shifts: Z[3 - p]).
 // Compact rotated lookups: lane l (r = l & 7, q = (l >> 3) & 3) performs the four lookups of one step
 // as instructions i = 0..3 on position (i + q) & 3, replica r. In every 32-lane ds_read group the banks
 // 8*((i + q) & 3) + r are pairwise distinct, so all lookups are conflict-free with 8 replicas per table
-// instead of 32 -- which is what makes room to replicate the shift tables as well. The address is one
-// v_perm_b32 of a per-lane base (byte 0: half/position/replica, byte 2: region) and the data byte.
-//   [128 KiB, 144 KiB): staging of the source tables during the fill.
-//   [144 KiB, 152 KiB): Z1024, Z2048 (unreplicated) for the two upper levels of the block tree.
+// instead of 32. The address is one v_perm_b32 of a per-lane base (byte 0: half/position/replica) and the
+// data byte.
+//   [64 KiB, 76 KiB): Z256, Z512, Z1024 (unreplicated) for the block tree (its top level applies Z1024
+//   twice).
+// One 512-thread workgroup is launched per CU (measured: 1.3-1.7 us per 256 MiB launch faster than two
+// per CU, and than 256- or 1024-thread shapes). 76 KiB of LDS lets a second one be resident: the next
+// launch's workgroups fill a CU while this launch's tail is still on it.
 // ---------------------------------------------------------------------------------------------------
-#ifndef LCRC_WG1
-// Two 512-thread workgroups per CU (76 KiB each): only S0 and S1 are replicated (region 0); the tree's
-// Z256, Z512, Z1024 are unreplicated at A_ZT (its top level applies Z1024 twice). While one workgroup of
-// a CU is in its prologue or its tail, the other one computes -- also across consecutive launches.
-constexpr int A_WG_PER_CU = 2;
-constexpr int A_THREADS = 512;
-constexpr int A_REP_BYTES = 65536;
-constexpr int A_ZT = A_REP_BYTES;           // Z256, Z512, Z1024; fill staging (slice, Z64) before that
-constexpr int A_STAGE = A_ZT;
-constexpr int A_LDS_BYTES = A_ZT + 3 * 4096;
-#else
-// One 1024-thread workgroup per CU (152 KiB): S0..S3 replicated, staging, Z1024/Z2048 unreplicated.
-constexpr int A_WG_PER_CU = 1;
-constexpr int A_THREADS = 1024;
-constexpr int A_REP_BYTES = 131072;
-constexpr int A_STAGE = 131072;             // fill staging: slice, Z64, Z256, Z512 (dead after the fill),
-constexpr int A_ZUP = A_STAGE + 16384;      // then Z1024, Z2048 (live)
-constexpr int A_LDS_BYTES = A_ZUP + 2 * 4096;
-constexpr uint32_t SET_S2 = 1u << 16, SET_S3 = (1u << 16) | (1u << 7);
+#ifndef LCRC_A_WGCU
+#define LCRC_A_WGCU 1
 #endif
+#ifndef LCRC_A_THREADS
+#define LCRC_A_THREADS 512
+#endif
+constexpr int A_WG_PER_CU = LCRC_A_WGCU;  // workgroups launched per CU (LDS allows two to be resident)
+constexpr int A_THREADS = LCRC_A_THREADS;
+constexpr int A_REP_BYTES = 65536;
+constexpr int A_ZT = A_REP_BYTES;
+constexpr int A_LDS_BYTES = A_ZT + 3 * 4096;
 constexpr int REGION = 16384;  // bytes per wave iteration: two 8 KiB half-tiles, 64 windows of 256 B
 constexpr uint32_t SET_S1 = 1u << 7;
 
@@ -256,19 +250,10 @@ template <int M>
 __device__ __forceinline__ uint32_t tree_level(const void* L, const Rot& R, uint32_t p, uint32_t lane) {
   const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x100 + (1 << M), 0xF, 0xF, false);
   if ((lane & ((2u << M) - 1)) == 0) {
-#ifndef LCRC_WG1
     if constexpr (M < 3)
       p = zlook(L, A_ZT + M * 4096, p) ^ pn;
     else
       p = zlook(L, A_ZT + 2 * 4096, zlook(L, A_ZT + 2 * 4096, p)) ^ pn;  // Z2048 = Z1024 o Z1024
-#else
-    if constexpr (M == 0)
-      p = zrot<SET_S2>(L, R, p) ^ pn;
-    else if constexpr (M == 1)
-      p = zrot<SET_S3>(L, R, p) ^ pn;
-    else
-      p = zlook(L, A_ZUP + (M - 2) * 4096, p) ^ pn;
-#endif
   }
   return p;
 }
@@ -300,18 +285,70 @@ __device__ __forceinline__ void finish_region(const void* L, const Rot& R, uint3
 // Region scheduler: the regions are split into equal contiguous shares, one per workgroup, and dealt to
 // the workgroup's waves from a counter in LDS. Inside a CU the instruction arbiter favours older waves
 // (with a fixed per-wave split the first wave of each SIMD finished in ~60% of the time of the fourth).
-// An LDS atomic returns through lgkmcnt, never behind the HBM loads. (A pool of regions dealt by global
-// atomics to balance CUs against each other cost more than it won: same-address device atomics
-// serialise at ~11 ns, and their returns queue behind the CU's HBM loads. Raising the issue priority of
-// the workgroup that is further behind, with s_setprio, evened out the two workgroups of a CU without
-// shortening the launch.)
+// An LDS atomic returns through lgkmcnt, never behind the HBM loads. CUs do not stream at one rate
+// (whole XCDs differ by up to 10 %, so per-CU end times spread over ~5 us), but every way tried to
+// balance them cost more than the spread: a global pool, work stealing with one global atomic per claim
+// (61 us instead of 46: a wave's loads issued after an atomic return only after it), and more, smaller
+// workgroups left to the hardware dispatcher (49-55 us: more prologues, a coarser tail).
 constexpr uint64_t NO_REGION = ~0ull;
 
-__device__ __forceinline__ uint64_t take_region(uint32_t* lctr, uint64_t reg_lo, uint64_t count, uint32_t lane) {
+// A workgroup's share: regions lo + v * step for tickets v < count.
+struct Share {
+  uint64_t lo, step, count;
+  __device__ __forceinline__ uint64_t region(uint64_t v) const { return v < count ? lo + v * step : NO_REGION; }
+};
+
+__device__ __forceinline__ Share make_share(uint64_t nreg) {
+  Share sh;  // a contiguous range per workgroup
+  const uint64_t per = (nreg + gridDim.x - 1) / gridDim.x;
+  sh.lo = (uint64_t)blockIdx.x * per;
+  sh.step = 1;
+  sh.count = sh.lo < nreg ? (nreg - sh.lo < per ? nreg - sh.lo : per) : 0;
+  return sh;
+}
+
+__device__ __forceinline__ uint64_t take_region(uint32_t* lctr, const Share& sh, uint32_t lane) {
   uint32_t v = 0;
   if (lane == 0) v = atomicAdd(lctr, 1u);
   v = __builtin_amdgcn_readfirstlane(v);
-  return v < count ? reg_lo + v : NO_REGION;
+  return sh.region(v);
+}
+
+// Entry e of a linear byte table from its 8 columns c[i] = table[1 << i] (wave-uniform): xor of the
+// columns of the set bits of e.
+__device__ __forceinline__ uint32_t lin8(const uint32_t* __restrict__ col, uint32_t e) {
+  uint32_t c[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = col[i];  // all loaded unconditionally: one s_load_dwordx8
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v ^= c[i] & (0u - ((e >> i) & 1u));
+  return v;
+}
+
+// k_windows' LDS image built from the column block TAB_COLS. 80 wave passes of 64 entries each, one
+// byte table per pass (uniform columns -> scalar loads): passes 0..31 the replicated sets (set s,
+// position p), passes 32..79 the tree's Z256/Z512/Z1024 (same word order as the global TAB_ZWIN).
+__device__ __forceinline__ void build_tables(uint32_t* L, const uint32_t* __restrict__ gtab, uint32_t wv,
+                                             uint32_t lane) {
+  constexpr int WAVES = A_THREADS / 64;
+  static_assert(80 % WAVES == 0, "passes per wave");
+#pragma unroll
+  for (int k = 0; k < 80 / WAVES; ++k) {
+    const uint32_t P = wv + WAVES * k;  // uniform
+    const uint32_t e = ((P & 3) << 6) | lane;
+    if (P < 32) {
+      const uint32_t set = P >> 4, p = (P >> 2) & 3;
+      // S0: T_p | S1: Z64[3 - p]
+      const uint32_t v = lin8(gtab + TAB_COLS + (P >> 2) * 8, e);
+      u32x4* dst = (u32x4*)((char*)L + e * 256 + set * 128 + p * 32);
+      dst[0] = u32x4{v, v, v, v};
+      dst[1] = u32x4{v, v, v, v};
+    } else {
+      const uint32_t zt = (P - 32) >> 2;  // level * 4 + byte position
+      L[A_ZT / 4 + zt * 256 + e] = lin8(gtab + TAB_COLS + (8 + zt) * 8, e);
+    }
+  }
 }
 
 #ifdef LCRC_PROBE_CLOCK  // diagnostic build: per-workgroup shader/real clock stamps around the tile loop
@@ -330,10 +367,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   __shared__ uint32_t wg_ticket;
   const uint32_t lane = __lane_id();
   const uint32_t tid = threadIdx.x;
-  // this workgroup's share of the regions: [reg_lo, reg_lo + count)
-  const uint64_t per = (nreg + gridDim.x - 1) / gridDim.x;
-  const uint64_t reg_lo = (uint64_t)blockIdx.x * per;
-  const uint64_t count = reg_lo < nreg ? (nreg - reg_lo < per ? nreg - reg_lo : per) : 0;
+  const Share share = make_share(nreg);  // this workgroup's regions
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long s_first = 0;
@@ -347,65 +381,16 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   __syncthreads();
 #endif
 
-  // Table image, step 1: coalesced 16 B loads of the 24 KiB of source tables (slice T0..T3, Z64, then
-  // Z256 .. Z2048 -- adjacent in the global image), completed BEFORE the first region's HBM loads are
-  // issued: vector-memory returns reach a CU in issue order across its waves, so a table load issued
-  // after other waves' HBM loads would wait for all of them (measured: tables ready at ~10 us).
-  const u32x4* g_sl = (const u32x4*)(gtab + TAB_SLICE);
-  const u32x4* g_z64 = (const u32x4*)(gtab + TAB_ZPIECE + 2048);
-  const u32x4* g_zw = (const u32x4*)(gtab + TAB_ZWIN);
-#ifndef LCRC_WG1
-  static_assert(A_THREADS == 512, "the table fill maps one 16 B source chunk per thread");
-  const u32x4 src0 = tid < 256 ? g_sl[tid] : g_z64[tid - 256];  // slice, Z64
-  const u32x4 zs0 = g_zw[tid];                                   // Z256, Z512
-  u32x4 zs1 = {0, 0, 0, 0};
-  if (tid < 256) zs1 = g_zw[512 + tid];                          // Z1024
-  // step 2: stage [slice | Z64] at A_STAGE
-  *(u32x4*)((char*)L + A_STAGE + (tid << 4)) = src0;
-#else
-  static_assert(A_THREADS == 1024, "the table fill maps one 16 B source chunk per thread");
-  const u32x4 src0 = tid < 256 ? g_sl[tid] : (tid < 512 ? g_z64[tid - 256] : g_zw[tid - 512]);
-  u32x4 src1 = {0, 0, 0, 0};
-  if (tid < 512) src1 = g_zw[512 + tid];
-  // step 2: stage [slice | Z64 | Z256 | Z512 | Z1024 | Z2048] at A_STAGE (Z1024/Z2048 are already in their
-  // final place).
-  *(u32x4*)((char*)L + A_STAGE + (tid << 4)) = src0;
-  if (tid < 512) *(u32x4*)((char*)L + A_STAGE + 16384 + (tid << 4)) = src1;
-#endif
-  __syncthreads();
-#ifdef LCRC_PROBE_CLOCK
-  const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
-#endif
-
+  // Prologue. The first region of wave w is region w of the share (static), so its HBM loads go out at
+  // once; the tables are then built while they are in flight. Nothing in the build waits behind them: the
+  // byte tables are linear maps of their 8-bit index, so every entry is an xor of 8 columns (entries
+  // 1, 2, 4, .., 128 of the global image), read with SCALAR loads -- vector-memory returns reach a CU in
+  // issue order, and a table read through the vector path would wait for every HBM load issued before it.
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint64_t t = share.region(wv);
   // lane (k, c) = (lane & 7, lane >> 3) reads piece 16*k + 8*h + c of every 2 KiB of the region
   const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
   u32x4 va[8], vb[8];
-  // step 3: every thread writes 8 replicated 16 B chunks of the rotated sets
-#ifdef LCRC_PROBE_CLOCK
-  const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
-#endif
-  {
-    constexpr int FILL = A_REP_BYTES / 16 / A_THREADS;  // 16 B chunks of the replicated sets per thread
-    const uint32_t* stage = (const uint32_t*)((const char*)L + A_STAGE);
-#pragma unroll
-    for (int k = 0; k < FILL; ++k) {
-      const uint32_t off = (tid + k * A_THREADS) << 4;
-      const uint32_t set = ((off >> 16) << 1) | ((off >> 7) & 1), e = (off >> 8) & 255, p = (off >> 5) & 3;
-      // S0: T_p | S1: Z64[3-p] | S2: Z256[3-p] | S3: Z512[3-p]
-      const uint32_t v = stage[set * 1024 + (set == 0 ? p : 3 - p) * 256 + e];
-      *(u32x4*)((char*)L + off) = u32x4{v, v, v, v};
-    }
-  }
-#ifndef LCRC_WG1
-  lds_barrier();  // the staging area becomes the tree's tables
-  *(u32x4*)((char*)L + A_ZT + (tid << 4)) = zs0;
-  if (tid < 256) *(u32x4*)((char*)L + A_ZT + 8192 + (tid << 4)) = zs1;
-#endif
-  if (tid == 0) wg_ticket = 0;
-  lds_barrier();
-  // the first region's loads go out only now: a wave blocks at VMEM issue once its CU's queue is full,
-  // and issued earlier they kept waves from the replication above (tables ready at ~9 us instead of ~2)
-  uint64_t t = take_region(&wg_ticket, reg_lo, count, lane);
   {
     const __amdgpu_buffer_rsrc_t rs0 = region_rsrc(base, span, t, nreg);
     __builtin_amdgcn_sched_barrier(0);
@@ -414,7 +399,16 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     load_half(vb, rs0, voff_b);
     __builtin_amdgcn_sched_barrier(0);
   }
-  uint64_t tn = take_region(&wg_ticket, reg_lo, count, lane);
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
+#endif
+  build_tables(L, gtab, wv, lane);
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (tid == 0) wg_ticket = A_THREADS / 64;  // tickets 0 .. waves-1 were the static first regions
+  lds_barrier();
+  uint64_t tn = take_region(&wg_ticket, share, lane);
 
   const Rot R = make_rot(lane);
 #ifdef LCRC_PROBE_CLOCK
@@ -441,7 +435,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     if (!s_first) s_first = __builtin_amdgcn_s_memrealtime();
 #endif
     __builtin_amdgcn_sched_barrier(0);
-    const uint64_t tnn = take_region(&wg_ticket, reg_lo, count, lane);
+    const uint64_t tnn = take_region(&wg_ticket, share, lane);
     const uint32_t p = walk_half(L, R, vb, x, rsn, voff_b);
     finish_region<FINAL>(L, R, p, t, lane, out, nblk, fin, flags, expected, ev, mismatch);
     t = tn;
@@ -476,7 +470,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
 // used, and 512-thread workgroups (4 per CU by LDS) keep 32 waves per CU in flight.
 // ---------------------------------------------------------------------------------------------------
 constexpr int B_THREADS = 512;
-constexpr int B_LDS_DWORDS = TAB_TOTAL;
+constexpr int B_LDS_DWORDS = TAB_COLS;  // slice and shift tables (not the column block)
 constexpr int B_BATCH = 8;  // window values per lane loaded ahead of the fold
 
 __device__ __forceinline__ uint32_t byte_step(const uint32_t* L, uint32_t r, uint32_t b) {

@@ -10,6 +10,5 @@ build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_L2 -o tools/probe/variants/l2.so &
 build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_LDSDATA -o tools/probe/variants/ldsdata.so &
 build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_NOLOAD -o tools/probe/variants/noload.so &
 build -DLCRC_PROBE_CLOCK -DLCRC_PROBE_NOWALK -o tools/probe/variants/nowalk.so &
-build -DLCRC_PROBE_CLOCK -DLCRC_WG1 -o tools/probe/variants/wg1.so &
 wait
 ls tools/probe/variants
