@@ -211,13 +211,15 @@ def workload_wal(m, synth, engs, rank, device):
     dev = m.DeviceBuffer.from_host(data, device)
     maxr = len(data) // 7 + 1
     recs = [m.DeviceBuffer(maxr * m.WAL_REC_DTYPE.itemsize, device) for _ in engs]
+    counts = [m.DeviceBuffer(8, device) for _ in engs]
     for e in engs:
         e.reserve(len(data))
     first = engs[0].wal_scan(dev, len(data), maxr, recs[0])
     covered = int((first["length"].astype(np.uint64) + 1).sum())
 
-    def step_on(i, eng):  # wal_scan returns the record count to the host: it ends in a stream sync
-        eng.wal_scan(dev, len(data), maxr, recs[engs.index(eng)])
+    def step_on(i, eng):  # enqueued like the other workloads; records and their count stay on the device
+        k = engs.index(eng)
+        eng.wal_scan_async(dev, len(data), recs[k], maxr, counts[k])
 
     cfg = {"workload": "WAL: 32 KiB log blocks, records n~U[1,2^k), k~U[1,16] (BASELINE configs[3])",
            "file_bytes": int(len(data)), "records": int(len(first)), "bytes_counted": "sum(1+len)"}

@@ -22,7 +22,7 @@
  *                                          optionally verifies thousands of device-resident blocks
  *   lcrc_batch_host_uniform             <- the same starting and ending in host memory (pinned H2D,
  *                                          kernel, D2H, double-buffered)
- *   lcrc_wal_scan                       <- the header parse + CRC verify of (2) for every physical record
+ *   lcrc_wal_scan / lcrc_wal_scan_async <- the header parse + CRC verify of (2) for every physical record
  *                                          of a device-resident log file, 32 KiB block by block
  *   lcrc_table_scan                     <- Table::open with paranoid_checks (table.rs:39-103) followed by
  *                                          read_block_from_file(verify_checksum) (format.rs:146-171) of
@@ -148,6 +148,10 @@ int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32
  * max_recs); *n_recs (host) receives the count. Returns LCRC_EINVAL if max_recs is too small. */
 int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs,
                   size_t max_recs, size_t* n_recs, void* stream);
+/* Asynchronous form: enqueued on `stream`, nothing is synchronized; the record count is written to
+ * *n_recs (DEVICE or pinned host memory) by the last kernel. Records past max_recs are not written. */
+int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs,
+                        size_t max_recs, uint64_t* n_recs, void* stream);
 
 /* One block of an SSTable located by lcrc_table_scan (host struct, 24 B). */
 typedef struct lcrc_tblk {

@@ -81,7 +81,7 @@ ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
-    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_host_uniform", "lcrc_wal_scan",
+    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
     "lcrc_table_scan", "lcrc_batch_seal",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
@@ -126,6 +126,7 @@ def lib():
     sig("lcrc_batch_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, vp)
     sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
     sig("lcrc_wal_scan", i32, vp, vp, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp)
+    sig("lcrc_wal_scan_async", i32, vp, vp, u64, vp, sz, vp, vp)
     sig("lcrc_table_scan", i32, vp, vp, u64, cp, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp, sz)
     sig("lcrc_batch_seal", i32, vp, vp, u64, vp, sz, vp, vp)
     sig("lcrc_snappy_frame_decode", ctypes.c_int64, vp, sz, vp, sz)
@@ -385,6 +386,18 @@ class Engine:
                                              int(chunk_bytes)), "lcrc_batch_host_uniform")
         del keep, keep2
         return out, mm
+
+    def wal_scan_async(self, file_dev, file_len, recs_dev, max_recs, count_dev, stream=None):
+        """lcrc_wal_scan_async: enqueue the scan; the record count lands in count_dev (device u64)."""
+        _check(lib().lcrc_wal_scan_async(self.ctx, _ptr(file_dev), int(file_len), _ptr(recs_dev), int(max_recs),
+                                         _ptr(count_dev), stream), "lcrc_wal_scan_async")
+
+    def wal_scan_device(self, file_dev, file_len, recs_dev, max_recs):
+        """lcrc_wal_scan leaving the records on the device (recs_dev); returns the record count."""
+        n = ctypes.c_size_t(0)
+        _check(lib().lcrc_wal_scan(self.ctx, _ptr(file_dev), int(file_len), _ptr(recs_dev), int(max_recs),
+                                   ctypes.byref(n), None), "lcrc_wal_scan")
+        return n.value
 
     def wal_scan(self, file_dev, file_len, max_recs=None, recs_dev=None):
         """Parse + verify every physical record of a device-resident log. Returns a WAL_REC_DTYPE array."""

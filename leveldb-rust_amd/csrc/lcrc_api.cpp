@@ -24,15 +24,16 @@ hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, u
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
-                              uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch, hipStream_t st);
+                              uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
+                              const uint64_t* n_dev, hipStream_t st);
 hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
-                                 const uint64_t* offsets, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
-                                 hipStream_t st);
+                                 uint2* slots, uint8_t* stops, uint64_t* offsets, lcrc_wal_rec_dev* recs,
+                                 lcrc_desc_dev* descs, uint64_t max_recs, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
 hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
-hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, uint64_t n, const uint32_t* crcs, const uint32_t* mismatch,
-                                  hipStream_t st);
+hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, const uint64_t* n_dev, uint64_t max_recs, const uint32_t* crcs,
+                                  const uint8_t* file, uint64_t* n_out, hipStream_t st);
 }
 
 static_assert(sizeof(lcrc_desc) == sizeof(lcrc_desc_dev), "desc layout");
@@ -96,9 +97,12 @@ struct lcrc_ctx {
   DevBuf<uint32_t> hexp[2];   // expected values per chunk
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   DevBuf<uint32_t> wal_counts;
+  DevBuf<uint2> wal_slots;
+  DevBuf<uint8_t> wal_stops;
   DevBuf<uint64_t> wal_offsets;
   DevBuf<lcrc_desc_dev> wal_descs;
-  DevBuf<uint32_t> wal_crcs, wal_mm;
+  DevBuf<uint32_t> wal_crcs;
+  uint64_t* h_count = nullptr;  // pinned: record count of the synchronous WAL scan
   DevBuf<lcrc_desc_dev> tbl_descs;  // table scan / seal
   DevBuf<uint32_t> tbl_crcs, tbl_mm;
   DevBuf<uint64_t> tbl_pos;
@@ -168,6 +172,8 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
     if ((e = hipEventCreateWithFlags(&ctx->ev_copied[i], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming)) != hipSuccess)
       return bail(fail_hip(e, "hipEventCreate"));
+  if ((e = hipHostMalloc(&ctx->h_count, sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
+    return bail(fail_hip(e, "hipHostMalloc"));
 
   // constant tables for this mode
   const uint32_t poly = lcrc::poly_of(mode);
@@ -204,10 +210,12 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
     if (ctx->ev_done[i]) (void)hipEventDestroy(ctx->ev_done[i]);
   }
   ctx->wal_counts.release();
+  ctx->wal_slots.release();
+  ctx->wal_stops.release();
   ctx->wal_offsets.release();
   ctx->wal_descs.release();
   ctx->wal_crcs.release();
-  ctx->wal_mm.release();
+  if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   ctx->tbl_descs.release();
   ctx->tbl_crcs.release();
   ctx->tbl_mm.release();
@@ -257,7 +265,7 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
   }
   HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
                             ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK, out_crc,
-                            out_mismatch, st));
+                            out_mismatch, nullptr, st));
   return LCRC_OK;
 }
 
@@ -284,7 +292,7 @@ static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint
     win = ctx->win.p;
   }
   HIPCHK(lcrc_launch_blocks(true, ctx->grid_b, base, span, nullptr, n, stride, length, expected, win, ctx->d_tab,
-                            ctx->init, ctx->xorout, mflags, out_crc, out_mismatch, st));
+                            ctx->init, ctx->xorout, mflags, out_crc, out_mismatch, nullptr, st));
   return LCRC_OK;
 }
 
@@ -379,42 +387,48 @@ int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32
   return result;
 }
 
-int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs, size_t max_recs,
-                  size_t* n_recs, void* stream) {
-  if (!ctx || !n_recs || (file_len && !file)) return LCRC_EINVAL;
-  *n_recs = 0;
+int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs, size_t max_recs,
+                        uint64_t* n_recs, void* stream) {
+  if (!ctx || !n_recs || (file_len && !file) || (max_recs && !recs)) return LCRC_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
   hipStream_t st = pick_stream(ctx, stream);
   const uint64_t nblocks = (file_len + 32767) / 32768;
-  if (nblocks == 0) return LCRC_OK;
-  if ((rc = ctx->wal_counts.ensure(nblocks)) || (rc = ctx->wal_offsets.ensure(nblocks))) return rc;
-  HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, nullptr, nullptr, nullptr, st));
-  std::vector<uint32_t> counts(nblocks);
-  HIPCHK(hipMemcpyAsync(counts.data(), ctx->wal_counts.p, nblocks * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  std::vector<uint64_t> offs(nblocks);
-  uint64_t total = 0;
-  for (uint64_t b = 0; b < nblocks; ++b) {
-    offs[b] = total;
-    total += counts[b];
-  }
-  *n_recs = total;
-  if (total > max_recs || (total && !recs)) return LCRC_EINVAL;
-  if (total == 0) return LCRC_OK;
-  if ((rc = ctx->wal_descs.ensure(total)) || (rc = ctx->wal_crcs.ensure(total)) ||
-      (rc = ctx->wal_mm.ensure((total + 31) / 32)))
+  // offsets: nblocks + 1 positions, then the parse's scratch (nblocks u32 local offsets, one u64 per 256 blocks)
+  if ((rc = ctx->wal_counts.ensure(nblocks + 1)) || (rc = ctx->wal_slots.ensure(nblocks * 64 + 1)) ||
+      (rc = ctx->wal_stops.ensure(nblocks + 1)) ||
+      (rc = ctx->wal_offsets.ensure(nblocks + 1 + (nblocks + 1) / 2 + (nblocks + 255) / 256 + 1)))
     return rc;
-  HIPCHK(hipMemcpyAsync(ctx->wal_offsets.p, offs.data(), nblocks * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-  HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_offsets.p,
-                               (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, st));
-  const uint32_t saved = ctx->flags;
-  ctx->flags &= ~LCRC_FLAG_MASK;  // the log format stores the raw crc
-  rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->wal_descs.p, total, ctx->wal_crcs.p, ctx->wal_mm.p, st);
-  ctx->flags = saved;
-  if (rc) return rc;
-  HIPCHK(lcrc_launch_wal_finish((lcrc_wal_rec_dev*)recs, total, ctx->wal_crcs.p, ctx->wal_mm.p, st));
+  if (max_recs && ((rc = ctx->wal_descs.ensure(max_recs)) || (rc = ctx->wal_crcs.ensure(max_recs)) ||
+                   (rc = ctx->win.ensure(window_words(file_len)))))
+    return rc;
+  // One stream: header walk -> file-order positions -> record descriptors, the window pass over the whole
+  // file, one k_blocks over all records (the log format stores the raw crc: no mask), the verdicts. (Run
+  // beside the window pass on a second stream the latency-bound header walk slowed down ~3x and ended later.)
+  HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p,
+                               ctx->wal_offsets.p, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, st));
+  const uint64_t* n_dev = ctx->wal_offsets.p + nblocks;
+  if (max_recs) {
+    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
+                               st));
+    HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, file, file_len, ctx->wal_descs.p, max_recs, 0, 0, nullptr,
+                              ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr, n_dev, st));
+  }
+  HIPCHK(lcrc_launch_wal_finish((lcrc_wal_rec_dev*)recs, n_dev, max_recs, ctx->wal_crcs.p, file, n_recs, st));
   return LCRC_OK;
+}
+
+int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs, size_t max_recs,
+                  size_t* n_recs, void* stream) {
+  if (!ctx || !n_recs) return LCRC_EINVAL;
+  *n_recs = 0;
+  *ctx->h_count = 0;
+  int rc = lcrc_wal_scan_async(ctx, file, file_len, recs, max_recs, ctx->h_count, stream);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(pick_stream(ctx, stream)));
+  const uint64_t total = *ctx->h_count;
+  *n_recs = total;
+  return total > max_recs ? LCRC_EINVAL : LCRC_OK;
 }
 
 // ---- whole-table verify scan ----

@@ -568,8 +568,10 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
                                                      const uint32_t* __restrict__ uexp,
                                                      const uint32_t* __restrict__ win, const uint32_t* __restrict__ gtab,
                                                      uint32_t init, uint32_t xorout, uint32_t flags,
-                                                     uint32_t* __restrict__ out, uint32_t* __restrict__ mismatch) {
+                                                     uint32_t* __restrict__ out, uint32_t* __restrict__ mismatch,
+                                                     const uint64_t* __restrict__ n_dev) {
   __shared__ __attribute__((aligned(16))) uint32_t L[B_LDS_DWORDS];
+  if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
   for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS)
     ((u32x4*)L)[i] = ((const u32x4*)gtab)[i];
   __syncthreads();
@@ -688,29 +690,40 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------------
-// k_wal_parse: one lane per 32 KiB log block, walking the record headers exactly as
-// LogReader::read_physical_record (src/db/log.rs:204-279) does, minus the checksum (k_blocks computes
-// it afterwards, in parallel over all records). Pass 1 (recs == nullptr) counts records per block;
-// pass 2 writes them at the exclusive-scan offsets.
+// WAL scan: k_wal_parse walks the record headers of every 32 KiB log block exactly as
+// LogReader::read_physical_record (src/db/log.rs:204-279) does, minus the checksum (k_blocks computes it,
+// in parallel over all records); k_wal_offsets turns the per-block counts into file-order positions;
+// k_wal_emit writes the records and their descriptors. Nothing returns to the host in between, and the
+// three run on a side stream while k_windows streams the file on the main one.
 // ---------------------------------------------------------------------------------------------------
+constexpr uint32_t WAL_SLOTS = 64;  // records per block kept by the parse (a block with more is re-walked)
+
+// header of the record at in-block offset `at`: length (bytes 4..5) and type (byte 6), three independent
+// byte loads (one memory round trip per hop of the walk)
+__device__ __forceinline__ void wal_header(const uint8_t* __restrict__ blk, uint32_t at, uint32_t& length,
+                                           uint32_t& type) {
+  const uint32_t l0 = blk[at + 4], l1 = blk[at + 5], ty = blk[at + 6];
+  length = l0 | (l1 << 8);
+  type = ty;
+}
+
+// one lane per block: record count, stop reason and the first WAL_SLOTS records as (offset | length << 16,
+// type)
+// ... and the workgroup's exclusive scan of the counts: local[b] (u32) and part[workgroup] (the total)
 __global__ void __launch_bounds__(256) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
                                                    uint64_t nblocks, uint32_t* __restrict__ counts,
-                                                   const uint64_t* __restrict__ offsets,
-                                                   lcrc_wal_rec_dev* __restrict__ recs,
-                                                   lcrc_desc_dev* __restrict__ descs) {
+                                                   uint2* __restrict__ slots, uint8_t* __restrict__ stops,
+                                                   uint32_t* __restrict__ local, uint64_t* __restrict__ part) {
+  __shared__ uint32_t wsum[4];
   const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
-  const uint64_t bstart = b * 32768ull;
-  const uint64_t rem = file_len - bstart;
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  const uint8_t* blk = file + b * 32768ull;
+  const uint64_t rem = b < nblocks ? file_len - b * 32768ull : 0;
   const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
-  uint32_t consumed = 0;
-  uint32_t nrec = 0;
-  uint64_t o = recs ? offsets[b] : 0;
-  uint32_t stop = LCRC_WAL_STOP_TRAILER_DEV;
+  uint32_t consumed = 0, nrec = 0, stop = LCRC_WAL_STOP_TRAILER_DEV;
   while (cap - consumed >= 7) {
-    const uint8_t* h = file + bstart + consumed;
-    const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
-    const uint32_t type = h[6];
+    uint32_t length, type;
+    wal_header(blk, consumed, length, type);
     if (7 + length > cap - consumed) {
       stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
       break;
@@ -719,43 +732,127 @@ __global__ void __launch_bounds__(256) k_wal_parse(const uint8_t* __restrict__ f
       stop = LCRC_WAL_STOP_ZERO_DEV;
       break;
     }
-    if (recs) {
-      lcrc_wal_rec_dev rr;
-      rr.header = bstart + consumed;
-      rr.length = length;
-      rr.type = (uint8_t)type;
-      rr.status = 0;
-      rr.block_end = 0;
-      rr.crc = 0;
-      rr.stop = 0;
-      recs[o] = rr;
-      lcrc_desc_dev d;
-      d.offset = bstart + consumed + 6;
-      d.length = 1 + length;
-      d.expect_rel = -6;
-      descs[o] = d;
-      ++o;
-    }
+    if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type);
     ++nrec;
     consumed += 7 + length;
   }
-  if (!recs) {
+  // workgroup exclusive scan: wave inclusive scan by shuffles, then the wave totals
+  uint32_t inc = nrec;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += v;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t k = 0; k < w; ++k) base += wsum[k];
+  if (b < nblocks) {
     counts[b] = nrec;
-  } else if (nrec) {
-    recs[o - 1].block_end = 1;
-    recs[o - 1].stop = stop;
+    stops[b] = (uint8_t)stop;
+    local[b] = base + inc - nrec;
+  }
+  if (threadIdx.x == 255) part[blockIdx.x] = base + inc;
+}
+
+// file-order position of every block's first record: offsets[b] = (exclusive scan of the parse
+// workgroups' totals)[b / 256] + local[b]; offsets[n] = total. One 1024-thread workgroup.
+__global__ void __launch_bounds__(1024) k_wal_offsets(const uint32_t* __restrict__ local,
+                                                      const uint64_t* __restrict__ part, uint64_t n,
+                                                      uint64_t* __restrict__ offsets) {
+  __shared__ uint64_t carry;
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t pex[1024];
+  const uint32_t t = threadIdx.x, lane = __lane_id(), w = t >> 6;
+  const uint64_t nparts = (n + 255) / 256;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t p0 = 0; p0 < nparts; p0 += 1024) {  // tiles of 1024 parts (256 Ki blocks)
+    const uint64_t i = p0 + t;
+    const uint64_t v = i < nparts ? part[i] : 0;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t u = __shfl_up(inc, d, 64);
+      if (lane >= (uint32_t)d) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint64_t base = carry;
+    for (uint32_t k = 0; k < w; ++k) base += wsum[k];
+    pex[t] = base + inc - v;
+    __syncthreads();
+    const uint64_t b_lo = p0 * 256, b_hi = (p0 + 1024) * 256 < n ? (p0 + 1024) * 256 : n;
+    for (uint64_t blk = b_lo + t; blk < b_hi; blk += 1024) offsets[blk] = pex[(blk - b_lo) >> 8] + local[blk];
+    if (t == 1023) carry = base + inc;
+    __syncthreads();
+  }
+  if (t == 0) offsets[n] = carry;
+}
+
+__device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcrc_desc_dev* __restrict__ descs,
+                                        uint64_t o, uint64_t header, uint32_t length, uint32_t type, bool last,
+                                        uint32_t stop) {
+  lcrc_wal_rec_dev rr;
+  rr.header = header;
+  rr.length = length;
+  rr.type = (uint8_t)type;
+  rr.status = 0;
+  rr.block_end = last ? 1 : 0;
+  rr.crc = 0;
+  rr.stop = last ? stop : 0;
+  recs[o] = rr;
+  lcrc_desc_dev d;
+  d.offset = header + 6;
+  d.length = 1 + length;
+  d.expect_rel = -6;
+  descs[o] = d;
+}
+
+// one thread per (block, slot): records in file order at offsets[b] + i (those below max_recs); the
+// thread of the last slot re-walks a block that has more records than slots
+__global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ file, uint64_t nblocks,
+                                                  const uint32_t* __restrict__ counts,
+                                                  const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
+                                                  const uint64_t* __restrict__ offsets,
+                                                  lcrc_wal_rec_dev* __restrict__ recs,
+                                                  lcrc_desc_dev* __restrict__ descs, uint64_t max_recs) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t b = g / WAL_SLOTS;
+  const uint32_t i = (uint32_t)(g % WAL_SLOTS);
+  if (b >= nblocks) return;
+  const uint32_t cnt = counts[b];
+  if (i >= cnt) return;
+  const uint64_t o = offsets[b] + i;
+  const uint2 sl = slots[g];
+  uint32_t at = sl.x & 0xFFFFu, length = sl.x >> 16;
+  if (o < max_recs) wal_put(recs, descs, o, b * 32768ull + at, length, sl.y, i + 1 == cnt, stops[b]);
+  if (i == WAL_SLOTS - 1 && cnt > WAL_SLOTS) {
+    const uint8_t* blk = file + b * 32768ull;
+    for (uint32_t j = WAL_SLOTS; j < cnt; ++j) {  // the parse already validated every header up to cnt
+      at += 7 + length;
+      uint32_t type;
+      wal_header(blk, at, length, type);
+      const uint64_t oj = offsets[b] + j;
+      if (oj < max_recs) wal_put(recs, descs, oj, b * 32768ull + at, length, type, j + 1 == cnt, stops[b]);
+    }
   }
 }
 
-// Per-record verdicts from the k_blocks outputs; the first mismatch of a 32 KiB block ends the block
-// (the reader drops the rest of it, log.rs:260-273): later records of that block are marked by stop.
-__global__ void __launch_bounds__(256) k_wal_finish(lcrc_wal_rec_dev* __restrict__ recs, uint64_t n,
+// Per-record verdicts: crc from k_blocks, status = the stored header crc differs. The reader's handling
+// of a mismatch (drop the rest of the 32 KiB block, log.rs:260-273) is replayed on the host.
+// n_out (device or pinned host memory) receives the total record count.
+__global__ void __launch_bounds__(256) k_wal_finish(lcrc_wal_rec_dev* __restrict__ recs,
+                                                    const uint64_t* __restrict__ n_dev, uint64_t max_recs,
                                                     const uint32_t* __restrict__ crcs,
-                                                    const uint32_t* __restrict__ mismatch) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  recs[i].crc = crcs[i];
-  recs[i].status = (mismatch[i >> 5] >> (i & 31)) & 1;
+                                                    const uint8_t* __restrict__ file, uint64_t* __restrict__ n_out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = *n_dev;
+  const uint64_t n = *n_dev < max_recs ? *n_dev : max_recs;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = crcs[i];
+    recs[i].crc = c;
+    recs[i].status = load_le32(file + recs[i].header) != c;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -833,30 +930,40 @@ hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, u
   return hipGetLastError();
 }
 
+// n_dev (device, nullable): the actual count when it is only known on the device; n is then a bound
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
-                              uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch, hipStream_t st) {
+                              uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
+                              const uint64_t* n_dev, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint64_t per_wg = lcrc_dev::B_THREADS / 16;  // one range per 16-lane row
   uint64_t need = (n + per_wg - 1) / per_wg;
   int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   if (uniform)
     hipLaunchKernelGGL(lcrc_dev::k_blocks<true>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs, n,
-                       ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch);
+                       ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev);
   else
     hipLaunchKernelGGL(lcrc_dev::k_blocks<false>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs,
-                       n, ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch);
+                       n, ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev);
   return hipGetLastError();
 }
 
 hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
-                                 const uint64_t* offsets, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
-                                 hipStream_t st) {
-  if (nblocks == 0) return hipSuccess;
-  int g = (int)((nblocks + 255) / 256);
-  hipLaunchKernelGGL(lcrc_dev::k_wal_parse, dim3(g), dim3(256), 0, st, file, file_len, nblocks, counts, offsets, recs,
-                     descs);
+                                 uint2* slots, uint8_t* stops, uint64_t* offsets, lcrc_wal_rec_dev* recs,
+                                 lcrc_desc_dev* descs, uint64_t max_recs, hipStream_t st) {
+  const uint64_t nparts = (nblocks + 255) / 256;
+  uint32_t* local = (uint32_t*)(offsets + nblocks + 1);         // scratch after offsets (nblocks u32)
+  uint64_t* part = offsets + nblocks + 1 + (nblocks + 1) / 2;  // then nparts u64
+  if (nparts)
+    hipLaunchKernelGGL(lcrc_dev::k_wal_parse, dim3((unsigned)nparts), dim3(256), 0, st, file, file_len, nblocks, counts,
+                       slots, stops, local, part);
+  hipLaunchKernelGGL(lcrc_dev::k_wal_offsets, dim3(1), dim3(1024), 0, st, local, part, nblocks, offsets);
+  if (max_recs && nblocks) {
+    const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
+    hipLaunchKernelGGL(lcrc_dev::k_wal_emit, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, file, nblocks,
+                       counts, slots, stops, offsets, recs, descs, max_recs);
+  }
   return hipGetLastError();
 }
 
@@ -873,11 +980,11 @@ hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, cons
   return hipGetLastError();
 }
 
-hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, uint64_t n, const uint32_t* crcs, const uint32_t* mismatch,
-                                  hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  int g = (int)((n + 255) / 256);
-  hipLaunchKernelGGL(lcrc_dev::k_wal_finish, dim3(g), dim3(256), 0, st, recs, n, crcs, mismatch);
+hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, const uint64_t* n_dev, uint64_t max_recs, const uint32_t* crcs,
+                                  const uint8_t* file, uint64_t* n_out, hipStream_t st) {
+  const uint64_t g = (max_recs + 255) / 256;
+  hipLaunchKernelGGL(lcrc_dev::k_wal_finish, dim3((unsigned)(g < 1 ? 1 : g < 2048 ? g : 2048)), dim3(256), 0, st, recs,
+                     n_dev, max_recs, crcs, file, n_out);
   return hipGetLastError();
 }
 

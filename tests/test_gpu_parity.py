@@ -210,3 +210,62 @@ def test_wal_batch_equals_host_reader_under_corruption(lcrc, orc, engines, seed)
         body = bytes(data[h + 6:h + 7 + int(r["length"])])
         assert int(r["crc"]) == orc.crc(body, 0)
         assert int(r["status"]) == (int.from_bytes(data[h:h + 4], "little") != orc.crc(body, 0))
+
+
+def _wal_expect(orc, data):
+    """(header, length, type) of every physical record the reader's header walk visits (log.rs:204-279)."""
+    out = []
+    for b0 in range(0, len(data), 32768):
+        blk = data[b0:b0 + 32768]
+        at = 0
+        while len(blk) - at >= 7:
+            n = blk[at + 4] | (blk[at + 5] << 8)
+            t = blk[at + 6]
+            if 7 + n > len(blk) - at or (t == 0 and n == 0):
+                break
+            out.append((b0 + at, n, t))
+            at += 7 + n
+    return out
+
+
+def test_wal_scan_many_records_per_block(lcrc, orc, engines):
+    """Blocks holding far more records than the parse keeps per block (the emit re-walks them)."""
+    rng = np.random.default_rng(77)
+    recs = [rng.integers(0, 256, int(rng.integers(0, 4)), dtype=np.uint8).tobytes() for _ in range(30000)]
+    recs += [rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()]  # and a multi-block record
+    data = orc.log_write(recs)
+    dev = lcrc.DeviceBuffer.from_host(np.frombuffer(data, np.uint8))
+    got = engines[0].wal_scan(dev, len(data))
+    want = _wal_expect(orc, data)
+    assert [(int(r["header"]), int(r["length"]), int(r["type"])) for r in got] == want
+    assert (got["status"] == 0).all()
+    for r in got[::997]:
+        h = int(r["header"])
+        assert int(r["crc"]) == orc.crc(data[h + 6:h + 7 + int(r["length"])], 0)
+    # too small a capacity: LCRC_EINVAL and the count
+    import ctypes
+    small = lcrc.DeviceBuffer(10 * lcrc.WAL_REC_DTYPE.itemsize)
+    n = ctypes.c_size_t(0)
+    rc = lcrc.lib().lcrc_wal_scan(engines[0].ctx, dev.ptr, len(data), small.ptr, 10, ctypes.byref(n), None)
+    assert rc == lcrc.EINVAL and n.value == len(want)
+    assert small.download(lcrc.WAL_REC_DTYPE, 10)["header"].tolist() == [h for h, _, _ in want[:10]]
+
+
+def test_wal_scan_async_matches_sync(lcrc, orc, engines):
+    rng = np.random.default_rng(78)
+    recs = [rng.integers(0, 256, int(rng.integers(0, 1 << int(rng.integers(1, 17)))), dtype=np.uint8).tobytes()
+            for _ in range(300)]
+    data = orc.log_write(recs)
+    dev = lcrc.DeviceBuffer.from_host(np.frombuffer(data, np.uint8))
+    sync = engines[1].wal_scan(dev, len(data))
+    cap = len(data) // 7 + 1
+    rd = lcrc.DeviceBuffer(cap * lcrc.WAL_REC_DTYPE.itemsize)
+    cnt = lcrc.DeviceBuffer(8)
+    engines[1].wal_scan_async(dev, len(data), rd, cap, cnt)
+    engines[1].sync()
+    n = int(cnt.download(np.uint64, 1)[0])
+    assert n == len(sync)
+    assert rd.download(lcrc.WAL_REC_DTYPE, n).tobytes() == sync.tobytes()
+    # an empty log
+    empty = lcrc.DeviceBuffer(16)
+    assert len(engines[1].wal_scan(empty, 0)) == 0
