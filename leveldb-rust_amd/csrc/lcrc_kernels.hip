@@ -353,7 +353,8 @@ __device__ __forceinline__ void build_tables(uint32_t* L, const uint32_t* __rest
 
 #ifdef LCRC_PROBE_CLOCK  // diagnostic build: per-workgroup shader/real clock stamps around the tile loop
 __device__ unsigned long long lcrc_dbg_clock[4096];
-__device__ unsigned long long lcrc_dbg_stamp[4096 * 8];  // per wave: entry, tables ready, first half, end,
+__device__ unsigned long long lcrc_dbg_stamp[4096 * 8];
+__device__ unsigned long long lcrc_dbg_bstamp[8192 * 4];  // k_blocks per wave: entry, tables, first range, end  // per wave: entry, tables ready, first half, end,
                                                          // table source loaded, staged
 #endif
 
@@ -571,10 +572,17 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
                                                      uint32_t* __restrict__ out, uint32_t* __restrict__ mismatch,
                                                      const uint64_t* __restrict__ n_dev) {
   __shared__ __attribute__((aligned(16))) uint32_t L[B_LDS_DWORDS];
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long b_entry = __builtin_amdgcn_s_memrealtime();
+  unsigned long long b_first = 0;
+#endif
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
   for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS)
     ((u32x4*)L)[i] = ((const u32x4*)gtab)[i];
   __syncthreads();
+#ifdef LCRC_PROBE_CLOCK
+  const unsigned long long b_tab = __builtin_amdgcn_s_memrealtime();
+#endif
 
   const uint32_t lane = __lane_id();
   const uint32_t g = lane & 15, row = lane >> 4;
@@ -686,7 +694,19 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
       }
       if (bad && mismatch) atomicOr(&mismatch[i >> 5], 1u << (i & 31));
     }
+#ifdef LCRC_PROBE_CLOCK
+    if (!b_first) b_first = __builtin_amdgcn_s_memrealtime();
+#endif
   }
+#ifdef LCRC_PROBE_CLOCK
+  const uint64_t gw = (uint64_t)blockIdx.x * (B_THREADS / 64) + (threadIdx.x >> 6);
+  if (lane == 0 && gw < 8192) {
+    lcrc_dbg_bstamp[gw * 4 + 0] = b_entry;
+    lcrc_dbg_bstamp[gw * 4 + 1] = b_tab;
+    lcrc_dbg_bstamp[gw * 4 + 2] = b_first;
+    lcrc_dbg_bstamp[gw * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -895,6 +915,11 @@ extern "C" {
 // first half-tile walked, end
 int lcrc_probe_stamps(unsigned long long* dst) {
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(lcrc_dev::lcrc_dbg_stamp), sizeof(unsigned long long) * 4096 * 8) ==
+                 hipSuccess ? 0 : -1;
+}
+
+int lcrc_probe_bstamps(unsigned long long* dst) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(lcrc_dev::lcrc_dbg_bstamp), sizeof(unsigned long long) * 8192 * 4) ==
                  hipSuccess ? 0 : -1;
 }
 

@@ -1,0 +1,37 @@
+"""Per-wave timeline of one k_blocks launch on the mixed (SSTable) workload (LCRC_PROBE_CLOCK build)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import __graft_entry__ as g  # noqa: E402
+
+m = g.load()
+synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
+sizes = synth.mixed_sizes(256 << 20, seed=synth.SEED_MIXED)
+offs, total = synth.sstable_layout(sizes)
+data = synth.splitmix_bytes(synth.SEED_MIXED + 1000, total)
+d = np.zeros(len(sizes), m.DESC_DTYPE)
+d["offset"], d["length"], d["expect_rel"] = offs, sizes.astype(np.uint64) + 1, m.NO_EXPECT
+buf = m.DeviceBuffer.from_host(data)
+dd = m.DeviceBuffer.from_host(d.view(np.uint8))
+out = m.DeviceBuffer(4 * len(sizes))
+eng = m.Engine(0, 1)
+eng.reserve(total)
+for i in range(10):
+    eng.batch(buf, total, dd, len(sizes), out)
+eng.sync()
+eng.batch(buf, total, dd, len(sizes), out)
+eng.sync()
+st = (ctypes.c_ulonglong * (8192 * 4))()
+m.lib().lcrc_probe_bstamps(st)
+a = np.frombuffer(st, dtype=np.uint64).reshape(8192, 4).astype(np.int64)
+a = a[a[:, 0] != 0]
+t0 = a[:, 0].min()
+r = (a - t0) / 100.0
+print(f"k_blocks: ranges {len(sizes)}, waves {len(a)}")
+for k, name in enumerate(["entry", "tables", "first", "end"]):
+    col = r[:, k][a[:, k] != 0]
+    print(f"  {name:7s} " + " ".join(f"{x:7.2f}" for x in np.percentile(col, [0, 10, 50, 90, 100])))
