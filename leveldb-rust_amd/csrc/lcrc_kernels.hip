@@ -488,8 +488,8 @@ __device__ __forceinline__ uint32_t zl(const uint32_t* L, int off, uint32_t r) {
 }
 
 // Lane g's share of a row walk over [a, e) (0 <= e - a <= 256): the 16 B piece ending at
-// e - 16*(15-g). kind 0: empty, 1: whole piece inside [a, e), 2: straddles a (bytes [first, 16) only,
-// gathered bytewise so nothing before a -- possibly before the buffer -- is read).
+// e - 16*(15-g). kind 0: empty, 1: whole piece inside [a, e), 2: straddles a (only bytes [first, 16) are
+// walked; the piece is read whole when it starts inside the buffer, else bytewise from a on).
 struct RowPiece {
   u32x4 w;
   uint32_t kind, first, at_a;
@@ -511,15 +511,36 @@ __device__ __forceinline__ RowPiece row_load(const uint8_t* __restrict__ base, u
     } else {
       p.kind = 2;
       p.first = (uint32_t)((int64_t)a - ps);
-      uint32_t b[16];
+      if (ps >= 0) {
+        p.w = *(const u32x4_ua*)(base + ps);
+      } else {  // the range starts in the buffer's first 16 bytes
+        uint32_t b[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) b[i] = (i >= 1 && (uint32_t)i >= p.first) ? base[ps + i] : 0u;
+        for (int i = 0; i < 16; ++i) b[i] = (i >= 1 && (uint32_t)i >= p.first) ? base[ps + i] : 0u;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        p.w[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | (b[4 * q + 3] << 24);
+        for (int q = 0; q < 4; ++q)
+          p.w[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | (b[4 * q + 3] << 24);
+      }
     }
   }
   return p;
+}
+
+// lane g of a 16-lane row <- lane g + 2^m of the same row (0 past the row's end): DPP row_shl
+__device__ __forceinline__ uint32_t row_down(uint32_t v, int m) {
+  switch (m) {
+    case 0: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xF, 0xF, false);
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x102, 0xF, 0xF, false);
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x108, 0xF, 0xF, false);
+  }
+}
+
+// every lane of a 16-lane row <- lane 0 of its row (four scalar reads, no LDS round trip)
+__device__ __forceinline__ uint32_t row_bcast0(uint32_t v, uint32_t lane) {
+  const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+  return lane < 32 ? (lane < 16 ? r0 : r1) : (lane < 48 ? r2 : r3);
 }
 
 // walk(R0, base[a, e)) from the row's loaded pieces, returned to every lane of the row; a == e -> R0.
@@ -549,12 +570,11 @@ __device__ uint32_t row_walk(const uint32_t* L, const RowPiece& p, bool empty_ra
   }
   // row tree: level m joins lane g with g + 2^m, shifting the left part by 16*2^m bytes
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    uint32_t pn = __shfl_down(cv, 1 << m, 16);
-    uint32_t sh = zl(L, TAB_ZPIECE + m * 1024, cv);
-    if ((g & ((2u << m) - 1)) == 0) cv = sh ^ pn;
+  for (int m = 0; m < 4; ++m) {  // only the combining lanes look up (exec-masked: fewer bank conflicts)
+    const uint32_t pn = row_down(cv, m);
+    if ((g & ((2u << m) - 1)) == 0) cv = zl(L, TAB_ZPIECE + m * 1024, cv) ^ pn;
   }
-  uint32_t res = __shfl(cv, lane & ~15u, 64);
+  const uint32_t res = row_bcast0(cv, lane);
   return empty_range ? R0 : res;
 }
 
@@ -562,8 +582,10 @@ __device__ __forceinline__ uint32_t load_le32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// waves_per_eu(8): 64 VGPRs and few enough SGPRs for 8 waves per SIMD (at 97 SGPRs only 6 fit, so a
+// quarter of the 4 x 512-thread workgroups per CU started only when others had finished)
 template <bool UNIFORM>
-__global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict__ base, uint64_t base_len,
+__global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) k_blocks(const uint8_t* __restrict__ base, uint64_t base_len,
                                                      const lcrc_desc_dev* __restrict__ descs, uint64_t n,
                                                      uint64_t ustride, uint32_t ulen,
                                                      const uint32_t* __restrict__ uexp,
@@ -577,6 +599,32 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
   unsigned long long b_first = 0;
 #endif
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
+  const uint32_t lane = __lane_id();
+  const uint32_t g = lane & 15, row = lane >> 4;
+  const uint64_t wave = (uint64_t)blockIdx.x * (B_THREADS / 64) + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (B_THREADS / 64);
+  const bool use_win = win != nullptr;
+  // descriptors are loaded one iteration ahead of their use (the first one before the table fill)
+  auto load_desc = [&](uint64_t i, uint64_t& s, uint32_t& len, int32_t& xrel) {
+    s = 0;
+    len = 0;
+    xrel = LCRC_NO_EXPECT_DEV;
+    if (i < n) {
+      if (UNIFORM) {
+        s = i * ustride;
+        len = ulen;
+      } else {
+        const lcrc_desc_dev d = descs[i];
+        s = d.offset;
+        len = d.length;
+        xrel = d.expect_rel;
+      }
+    }
+  };
+  uint64_t s_nx;
+  uint32_t len_nx;
+  int32_t xrel_nx;
+  load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx);
   for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS)
     ((u32x4*)L)[i] = ((const u32x4*)gtab)[i];
   __syncthreads();
@@ -584,30 +632,22 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
   const unsigned long long b_tab = __builtin_amdgcn_s_memrealtime();
 #endif
 
-  const uint32_t lane = __lane_id();
-  const uint32_t g = lane & 15, row = lane >> 4;
-  const uint64_t wave = (uint64_t)blockIdx.x * (B_THREADS / 64) + (threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * (B_THREADS / 64);
-  const bool use_win = win != nullptr;
-
   for (uint64_t i0 = wave * 4; i0 < n; i0 += nwaves * 4) {
     const uint64_t i = i0 + row;
     const bool valid = i < n;
-    uint64_t s = 0;
-    uint32_t len = 0;
-    int32_t xrel = LCRC_NO_EXPECT_DEV;
-    if (valid) {
-      if (UNIFORM) {
-        s = i * ustride;
-        len = ulen;
-      } else {
-        lcrc_desc_dev d = descs[i];
-        s = d.offset;
-        len = d.length;
-        xrel = d.expect_rel;
-      }
-    }
+    const uint64_t s = s_nx;
+    const uint32_t len = len_nx;
+    const int32_t xrel = xrel_nx;
+    load_desc(i + nwaves * 4, s_nx, len_nx, xrel_nx);
     const uint64_t e = s + len;
+    // the expected value, loaded with the data (bytewise: any alignment, and checked against the buffer)
+    uint32_t expv = 0;
+    bool exp_ok = false;
+    if (!UNIFORM && valid && g == 0 && xrel != LCRC_NO_EXPECT_DEV) {
+      const int64_t xp = (int64_t)s + xrel;
+      exp_ok = !(xp < 0 || (uint64_t)xp + 4 > base_len);
+      if (exp_ok) expv = load_le32(base + xp);
+    }
     uint32_t acc;
     if (use_win) {
       // window indices: head = partial-or-full window ws, full windows (ws, wfull], tail = partial window wl
@@ -622,9 +662,9 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
       const uint64_t items = single ? 0 : (wfull - ws) + 1;  // head + full windows
       const uint64_t npad = (16 - (items & 15)) & 15;
       const uint64_t rounds = single ? 0 : (npad + items) >> 4;
-      uint32_t rmax = (uint32_t)rounds;
-      rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 16, 64));
-      rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 32, 64));
+      const uint32_t rr32 = (uint32_t)rounds;
+      const uint32_t rmax = max(max(__builtin_amdgcn_readlane(rr32, 0), __builtin_amdgcn_readlane(rr32, 16)),
+                                max(__builtin_amdgcn_readlane(rr32, 32), __builtin_amdgcn_readlane(rr32, 48)));
 
       // every load this range needs first: head and tail pieces, the first batch of window values
       const RowPiece ph = row_load(base, s, head_end, g);
@@ -654,11 +694,10 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        uint32_t pn = __shfl_down(a, 1 << m, 16);
-        uint32_t sh = zl(L, TAB_ZWIN + m * 1024, a);
-        if ((g & ((2u << m) - 1)) == 0) a = sh ^ pn;
+        const uint32_t pn = row_down(a, m);
+        if ((g & ((2u << m) - 1)) == 0) a = zl(L, TAB_ZWIN + m * 1024, a) ^ pn;
       }
-      const uint32_t mid = __shfl(a, lane & ~15u, 64);
+      const uint32_t mid = row_bcast0(a, lane);
       acc = single ? head : mid;
       // tail: the partial last window, walked from the folded value
       acc = row_walk(L, pt, ta == e, acc, g, lane);
@@ -689,8 +728,7 @@ __global__ void __launch_bounds__(B_THREADS) k_blocks(const uint8_t* __restrict_
       if (UNIFORM) {
         if (uexp) bad = uexp[i] != crc;
       } else if (xrel != LCRC_NO_EXPECT_DEV) {
-        const int64_t xp = (int64_t)s + xrel;
-        bad = (xp < 0 || (uint64_t)xp + 4 > base_len) ? true : load_le32(base + xp) != crc;
+        bad = !exp_ok || expv != crc;
       }
       if (bad && mismatch) atomicOr(&mismatch[i >> 5], 1u << (i & 31));
     }
