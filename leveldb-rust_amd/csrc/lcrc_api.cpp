@@ -25,15 +25,14 @@ hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint6
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
                               uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
-                              const uint64_t* n_dev, hipStream_t st);
+                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st);
 hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
-                                 uint2* slots, uint8_t* stops, uint64_t* offsets, lcrc_wal_rec_dev* recs,
-                                 lcrc_desc_dev* descs, uint64_t max_recs, hipStream_t st);
+                                 uint2* slots, uint8_t* stops, uint32_t* local, uint64_t* part,
+                                 lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
+                                 uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
 hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
-hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, const uint64_t* n_dev, uint64_t max_recs, const uint32_t* crcs,
-                                  const uint8_t* file, uint64_t* n_out, hipStream_t st);
 }
 
 static_assert(sizeof(lcrc_desc) == sizeof(lcrc_desc_dev), "desc layout");
@@ -265,7 +264,7 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
   }
   HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
                             ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK, out_crc,
-                            out_mismatch, nullptr, st));
+                            out_mismatch, nullptr, nullptr, st));
   return LCRC_OK;
 }
 
@@ -292,7 +291,7 @@ static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint
     win = ctx->win.p;
   }
   HIPCHK(lcrc_launch_blocks(true, ctx->grid_b, base, span, nullptr, n, stride, length, expected, win, ctx->d_tab,
-                            ctx->init, ctx->xorout, mflags, out_crc, out_mismatch, nullptr, st));
+                            ctx->init, ctx->xorout, mflags, out_crc, out_mismatch, nullptr, nullptr, st));
   return LCRC_OK;
 }
 
@@ -394,27 +393,30 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   if (rc) return rc;
   hipStream_t st = pick_stream(ctx, stream);
   const uint64_t nblocks = (file_len + 32767) / 32768;
-  // offsets: nblocks + 1 positions, then the parse's scratch (nblocks u32 local offsets, one u64 per 256 blocks)
+  // wal_offsets: [0] the total, then per block the in-workgroup offset (u32) and per 256 blocks a total
   if ((rc = ctx->wal_counts.ensure(nblocks + 1)) || (rc = ctx->wal_slots.ensure(nblocks * 64 + 1)) ||
       (rc = ctx->wal_stops.ensure(nblocks + 1)) ||
-      (rc = ctx->wal_offsets.ensure(nblocks + 1 + (nblocks + 1) / 2 + (nblocks + 255) / 256 + 1)))
+      (rc = ctx->wal_offsets.ensure(1 + (nblocks + 1) / 2 + (nblocks + 255) / 256 + 1)))
     return rc;
   if (max_recs && ((rc = ctx->wal_descs.ensure(max_recs)) || (rc = ctx->wal_crcs.ensure(max_recs)) ||
                    (rc = ctx->win.ensure(window_words(file_len)))))
     return rc;
-  // One stream: header walk -> file-order positions -> record descriptors, the window pass over the whole
-  // file, one k_blocks over all records (the log format stores the raw crc: no mask), the verdicts. (Run
-  // beside the window pass on a second stream the latency-bound header walk slowed down ~3x and ended later.)
-  HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p,
-                               ctx->wal_offsets.p, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, st));
-  const uint64_t* n_dev = ctx->wal_offsets.p + nblocks;
+  uint64_t* n_total = ctx->wal_offsets.p;
+  uint32_t* local = (uint32_t*)(ctx->wal_offsets.p + 1);
+  uint64_t* part = ctx->wal_offsets.p + 1 + (nblocks + 1) / 2;
+  // One stream: the header walk, the records at their file-order positions, the window pass over the whole
+  // file, then one k_blocks over all records (the log format stores the raw crc: no mask) that also stores
+  // each record's crc and verdict. (Run beside the window pass on a second stream the latency-bound header
+  // walk slowed down ~3x and ended later.)
+  HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local,
+                               part, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, n_total, n_recs, st));
   if (max_recs) {
     HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
                                st));
     HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, file, file_len, ctx->wal_descs.p, max_recs, 0, 0, nullptr,
-                              ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr, n_dev, st));
+                              ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr, n_total,
+                              (lcrc_wal_rec_dev*)recs, st));
   }
-  HIPCHK(lcrc_launch_wal_finish((lcrc_wal_rec_dev*)recs, n_dev, max_recs, ctx->wal_crcs.p, file, n_recs, st));
   return LCRC_OK;
 }
 

@@ -592,7 +592,8 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
                                                      const uint32_t* __restrict__ win, const uint32_t* __restrict__ gtab,
                                                      uint32_t init, uint32_t xorout, uint32_t flags,
                                                      uint32_t* __restrict__ out, uint32_t* __restrict__ mismatch,
-                                                     const uint64_t* __restrict__ n_dev) {
+                                                     const uint64_t* __restrict__ n_dev,
+                                                     lcrc_wal_rec_dev* __restrict__ recs) {
   __shared__ __attribute__((aligned(16))) uint32_t L[B_LDS_DWORDS];
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long b_entry = __builtin_amdgcn_s_memrealtime();
@@ -731,6 +732,10 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
         bad = !exp_ok || expv != crc;
       }
       if (bad && mismatch) atomicOr(&mismatch[i >> 5], 1u << (i & 31));
+      if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
+        recs[i].crc = crc;
+        recs[i].status = bad ? 1 : 0;
+      }
     }
 #ifdef LCRC_PROBE_CLOCK
     if (!b_first) b_first = __builtin_amdgcn_s_memrealtime();
@@ -750,9 +755,8 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 // ---------------------------------------------------------------------------------------------------
 // WAL scan: k_wal_parse walks the record headers of every 32 KiB log block exactly as
 // LogReader::read_physical_record (src/db/log.rs:204-279) does, minus the checksum (k_blocks computes it,
-// in parallel over all records); k_wal_offsets turns the per-block counts into file-order positions;
-// k_wal_emit writes the records and their descriptors. Nothing returns to the host in between, and the
-// three run on a side stream while k_windows streams the file on the main one.
+// in parallel over all records, and stores it with the verdict in the record); k_wal_emit writes the
+// records and their descriptors at their file-order positions. Nothing returns to the host in between.
 // ---------------------------------------------------------------------------------------------------
 constexpr uint32_t WAL_SLOTS = 64;  // records per block kept by the parse (a block with more is re-walked)
 
@@ -813,41 +817,6 @@ __global__ void __launch_bounds__(256) k_wal_parse(const uint8_t* __restrict__ f
   if (threadIdx.x == 255) part[blockIdx.x] = base + inc;
 }
 
-// file-order position of every block's first record: offsets[b] = (exclusive scan of the parse
-// workgroups' totals)[b / 256] + local[b]; offsets[n] = total. One 1024-thread workgroup.
-__global__ void __launch_bounds__(1024) k_wal_offsets(const uint32_t* __restrict__ local,
-                                                      const uint64_t* __restrict__ part, uint64_t n,
-                                                      uint64_t* __restrict__ offsets) {
-  __shared__ uint64_t carry;
-  __shared__ uint64_t wsum[16];
-  __shared__ uint64_t pex[1024];
-  const uint32_t t = threadIdx.x, lane = __lane_id(), w = t >> 6;
-  const uint64_t nparts = (n + 255) / 256;
-  if (t == 0) carry = 0;
-  __syncthreads();
-  for (uint64_t p0 = 0; p0 < nparts; p0 += 1024) {  // tiles of 1024 parts (256 Ki blocks)
-    const uint64_t i = p0 + t;
-    const uint64_t v = i < nparts ? part[i] : 0;
-    uint64_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t u = __shfl_up(inc, d, 64);
-      if (lane >= (uint32_t)d) inc += u;
-    }
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    uint64_t base = carry;
-    for (uint32_t k = 0; k < w; ++k) base += wsum[k];
-    pex[t] = base + inc - v;
-    __syncthreads();
-    const uint64_t b_lo = p0 * 256, b_hi = (p0 + 1024) * 256 < n ? (p0 + 1024) * 256 : n;
-    for (uint64_t blk = b_lo + t; blk < b_hi; blk += 1024) offsets[blk] = pex[(blk - b_lo) >> 8] + local[blk];
-    if (t == 1023) carry = base + inc;
-    __syncthreads();
-  }
-  if (t == 0) offsets[n] = carry;
-}
-
 __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcrc_desc_dev* __restrict__ descs,
                                         uint64_t o, uint64_t header, uint32_t length, uint32_t type, bool last,
                                         uint32_t stop) {
@@ -867,21 +836,56 @@ __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcr
   descs[o] = d;
 }
 
-// one thread per (block, slot): records in file order at offsets[b] + i (those below max_recs); the
-// thread of the last slot re-walks a block that has more records than slots
+// one thread per (block, slot): records in file order at first(b) + i (those below max_recs); the thread
+// of the last slot re-walks a block that has more records than slots. first(b) = the parse workgroups'
+// totals before b's workgroup (summed by each emit workgroup) + local[b]. Workgroup 0 also writes the total
+// record count to n_total (device) and n_out (device or pinned host memory).
 __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ file, uint64_t nblocks,
                                                   const uint32_t* __restrict__ counts,
                                                   const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
-                                                  const uint64_t* __restrict__ offsets,
+                                                  const uint32_t* __restrict__ local,
+                                                  const uint64_t* __restrict__ part,
                                                   lcrc_wal_rec_dev* __restrict__ recs,
-                                                  lcrc_desc_dev* __restrict__ descs, uint64_t max_recs) {
+                                                  lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
+                                                  uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out) {
+  __shared__ uint64_t red[256];
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
-  if (b >= nblocks) return;
+  const uint64_t nparts = (nblocks + 255) / 256;
+  // sum of the parse workgroups' totals before this workgroup's blocks (all of them for workgroup 0's
+  // total); 256 | 256 / WAL_SLOTS blocks, so one parse workgroup covers every block here
+  const uint64_t upto = blockIdx.x == 0 ? nparts : ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / 256;
+  const uint64_t mine = ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / 256;
+  uint64_t acc = 0, accm = 0;
+  for (uint64_t w = threadIdx.x; w < upto; w += 256) {
+    acc += part[w];
+    if (w < mine) accm += part[w];
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t d = 128; d; d >>= 1) {
+    if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
+    __syncthreads();
+  }
+  const uint64_t total_upto = red[0];
+  __syncthreads();
+  red[threadIdx.x] = accm;
+  __syncthreads();
+  for (uint32_t d = 128; d; d >>= 1) {
+    if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
+    __syncthreads();
+  }
+  const uint64_t base = red[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *n_total = total_upto;
+    if (n_out) *n_out = total_upto;
+  }
+  if (b >= nblocks || max_recs == 0) return;
   const uint32_t cnt = counts[b];
   if (i >= cnt) return;
-  const uint64_t o = offsets[b] + i;
+  const uint64_t first = base + local[b];
+  const uint64_t o = first + i;
   const uint2 sl = slots[g];
   uint32_t at = sl.x & 0xFFFFu, length = sl.x >> 16;
   if (o < max_recs) wal_put(recs, descs, o, b * 32768ull + at, length, sl.y, i + 1 == cnt, stops[b]);
@@ -891,27 +895,12 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
       at += 7 + length;
       uint32_t type;
       wal_header(blk, at, length, type);
-      const uint64_t oj = offsets[b] + j;
+      const uint64_t oj = first + j;
       if (oj < max_recs) wal_put(recs, descs, oj, b * 32768ull + at, length, type, j + 1 == cnt, stops[b]);
     }
   }
 }
 
-// Per-record verdicts: crc from k_blocks, status = the stored header crc differs. The reader's handling
-// of a mismatch (drop the rest of the 32 KiB block, log.rs:260-273) is replayed on the host.
-// n_out (device or pinned host memory) receives the total record count.
-__global__ void __launch_bounds__(256) k_wal_finish(lcrc_wal_rec_dev* __restrict__ recs,
-                                                    const uint64_t* __restrict__ n_dev, uint64_t max_recs,
-                                                    const uint32_t* __restrict__ crcs,
-                                                    const uint8_t* __restrict__ file, uint64_t* __restrict__ n_out) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = *n_dev;
-  const uint64_t n = *n_dev < max_recs ? *n_dev : max_recs;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t c = crcs[i];
-    recs[i].crc = c;
-    recs[i].status = load_le32(file + recs[i].header) != c;
-  }
-}
 
 // ---------------------------------------------------------------------------------------------------
 // small helpers of the table scan and the writer-side seal
@@ -998,35 +987,34 @@ hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint6
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
                               uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
-                              const uint64_t* n_dev, hipStream_t st) {
+                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint64_t per_wg = lcrc_dev::B_THREADS / 16;  // one range per 16-lane row
   uint64_t need = (n + per_wg - 1) / per_wg;
   int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   if (uniform)
     hipLaunchKernelGGL(lcrc_dev::k_blocks<true>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs, n,
-                       ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev);
+                       ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev, recs);
   else
     hipLaunchKernelGGL(lcrc_dev::k_blocks<false>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs,
-                       n, ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev);
+                       n, ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev, recs);
   return hipGetLastError();
 }
 
+// n_total (device): the record count for k_blocks; n_out (device or pinned host, nullable): the same for
+// the caller
 hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
-                                 uint2* slots, uint8_t* stops, uint64_t* offsets, lcrc_wal_rec_dev* recs,
-                                 lcrc_desc_dev* descs, uint64_t max_recs, hipStream_t st) {
+                                 uint2* slots, uint8_t* stops, uint32_t* local, uint64_t* part,
+                                 lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
+                                 uint64_t* n_out, hipStream_t st) {
   const uint64_t nparts = (nblocks + 255) / 256;
-  uint32_t* local = (uint32_t*)(offsets + nblocks + 1);         // scratch after offsets (nblocks u32)
-  uint64_t* part = offsets + nblocks + 1 + (nblocks + 1) / 2;  // then nparts u64
   if (nparts)
     hipLaunchKernelGGL(lcrc_dev::k_wal_parse, dim3((unsigned)nparts), dim3(256), 0, st, file, file_len, nblocks, counts,
                        slots, stops, local, part);
-  hipLaunchKernelGGL(lcrc_dev::k_wal_offsets, dim3(1), dim3(1024), 0, st, local, part, nblocks, offsets);
-  if (max_recs && nblocks) {
-    const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
-    hipLaunchKernelGGL(lcrc_dev::k_wal_emit, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, file, nblocks,
-                       counts, slots, stops, offsets, recs, descs, max_recs);
-  }
+  const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
+  const uint64_t g = (nt + 255) / 256;
+  hipLaunchKernelGGL(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
+                     stops, local, part, recs, descs, max_recs, n_total, n_out);
   return hipGetLastError();
 }
 
@@ -1043,12 +1031,5 @@ hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, cons
   return hipGetLastError();
 }
 
-hipError_t lcrc_launch_wal_finish(lcrc_wal_rec_dev* recs, const uint64_t* n_dev, uint64_t max_recs, const uint32_t* crcs,
-                                  const uint8_t* file, uint64_t* n_out, hipStream_t st) {
-  const uint64_t g = (max_recs + 255) / 256;
-  hipLaunchKernelGGL(lcrc_dev::k_wal_finish, dim3((unsigned)(g < 1 ? 1 : g < 2048 ? g : 2048)), dim3(256), 0, st, recs,
-                     n_dev, max_recs, crcs, file, n_out);
-  return hipGetLastError();
-}
 
 }  // extern "C"
