@@ -198,9 +198,11 @@ __device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t 
 // (the same half of the next region), so every wave keeps between one and two half-tiles in flight.
 __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4 (&v)[8], uint32_t init,
                                               __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+#ifndef LCRC_PROBE_NOTRANSPOSE  // ablation build: walk the pieces as loaded (wrong CRCs, timing only)
   transpose_stage<3>(v);
   transpose_stage<4>(v);
   transpose_stage<5>(v);
+#endif
 #ifdef LCRC_PROBE_NOWALK  // ablation build: fold the data with xor only
   uint32_t p = init;
 #pragma unroll
@@ -299,11 +301,20 @@ struct Share {
 };
 
 __device__ __forceinline__ Share make_share(uint64_t nreg) {
-  Share sh;  // a contiguous range per workgroup
+  Share sh;
+#ifndef LCRC_REGION_CONTIG
+  // regions dealt round-robin over the workgroups: at any moment the whole chip streams one contiguous
+  // stretch of the buffer (memory skeleton: 39.9 us per 256 MiB against 41.4-42.0 with a contiguous
+  // range per workgroup, tools/probe/probe_skel.hip)
+  sh.lo = blockIdx.x;
+  sh.step = gridDim.x;
+  sh.count = nreg > sh.lo ? (nreg - sh.lo + gridDim.x - 1) / gridDim.x : 0;
+#else
   const uint64_t per = (nreg + gridDim.x - 1) / gridDim.x;
   sh.lo = (uint64_t)blockIdx.x * per;
   sh.step = 1;
   sh.count = sh.lo < nreg ? (nreg - sh.lo < per ? nreg - sh.lo : per) : 0;
+#endif
   return sh;
 }
 
@@ -403,7 +414,9 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifndef LCRC_PROBE_NOTABLES  // ablation build: no LDS image (wrong CRCs, timing only)
   build_tables(L, gtab, wv, lane);
+#endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
 #endif

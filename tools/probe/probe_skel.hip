@@ -31,7 +31,9 @@ __device__ __forceinline__ uint32_t voff(uint32_t lane, int h, int j) {
   return 1024u * (8 * h + j) + 16u * lane;
 }
 
-template <int PAT, int THREADS, int REFILL, int WORK>
+//   ASSIGN 0: contiguous share per workgroup, LDS tickets; 1: per-wave grid stride (static);
+//   2: per-workgroup grid stride (region b + G v), LDS tickets
+template <int PAT, int THREADS, int REFILL, int WORK, int ASSIGN = 0>
 __global__ void __launch_bounds__(THREADS) k_skel(const uint8_t* __restrict__ base, uint64_t nreg, uint32_t* out) {
   __shared__ uint32_t ticket;
   const uint32_t lane = __lane_id();
@@ -39,13 +41,21 @@ __global__ void __launch_bounds__(THREADS) k_skel(const uint8_t* __restrict__ ba
   const uint64_t lo = (uint64_t)blockIdx.x * per;
   const uint64_t cnt = lo < nreg ? (nreg - lo < per ? nreg - lo : per) : 0;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  auto region = [&](uint32_t v) -> uint64_t { return v < cnt ? lo + v : ~0ull; };
+  constexpr uint32_t W = THREADS / 64;
+  const uint64_t gw = (uint64_t)blockIdx.x * W + wv, nw = (uint64_t)gridDim.x * W;
+  uint32_t mine = 0;
+  auto region = [&](uint32_t v) -> uint64_t {
+    if (ASSIGN == 1) return gw + (uint64_t)v * nw < nreg ? gw + (uint64_t)v * nw : ~0ull;
+    if (ASSIGN == 2) return blockIdx.x + (uint64_t)v * gridDim.x < nreg ? blockIdx.x + (uint64_t)v * gridDim.x : ~0ull;
+    return v < cnt ? lo + v : ~0ull;
+  };
   auto take = [&]() -> uint64_t {
+    if (ASSIGN == 1) return region(++mine);
     uint32_t v = 0;
     if (lane == 0) v = atomicAdd(&ticket, 1u);
     return region(__builtin_amdgcn_readfirstlane(v));
   };
-  uint64_t t = region(wv);
+  uint64_t t = ASSIGN == 1 ? region(0) : region(wv);
   u32x4 va[8], vb[8];
   {
     auto rs = rsrc(base, t, nreg);
@@ -132,23 +142,22 @@ int main() {
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
   const uint64_t nreg = NB / REGION;
   auto rep = [&](const char* name, float ms) { printf("%-40s %7.1f us  %7.1f GB/s\n", name, ms * 1e3, NB / ms / 1e6); };
-#define RUN(PAT, TH, WPC, RF, WK)                                                                            \
-  rep("pat" #PAT " thr" #TH " wg/cu" #WPC " refill" #RF " work" #WK,                                          \
-      best_ms([&](int i) { k_skel<PAT, TH, RF, WK><<<ncu * WPC, TH>>>(buf + (i % NBUF) * NB, nreg, out); }, 50));
-  RUN(0, 512, 2, 0, 0)
-  RUN(1, 512, 2, 0, 0)
-  RUN(0, 512, 2, 1, 0)
-  RUN(1, 512, 2, 1, 0)
-  RUN(0, 256, 4, 0, 0)
-  RUN(1, 256, 4, 0, 0)
-  RUN(0, 256, 2, 0, 0)
-  RUN(1, 256, 2, 0, 0)
-  RUN(0, 1024, 1, 0, 0)
-  RUN(1, 1024, 1, 0, 0)
-  RUN(0, 512, 2, 0, 8)
-  RUN(1, 512, 2, 0, 8)
-  RUN(0, 512, 2, 1, 8)
-  RUN(1, 512, 2, 1, 8)
-  RUN(0, 512, 2, 0, 0)
+#define RUN(PAT, TH, WPC, RF, WK, AS)                                                                        \
+  rep("pat" #PAT " thr" #TH " wg/cu" #WPC " refill" #RF " work" #WK " assign" #AS,                            \
+      best_ms([&](int i) { k_skel<PAT, TH, RF, WK, AS><<<ncu * WPC, TH>>>(buf + (i % NBUF) * NB, nreg, out); }, 50));
+  RUN(0, 512, 1, 0, 0, 0)
+  RUN(0, 512, 1, 0, 0, 1)
+  RUN(0, 512, 1, 0, 0, 2)
+  RUN(0, 512, 1, 1, 0, 0)
+  RUN(0, 512, 1, 1, 0, 1)
+  RUN(1, 512, 1, 0, 0, 1)
+  RUN(1, 512, 1, 1, 0, 1)
+  RUN(0, 512, 2, 0, 0, 0)
+  RUN(0, 512, 2, 0, 0, 1)
+  RUN(0, 256, 4, 0, 0, 0)
+  RUN(0, 256, 4, 0, 0, 1)
+  RUN(0, 512, 1, 0, 8, 0)
+  RUN(0, 512, 1, 0, 8, 1)
+  RUN(0, 512, 1, 0, 0, 0)
   return 0;
 }
