@@ -27,6 +27,8 @@
  *   lcrc_table_scan                     <- Table::open with paranoid_checks (table.rs:39-103) followed by
  *                                          read_block_from_file(verify_checksum) (format.rs:146-171) of
  *                                          every data, filter, metaindex and index block: one batched verify
+ *   lcrc_snappy_frames                  <- snap::read::FrameDecoder at format.rs:194-206 (decode + the masked
+ *                                          CRC-32C of every chunk), for a batch of frames on the device
  *   lcrc_batch_seal                     <- (1)/(3) for a batch: the trailer CRCs of write_raw_block
  *                                          (table.rs:519-527) or the header CRCs of emit_physical_record
  *                                          (log.rs:61-70), computed and stored in place on the device
@@ -190,6 +192,17 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
  * also receives the values. Covered ranges must not contain another descriptor's CRC slot. */
 int lcrc_batch_seal(lcrc_ctx* ctx, uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
                     uint32_t* out_crc, void* stream);
+
+/* Snappy framing, on the device: the `snap` crate's FrameDecoder as read_block_from_file uses it for
+ * compressed blocks (src/sstable/format.rs:194-206; written by FrameEncoder, table.rs:481-497). Decodes the
+ * n frames base[frames[i].offset, +length) (device; expect_rel ignored) into out (device, capacity out_cap):
+ * frame i's bytes at out_off[i] (device, n + 1 entries, out_off[n] = total). Every data chunk's masked
+ * CRC-32C of its uncompressed bytes is checked whatever the context's mode. status[i] (device): 0 ok,
+ * 1 bad framing or Snappy data, 2 chunk CRC mismatch -- both are read_block_from_file's "corrupted
+ * compressed block content". *total (host) receives the decoded size; LCRC_ERANGE (nothing decoded) when
+ * it exceeds out_cap. Synchronous. */
+int lcrc_snappy_frames(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc* frames, size_t n, uint8_t* out,
+                       uint64_t out_cap, uint64_t* out_off, uint8_t* status, uint64_t* total);
 
 /* ---- device memory helpers (so a binding needs nothing but this library) ---- */
 int lcrc_dev_alloc(int device, size_t bytes, void** out);

@@ -82,7 +82,7 @@ ABI_SYMBOLS = [
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
-    "lcrc_table_scan", "lcrc_batch_seal",
+    "lcrc_table_scan", "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
     "lcrc_last_error", "lcrc_version",
@@ -129,6 +129,7 @@ def lib():
     sig("lcrc_wal_scan_async", i32, vp, vp, u64, vp, sz, vp, vp)
     sig("lcrc_table_scan", i32, vp, vp, u64, cp, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp, sz)
     sig("lcrc_batch_seal", i32, vp, vp, u64, vp, sz, vp, vp)
+    sig("lcrc_snappy_frames", i32, vp, vp, vp, sz, vp, u64, vp, vp, ctypes.POINTER(ctypes.c_uint64))
     sig("lcrc_snappy_frame_decode", ctypes.c_int64, vp, sz, vp, sz)
     sig("lcrc_dev_alloc", i32, i32, sz, ctypes.POINTER(vp))
     sig("lcrc_dev_free", i32, vp)
@@ -438,6 +439,30 @@ class Engine:
         """Compute each descriptor's CRC and store it at base[offset + expect_rel] (device, in place)."""
         _check(lib().lcrc_batch_seal(self.ctx, _ptr(base), int(base_len), _ptr(descs), int(n), _ptr(out_crc), stream),
                "lcrc_batch_seal")
+
+    def snappy_frames(self, base, frames_dev, n, out=None, out_cap=0):
+        """lcrc_snappy_frames: (decoded bytes per frame as a list, status array). base / frames_dev / out are
+        device buffers; with out None the decoded size is queried first and a buffer allocated."""
+        total = ctypes.c_uint64(0)
+        off = DeviceBuffer(8 * (n + 1), self.device)
+        st = DeviceBuffer(max(1, n), self.device)
+        own = out is None
+        if own:
+            rc = lib().lcrc_snappy_frames(self.ctx, _ptr(base), _ptr(frames_dev), int(n), None, 0, off.ptr, st.ptr,
+                                          ctypes.byref(total))
+            if rc not in (OK, ERANGE):
+                _check(rc, "lcrc_snappy_frames")
+            out = DeviceBuffer(max(1, total.value), self.device)
+            out_cap = total.value
+        _check(lib().lcrc_snappy_frames(self.ctx, _ptr(base), _ptr(frames_dev), int(n), _ptr(out), int(out_cap),
+                                        off.ptr, st.ptr, ctypes.byref(total)), "lcrc_snappy_frames")
+        offs = off.download(np.uint64, n + 1)
+        data = out.download(np.uint8, int(offs[n])) if n else np.zeros(0, np.uint8)
+        status = st.download(np.uint8, n)
+        frames_out = [data[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(n)]
+        for b in (off, st) + ((out,) if own else ()):
+            b.close()
+        return frames_out, status
 
     def timer_start(self):
         _check(lib().lcrc_timer_start(self.ctx), "lcrc_timer_start")

@@ -30,6 +30,15 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  uint2* slots, uint8_t* stops, uint32_t* local, uint64_t* part,
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
+hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
+                                   uint64_t* nchunks, uint8_t* status, hipStream_t st);
+hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
+                             uint64_t* part, hipStream_t st);
+hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
+                                     const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
+                                     lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, hipStream_t st);
+hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
+                                    const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
 hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
@@ -102,6 +111,13 @@ struct lcrc_ctx {
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs;
   uint64_t* h_count = nullptr;  // pinned: record count of the synchronous WAL scan
+  // Snappy frames: chunk CRCs are CRC-32C whatever the context's mode
+  uint32_t* d_tab_c = nullptr;  // CRC-32C image when mode != C (created on first use)
+  DevBuf<uint64_t> sn_size, sn_nch, sn_choff, sn_part;
+  DevBuf<lcrc_desc_dev> sn_cdesc;
+  DevBuf<uint32_t> sn_cexp, sn_cframe, sn_ccrc;
+  DevBuf<uint64_t> sn_out_off;  // table scan: frame output offsets
+  DevBuf<uint8_t> sn_out, sn_status;
   DevBuf<lcrc_desc_dev> tbl_descs;  // table scan / seal
   DevBuf<uint32_t> tbl_crcs, tbl_mm;
   DevBuf<uint64_t> tbl_pos;
@@ -109,6 +125,26 @@ struct lcrc_ctx {
 };
 
 namespace {
+
+// The per-mode constant image (TAB_* layout, lcrc_device.h), uploaded to a new device allocation.
+int upload_tables(int mode, uint32_t** d_tab) {
+  const uint32_t poly = lcrc::poly_of(mode);
+  std::vector<uint32_t> tab(TAB_TOTAL);
+  lcrc::make_slice_tables(poly, tab.data() + TAB_SLICE, 4);
+  for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 16ull << m, tab.data() + TAB_ZPIECE + m * 1024);
+  for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 256ull << m, tab.data() + TAB_ZWIN + m * 1024);
+  lcrc::make_shift_tables(poly, 4096, tab.data() + TAB_Z4096);
+  // k_windows builds its LDS image from columns (entries 1, 2, 4, .., 128) of the byte tables it uses
+  for (int t = 0; t < 20; ++t) {
+    const uint32_t src = t < 4 ? TAB_SLICE + t * 256                    // S0: T_p
+                         : t < 8 ? TAB_ZPIECE + 2048 + (7 - t) * 256      // S1: Z64[3 - p], p = t - 4
+                                 : TAB_ZWIN + (t - 8) * 256;              // Z256, Z512, Z1024
+    for (int i = 0; i < 8; ++i) tab[TAB_COLS + t * 8 + i] = tab[src + (1u << i)];
+  }
+  HIPCHK(hipMalloc(d_tab, TAB_TOTAL * sizeof(uint32_t)));
+  HIPCHK(hipMemcpy(*d_tab, tab.data(), TAB_TOTAL * sizeof(uint32_t), hipMemcpyHostToDevice));
+  return LCRC_OK;
+}
 
 int set_device(lcrc_ctx* ctx) {
   HIPCHK(hipSetDevice(ctx->device));
@@ -180,21 +216,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
 
   // constant tables for this mode
   const uint32_t poly = lcrc::poly_of(mode);
-  std::vector<uint32_t> tab(TAB_TOTAL);
-  lcrc::make_slice_tables(poly, tab.data() + TAB_SLICE, 4);
-  for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 16ull << m, tab.data() + TAB_ZPIECE + m * 1024);
-  for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 256ull << m, tab.data() + TAB_ZWIN + m * 1024);
-  lcrc::make_shift_tables(poly, 4096, tab.data() + TAB_Z4096);
-  // k_windows builds its LDS image from columns (entries 1, 2, 4, .., 128) of the byte tables it uses
-  for (int t = 0; t < 20; ++t) {
-    const uint32_t src = t < 4 ? TAB_SLICE + t * 256                    // S0: T_p
-                         : t < 8 ? TAB_ZPIECE + 2048 + (7 - t) * 256      // S1: Z64[3 - p], p = t - 4
-                                 : TAB_ZWIN + (t - 8) * 256;              // Z256, Z512, Z1024
-    for (int i = 0; i < 8; ++i) tab[TAB_COLS + t * 8 + i] = tab[src + (1u << i)];
-  }
-  if ((e = hipMalloc(&ctx->d_tab, TAB_TOTAL * sizeof(uint32_t))) != hipSuccess) return bail(fail_hip(e, "hipMalloc"));
-  if ((e = hipMemcpy(ctx->d_tab, tab.data(), TAB_TOTAL * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess)
-    return bail(fail_hip(e, "hipMemcpy"));
+  if ((rc = upload_tables(mode, &ctx->d_tab)) != LCRC_OK) return bail(rc);
   ctx->fin4096 = lcrc::zshift(ctx->init, 4096, poly) ^ ctx->xorout;
   *out = ctx;
   return LCRC_OK;
@@ -219,6 +241,12 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->wal_descs.release();
   ctx->wal_crcs.release();
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
+  if (ctx->d_tab_c) (void)hipFree(ctx->d_tab_c);
+  for (auto* b : {&ctx->sn_size, &ctx->sn_nch, &ctx->sn_choff, &ctx->sn_part, &ctx->sn_out_off}) b->release();
+  for (auto* b : {&ctx->sn_cexp, &ctx->sn_cframe, &ctx->sn_ccrc}) b->release();
+  ctx->sn_cdesc.release();
+  ctx->sn_out.release();
+  ctx->sn_status.release();
   ctx->tbl_descs.release();
   ctx->tbl_crcs.release();
   ctx->tbl_mm.release();
@@ -435,6 +463,53 @@ int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wa
   const uint64_t total = *ctx->h_count;
   *n_recs = total;
   return total > max_recs ? LCRC_EINVAL : LCRC_OK;
+}
+
+// ---- Snappy framing: decode + per-chunk masked CRC-32C verify ----
+static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* frames, size_t n, uint8_t* out,
+                              uint64_t out_cap, uint64_t* out_off, uint8_t* status, uint64_t* total_out, hipStream_t st) {
+  int rc;
+  *total_out = 0;
+  if (n == 0) return LCRC_OK;
+  const size_t nparts = (n + 255) / 256;
+  if ((rc = ctx->sn_size.ensure(n)) || (rc = ctx->sn_nch.ensure(n)) || (rc = ctx->sn_choff.ensure(n + 1)) ||
+      (rc = ctx->sn_part.ensure(2 * nparts)))
+    return rc;
+  HIPCHK(lcrc_launch_snappy_size(base, frames, n, ctx->sn_size.p, ctx->sn_nch.p, status, st));
+  HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, n, out_off, ctx->sn_choff.p, ctx->sn_part.p, st));
+  uint64_t tot[2];
+  HIPCHK(hipMemcpyAsync(&tot[0], out_off + n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&tot[1], ctx->sn_choff.p + n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  *total_out = tot[0];
+  if (tot[0] > out_cap || (tot[0] && !out)) return LCRC_ERANGE;
+  const uint64_t nch = tot[1];
+  if (nch == 0) return LCRC_OK;
+  if ((rc = ctx->sn_cdesc.ensure(nch)) || (rc = ctx->sn_cexp.ensure(nch)) || (rc = ctx->sn_cframe.ensure(nch)) ||
+      (rc = ctx->sn_ccrc.ensure(nch)) || (rc = ctx->win.ensure(window_words(tot[0]))))
+    return rc;
+  if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
+  const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
+  HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
+                                   ctx->sn_cexp.p, ctx->sn_cframe.p, st));
+  // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
+  HIPCHK(lcrc_launch_windows(false, ctx->grid_a, out, tot[0], tab_c, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
+  HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, out, tot[0], ctx->sn_cdesc.p, nch, 0, 0, nullptr, ctx->win.p, tab_c,
+                            lcrc::CRC_INIT, lcrc::CRC_XOROUT, LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr, nullptr, nullptr,
+                            st));
+  HIPCHK(lcrc_launch_snappy_check(ctx->sn_ccrc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, ctx->sn_choff.p + n, nch, status,
+                                  st));
+  HIPCHK(hipStreamSynchronize(st));
+  return LCRC_OK;
+}
+
+int lcrc_snappy_frames(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc* frames, size_t n, uint8_t* out,
+                       uint64_t out_cap, uint64_t* out_off, uint8_t* status, uint64_t* total) {
+  if (!ctx || !total || (n && (!base || !frames || !out_off || !status))) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return snappy_frames_impl(ctx, base, (const lcrc_desc_dev*)frames, n, out, out_cap, out_off, status, total,
+                            ctx->stream);
 }
 
 // ---- whole-table verify scan ----

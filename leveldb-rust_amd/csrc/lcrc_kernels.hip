@@ -916,6 +916,286 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
 
 
 // ---------------------------------------------------------------------------------------------------
+// Snappy framing (the `snap` crate's FrameEncoder / FrameDecoder used for compressed SSTable blocks,
+// src/sstable/table.rs:481-497, src/sstable/format.rs:194-206; framing format: stream identifier
+// ff 06 00 00 "sNaPpY", chunks [type u8][length u24 LE][body]; data chunks 0x00 (Snappy-compressed) and
+// 0x01 (uncompressed) start with the masked CRC-32C of their uncompressed bytes, at most 65,536 of them;
+// 0xfe padding and 0x80..0xfd are skipped, 0x02..0x7f are fatal). One lane per frame walks its chunks;
+// the chunk CRCs are computed by the general path over the decoded bytes.
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return *p; }
+
+// Snappy raw-format length preamble (varint32) of a compressed chunk's data; false when malformed
+__device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32_t& ulen, uint32_t& used) {
+  ulen = 0;
+  for (uint32_t i = 0; i < 5 && i < n; ++i) {
+    const uint32_t b = ld_u8(p + i);
+    ulen |= (b & 127u) << (7 * i);
+    if (!(b & 128)) {
+      used = i + 1;
+      return true;
+    }
+  }
+  return false;
+}
+
+// pass 1: decoded size, data-chunk count and framing verdict of every frame
+__global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__ base,
+                                                     const lcrc_desc_dev* __restrict__ frames, uint64_t n,
+                                                     uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
+                                                     uint8_t* __restrict__ status) {
+  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  const uint8_t* p = base + frames[f].offset;
+  const uint32_t len = frames[f].length;
+  uint64_t total = 0, chunks = 0;
+  bool ok = true, seen_id = false;
+  uint32_t at = 0;
+  while (ok && at < len) {
+    if (len - at < 4) {
+      ok = false;
+      break;
+    }
+    const uint32_t type = ld_u8(p + at);
+    const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
+    at += 4;
+    if (len - at < cl) {
+      ok = false;
+      break;
+    }
+    if (type == 0xff) {
+      ok = cl == 6 && ld_u8(p + at) == 's' && ld_u8(p + at + 1) == 'N' && ld_u8(p + at + 2) == 'a' &&
+           ld_u8(p + at + 3) == 'P' && ld_u8(p + at + 4) == 'p' && ld_u8(p + at + 5) == 'Y';
+      seen_id = true;
+    } else if (!seen_id) {
+      ok = false;
+    } else if (type <= 1) {
+      uint32_t ulen = cl >= 4 ? cl - 4 : 0, used = 0;
+      if (cl < 4) ok = false;
+      else if (type == 0) ok = snappy_ulen(p + at + 4, cl - 4, ulen, used);
+      if (ulen > 65536) ok = false;
+      total += ulen;
+      ++chunks;
+    } else if (type <= 0x7f) {
+      ok = false;  // reserved unskippable
+    }
+    at += cl;
+  }
+  size[f] = ok ? total : 0;
+  nchunks[f] = ok ? chunks : 0;
+  status[f] = ok ? 0 : 1;
+}
+
+// exclusive scans of two u64 arrays (n entries): per-workgroup part, then every element adds the totals
+// of the workgroups before it; out_a[n], out_b[n] = the totals
+__global__ void __launch_bounds__(256) k_scan2_local(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                     uint64_t n, uint64_t* __restrict__ out_a,
+                                                     uint64_t* __restrict__ out_b, uint64_t* __restrict__ part) {
+  __shared__ uint64_t sa[256], sb[256];
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+  const uint64_t va = i < n ? a[i] : 0, vb = i < n ? b[i] : 0;
+  sa[t] = va;
+  sb[t] = vb;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    const uint64_t xa = t >= d ? sa[t - d] : 0, xb = t >= d ? sb[t - d] : 0;
+    __syncthreads();
+    sa[t] += xa;
+    sb[t] += xb;
+    __syncthreads();
+  }
+  if (i < n) {
+    out_a[i] = sa[t] - va;
+    out_b[i] = sb[t] - vb;
+  }
+  if (t == 255) {
+    part[2 * blockIdx.x] = sa[255];
+    part[2 * blockIdx.x + 1] = sb[255];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_scan2_add(uint64_t n, uint64_t* __restrict__ out_a,
+                                                   uint64_t* __restrict__ out_b, const uint64_t* __restrict__ part) {
+  __shared__ uint64_t ra[256], rb[256];
+  const uint32_t t = threadIdx.x;
+  const uint64_t nparts = (n + 255) / 256;
+  const uint64_t upto = blockIdx.x == gridDim.x - 1 ? nparts : blockIdx.x;  // the last also sums for the totals
+  uint64_t xa = 0, xb = 0, ma = 0, mb = 0;
+  for (uint64_t w = t; w < upto; w += 256) {
+    xa += part[2 * w];
+    xb += part[2 * w + 1];
+    if (w < blockIdx.x) {
+      ma += part[2 * w];
+      mb += part[2 * w + 1];
+    }
+  }
+  ra[t] = ma;
+  rb[t] = mb;
+  __syncthreads();
+  for (uint32_t d = 128; d; d >>= 1) {
+    if (t < d) {
+      ra[t] += ra[t + d];
+      rb[t] += rb[t + d];
+    }
+    __syncthreads();
+  }
+  const uint64_t ba = ra[0], bb = rb[0];
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+  if (i < n) {
+    out_a[i] += ba;
+    out_b[i] += bb;
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    ra[t] = xa;
+    rb[t] = xb;
+    __syncthreads();
+    for (uint32_t d = 128; d; d >>= 1) {
+      if (t < d) {
+        ra[t] += ra[t + d];
+        rb[t] += rb[t + d];
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      out_a[n] = ra[0];
+      out_b[n] = rb[0];
+    }
+  }
+}
+
+// pass 2: decode frame f into out[out_off[f] ..) and describe its data chunks for the CRC pass:
+// cdesc (offset into out, length), cexp (stored masked CRC-32C), cframe (frame index)
+__global__ void __launch_bounds__(256) k_snappy_decode(const uint8_t* __restrict__ base,
+                                                       const lcrc_desc_dev* __restrict__ frames, uint64_t n,
+                                                       const uint64_t* __restrict__ out_off,
+                                                       const uint64_t* __restrict__ chunk_off,
+                                                       uint8_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                       lcrc_desc_dev* __restrict__ cdesc, uint32_t* __restrict__ cexp,
+                                                       uint32_t* __restrict__ cframe) {
+  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n || status[f]) return;
+  const uint8_t* p = base + frames[f].offset;
+  const uint32_t len = frames[f].length;
+  uint64_t o = out_off[f];
+  const uint64_t o_end = out_off[f + 1];
+  uint64_t c = chunk_off[f];
+  bool ok = true;
+  uint32_t at = 0;
+  while (ok && at < len) {
+    const uint32_t type = ld_u8(p + at);
+    const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
+    at += 4;
+    const uint8_t* body = p + at;
+    at += cl;
+    if (type > 1) continue;  // stream identifiers and skippable chunks (validated by pass 1)
+    const uint32_t want = ld_u8(body) | (ld_u8(body + 1) << 8) | (ld_u8(body + 2) << 16) | (ld_u8(body + 3) << 24);
+    const uint64_t start = o;
+    if (type == 1) {
+      for (uint32_t k = 4; k < cl; ++k) out[o++] = body[k];
+    } else {
+      uint32_t ulen, used;
+      snappy_ulen(body + 4, cl - 4, ulen, used);
+      const uint8_t* q = body + 4 + used;
+      const uint8_t* qe = body + cl;
+      const uint64_t lim = start + ulen;
+      while (ok && q < qe) {
+        const uint32_t tag = *q++;
+        uint32_t ln, off;
+        if ((tag & 3) == 0) {  // literal
+          ln = tag >> 2;
+          if (ln >= 60) {
+            const uint32_t nb = ln - 59;
+            if ((uint64_t)(qe - q) < nb) {
+              ok = false;
+              break;
+            }
+            ln = 0;
+            for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)q[k] << (8 * k);
+            q += nb;
+          }
+          ln += 1;
+          if ((uint64_t)(qe - q) < ln || o + ln > lim) {
+            ok = false;
+            break;
+          }
+          for (uint32_t k = 0; k < ln; ++k) out[o + k] = q[k];
+          o += ln;
+          q += ln;
+          continue;
+        }
+        if ((tag & 3) == 1) {
+          if (q >= qe) {
+            ok = false;
+            break;
+          }
+          ln = 4 + ((tag >> 2) & 7);
+          off = ((tag >> 5) << 8) | *q++;
+        } else if ((tag & 3) == 2) {
+          if (qe - q < 2) {
+            ok = false;
+            break;
+          }
+          ln = 1 + (tag >> 2);
+          off = q[0] | ((uint32_t)q[1] << 8);
+          q += 2;
+        } else {
+          if (qe - q < 4) {
+            ok = false;
+            break;
+          }
+          ln = 1 + (tag >> 2);
+          off = q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+          q += 4;
+        }
+        if (off == 0 || off > o - start || o + ln > lim) {
+          ok = false;
+          break;
+        }
+        for (uint32_t k = 0; k < ln; ++k, ++o) out[o] = out[o - off];  // overlapping copies byte by byte
+      }
+      if (ok && o != lim) ok = false;
+    }
+    if (!ok || o > o_end) break;
+    lcrc_desc_dev d;
+    d.offset = start;
+    d.length = (uint32_t)(o - start);
+    d.expect_rel = LCRC_NO_EXPECT_DEV;
+    cdesc[c] = d;
+    cexp[c] = want;
+    cframe[c] = (uint32_t)f;
+    ++c;
+  }
+  if (!ok) {
+    status[f] = 1;
+    // the chunk slots this frame did not fill: empty ranges that match by construction
+    for (const uint64_t ce = chunk_off[f + 1]; c < ce; ++c) {
+      lcrc_desc_dev d;
+      d.offset = 0;
+      d.length = 0;
+      d.expect_rel = LCRC_NO_EXPECT_DEV;
+      cdesc[c] = d;
+      cexp[c] = 0;
+      cframe[c] = (uint32_t)f;
+    }
+  }
+}
+
+// a chunk whose masked CRC-32C differs from the stored one marks its frame corrupt (frames already
+// marked corrupt by the decode are skipped: their empty placeholder chunks carry no CRC)
+__global__ void __launch_bounds__(256) k_snappy_check(const uint32_t* __restrict__ crc,
+                                                      const uint32_t* __restrict__ cexp,
+                                                      const uint32_t* __restrict__ cframe,
+                                                      const uint64_t* __restrict__ nch, uint8_t* __restrict__ status) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= *nch) return;
+  const uint32_t f = cframe[c];
+  if (status[f] == 1) return;
+  if (crc[c] != cexp[c]) status[f] = 2;  // 2: CRC mismatch (reported like 1)
+}
+
+// ---------------------------------------------------------------------------------------------------
 // small helpers of the table scan and the writer-side seal
 // ---------------------------------------------------------------------------------------------------
 // out[i] = base[pos[i]] (the type bytes of a table's blocks)
@@ -1028,6 +1308,41 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
   const uint64_t g = (nt + 255) / 256;
   hipLaunchKernelGGL(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
                      stops, local, part, recs, descs, max_recs, n_total, n_out);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
+                                   uint64_t* nchunks, uint8_t* status, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_snappy_size, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, frames, n, size,
+                     nchunks, status);
+  return hipGetLastError();
+}
+
+// out_a / out_b: n + 1 entries (exclusive scans, totals at [n]); part: 2 * ceil(n / 256) scratch words
+hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
+                             uint64_t* part, hipStream_t st) {
+  const uint64_t g = (n + 255) / 256;
+  if (g == 0) return hipMemsetAsync(out_a, 0, 8, st) == hipSuccess ? hipMemsetAsync(out_b, 0, 8, st) : hipErrorUnknown;
+  hipLaunchKernelGGL(lcrc_dev::k_scan2_local, dim3((unsigned)g), dim3(256), 0, st, a, b, n, out_a, out_b, part);
+  hipLaunchKernelGGL(lcrc_dev::k_scan2_add, dim3((unsigned)g), dim3(256), 0, st, n, out_a, out_b, part);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
+                                     const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
+                                     lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_snappy_decode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, frames, n,
+                     out_off, chunk_off, out, status, cdesc, cexp, cframe);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
+                                    const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st) {
+  if (nch_bound == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_snappy_check, dim3((unsigned)((nch_bound + 255) / 256)), dim3(256), 0, st, crc, cexp,
+                     cframe, nch, status);
   return hipGetLastError();
 }
 

@@ -284,3 +284,57 @@ def test_seal_wal_headers(lcrc, orc, engines):
     assert dev.download(np.uint8, len(f)).tobytes() == f
     dev.close()
     dd.close()
+
+
+# ---------------------------------------------------------------------------------------------------
+# Snappy framing on the device (§8(f) rank 4): decode + masked CRC-32C of every chunk
+# ---------------------------------------------------------------------------------------------------
+def _frames_on_device(lcrc, streams):
+    blob = b"".join(streams)
+    offs = np.cumsum([0] + [len(x) for x in streams])[:-1]
+    d = np.zeros(len(streams), lcrc.DESC_DTYPE)
+    d["offset"], d["length"], d["expect_rel"] = offs, [len(x) for x in streams], lcrc.NO_EXPECT
+    base = lcrc.DeviceBuffer.from_host(np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8))
+    dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8) if len(d) else np.zeros(16, np.uint8))
+    return base, dd
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_snappy_frames_device(lcrc, orc, engines, mode):
+    rng = np.random.default_rng(9)
+    raw = []
+    for k in range(300):
+        n = int(rng.integers(0, 3 * 65536)) if k % 50 == 0 else int(rng.integers(0, 6000))
+        a = rng.integers(0, 256, n // 2, dtype=np.uint8).tobytes()
+        raw.append((a + b"leveldb-rust " * (n // 13 + 1))[:n])
+    streams = [orc.snappy_frame_encode(x) for x in raw]
+    # uncompressed data chunks, padding, skippable chunks and a repeated stream identifier
+    streams.append(bytes(streams[1][:10]) + b"\x01\x09\x00\x00" + orc.mask(orc.crc(b"abcde", 1)).to_bytes(4, "little")
+                   + b"abcde" + b"\xfe\x02\x00\x00zz" + b"\x85\x01\x00\x00q" + bytes(streams[1][:10]))
+    raw.append(b"abcde")
+    base, dd = _frames_on_device(lcrc, streams)
+    got, status = engines[mode].snappy_frames(base, dd, len(streams))
+    assert status.tolist() == [0] * len(streams)
+    assert got == raw
+
+
+@pytest.mark.gpu
+def test_snappy_frames_device_corruption(lcrc, orc, engines):
+    good = orc.snappy_frame_encode(b"abcdefgh" * 3000 + bytes(range(256)) * 10)
+    cases = {
+        "chunk crc": bytearray(good),
+        "no stream id": bytearray(good[10:]),
+        "truncated": bytearray(good[:-3]),
+        "unskippable": bytearray(good[:10] + b"\x02\x01\x00\x00q" + good[10:]),
+        "bad literal": bytearray(good),
+    }
+    cases["chunk crc"][12] ^= 1
+    cases["bad literal"][len(good) - 5] ^= 0x40
+    streams = [good] + [bytes(v) for v in cases.values()] + [good]
+    base, dd = _frames_on_device(lcrc, streams)
+    got, status = engines[lcrc.MODE_REF].snappy_frames(base, dd, len(streams))
+    want = [0 if orc.snappy_frame_decode(s) is not None else 1 for s in streams]
+    assert [int(x != 0) for x in status] == want
+    assert want[1:-1] == [1] * len(cases)
+    assert got[0] == got[-1] == orc.snappy_frame_decode(good)
