@@ -162,7 +162,7 @@ typedef struct lcrc_tblk {
   uint32_t crc;     /* computed CRC of data[0..n+1] (masked if LCRC_FLAG_MASK) */
   uint8_t kind;     /* LCRC_TBLK_DATA / _FILTER / _METAINDEX / _INDEX */
   uint8_t type;     /* stored type byte data[n] (0 raw, 1 snappy, other: "bad block type" on read) */
-  uint8_t status;   /* LCRC_TBLK_OK / _CRC_MISMATCH / _TRUNCATED */
+  uint8_t status;   /* LCRC_TBLK_OK / _CRC_MISMATCH / _TRUNCATED / _BAD_CONTENT / _BAD_TYPE */
   uint8_t reserved;
 } lcrc_tblk;
 #define LCRC_TBLK_DATA 0
@@ -172,11 +172,15 @@ typedef struct lcrc_tblk {
 #define LCRC_TBLK_OK 0
 #define LCRC_TBLK_CRC_MISMATCH 1 /* read_block_from_file(verify) -> "block checksum mismatch" */
 #define LCRC_TBLK_TRUNCATED 2    /* handle past the end of the file -> "truncated block read" */
+#define LCRC_TBLK_BAD_CONTENT 3  /* good checksum, type 1, Snappy frames corrupt -> "corrupted compressed block content" */
+#define LCRC_TBLK_BAD_TYPE 4     /* good checksum, type byte > 1 -> "bad block type" */
 
 /* Whole-table verify scan of a device-resident SSTable file (file_len bytes). The host reads the footer
  * and the index block (verified: paranoid_checks), and -- when filter_name is non-NULL, as read_meta does
  * for a filter policy -- the metaindex block and the "filter" + filter_name entry; then ONE batched
- * device pass checksums every data, filter, metaindex and index block. blocks (host, capacity
+ * device pass checksums every data, filter, metaindex and index block, and every block whose checksum
+ * holds is put through read_block_from_file's type dispatch: Snappy-framed blocks (type 1) are decoded
+ * and their chunk CRCs checked on the device (lcrc_snappy_frames), other types > 1 are bad. blocks (host, capacity
  * max_blocks) receives them sorted by offset; *n_blocks the count (LCRC_ERANGE if it exceeds
  * max_blocks; blocks may be NULL to query). Structural corruption returns LCRC_ECORRUPT with the
  * reference's message ("file is too short to be an sstable", "not an sstable (bad magic number)",

@@ -55,7 +55,7 @@ DESC_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("expect_rel", "<i4
 TBLK_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u8"), ("crc", "<u4"), ("kind", "u1"), ("type", "u1"),
                        ("status", "u1"), ("reserved", "u1")])
 TBLK_DATA, TBLK_FILTER, TBLK_METAINDEX, TBLK_INDEX = 0, 1, 2, 3
-TBLK_OK, TBLK_CRC_MISMATCH, TBLK_TRUNCATED = 0, 1, 2
+TBLK_OK, TBLK_CRC_MISMATCH, TBLK_TRUNCATED, TBLK_BAD_CONTENT, TBLK_BAD_TYPE = 0, 1, 2, 3, 4
 WAL_REC_DTYPE = np.dtype([("header", "<u8"), ("length", "<u4"), ("type", "u1"), ("status", "u1"),
                           ("block_end", "<u2"), ("crc", "<u4"), ("stop", "<u4")])
 

@@ -624,11 +624,43 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
     HIPCHK(hipMemcpyAsync(mm.data(), ctx->tbl_mm.p, mm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(types.data(), ctx->tbl_types.p, m, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    std::vector<lcrc_desc_dev> frames;
+    std::vector<size_t> fwhich;
     for (size_t k = 0; k < m; ++k) {
       lcrc_tblk& b = found[which[k]];
       b.crc = crcs[k];
       b.type = types[k];
       b.status = ((mm[k >> 5] >> (k & 31)) & 1) ? LCRC_TBLK_CRC_MISMATCH : LCRC_TBLK_OK;
+      // read_block_from_file's type dispatch after a good checksum (format.rs:175-210)
+      if (b.status == LCRC_TBLK_OK && b.type > 1) b.status = LCRC_TBLK_BAD_TYPE;
+      if (b.status == LCRC_TBLK_OK && b.type == 1 && b.size <= 0xFFFFFFFFull) {
+        lcrc_desc_dev f;
+        f.offset = b.offset;
+        f.length = (uint32_t)b.size;
+        f.expect_rel = LCRC_NO_EXPECT_DEV;
+        frames.push_back(f);
+        fwhich.push_back(which[k]);
+      }
+    }
+    // Snappy-framed blocks: decoded and their chunk CRCs checked on the device, all in one batch
+    const size_t nf = frames.size();
+    if (nf) {
+      if ((rc = ctx->tbl_descs.ensure(nf)) || (rc = ctx->sn_out_off.ensure(nf + 1)) || (rc = ctx->sn_status.ensure(nf)))
+        return rc;
+      HIPCHK(hipMemcpyAsync(ctx->tbl_descs.p, frames.data(), nf * sizeof(lcrc_desc_dev), hipMemcpyHostToDevice, st));
+      uint64_t total = 0;
+      rc = snappy_frames_impl(ctx, file, ctx->tbl_descs.p, nf, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
+                              ctx->sn_status.p, &total, st);
+      if (rc == LCRC_ERANGE) {
+        if ((rc = ctx->sn_out.ensure(total))) return rc;
+        rc = snappy_frames_impl(ctx, file, ctx->tbl_descs.p, nf, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
+                                ctx->sn_status.p, &total, st);
+      }
+      if (rc) return rc;
+      std::vector<uint8_t> fst(nf);
+      HIPCHK(hipMemcpy(fst.data(), ctx->sn_status.p, nf, hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < nf; ++k)
+        if (fst[k]) found[fwhich[k]].status = LCRC_TBLK_BAD_CONTENT;
     }
   }
   memcpy(blocks, found.data(), n * sizeof(lcrc_tblk));

@@ -622,5 +622,10 @@ def table_scan_expect(f, filter_name=None, mode=0, masked=False):
             continue
         c = trailer_crc(off, n)
         st = 0 if c == int.from_bytes(f[off + n + 1:off + n + 5], "little") else 1
+        # read_block_from_file's type dispatch after a good checksum (format.rs:175-210)
+        if st == 0 and f[off + n] == 1 and snappy_frame_decode(f[off:off + n]) is None:
+            st = 3  # "corrupted compressed block content"
+        elif st == 0 and f[off + n] > 1:
+            st = 4  # "bad block type"
         out.append((off, n, kind, f[off + n], st, c))
     return out, None
