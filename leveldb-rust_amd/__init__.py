@@ -435,6 +435,25 @@ class Engine:
         _check(rc, "lcrc_table_scan")
         return out
 
+    def table_scan_into(self, file_dev, file_len, out, filter_name=None):
+        """lcrc_table_scan into a preallocated TBLK_DTYPE array; returns the block count."""
+        n = ctypes.c_size_t(0)
+        err = ctypes.create_string_buffer(256)
+        fname = filter_name.encode() if isinstance(filter_name, str) else filter_name
+        rc = lib().lcrc_table_scan(self.ctx, _ptr(file_dev), int(file_len), fname, out.ctypes.data_as(ctypes.c_void_p),
+                                   len(out), ctypes.byref(n), err, 256)
+        if rc == ECORRUPT:
+            raise TableCorruption(err.value.decode())
+        _check(rc, "lcrc_table_scan")
+        return n.value
+
+    def snappy_frames_into(self, base, frames_dev, n, out, out_cap, out_off, status):
+        """lcrc_snappy_frames with caller-owned device buffers; returns the decoded size."""
+        total = ctypes.c_uint64(0)
+        _check(lib().lcrc_snappy_frames(self.ctx, _ptr(base), _ptr(frames_dev), int(n), _ptr(out), int(out_cap),
+                                        _ptr(out_off), _ptr(status), ctypes.byref(total)), "lcrc_snappy_frames")
+        return total.value
+
     def batch_seal(self, base, base_len, descs, n, out_crc=None, stream=None):
         """Compute each descriptor's CRC and store it at base[offset + expect_rel] (device, in place)."""
         _check(lib().lcrc_batch_seal(self.ctx, _ptr(base), int(base_len), _ptr(descs), int(n), _ptr(out_crc), stream),

@@ -5,9 +5,11 @@
 #include <hip/hip_runtime_api.h>
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -39,6 +41,12 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, hipStream_t st);
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
+hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
+                                 uint64_t* count, uint64_t* flag, const uint64_t* pos, lcrc_tblk_dev* out,
+                                 lcrc_desc_dev* descs, hipStream_t st);
+hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
+                                  const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st);
+hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
 hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
@@ -46,6 +54,7 @@ hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, cons
 
 static_assert(sizeof(lcrc_desc) == sizeof(lcrc_desc_dev), "desc layout");
 static_assert(sizeof(lcrc_wal_rec) == sizeof(lcrc_wal_rec_dev), "wal rec layout");
+static_assert(sizeof(lcrc_tblk) == sizeof(lcrc_tblk_dev), "table block layout");
 
 namespace {
 
@@ -117,6 +126,9 @@ struct lcrc_ctx {
   DevBuf<lcrc_desc_dev> sn_cdesc;
   DevBuf<uint32_t> sn_cexp, sn_cframe, sn_ccrc;
   DevBuf<uint64_t> sn_out_off;  // table scan: frame output offsets
+  DevBuf<lcrc_tblk_dev> tbl_blk;  // table scan on the device: the blocks being assembled
+  DevBuf<uint64_t> idx_count, idx_flag, idx_pos, idx_fpos;
+  DevBuf<lcrc_desc_dev> tbl_frames;
   DevBuf<uint8_t> sn_out, sn_status;
   DevBuf<lcrc_desc_dev> tbl_descs;  // table scan / seal
   DevBuf<uint32_t> tbl_crcs, tbl_mm;
@@ -245,6 +257,9 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   for (auto* b : {&ctx->sn_size, &ctx->sn_nch, &ctx->sn_choff, &ctx->sn_part, &ctx->sn_out_off}) b->release();
   for (auto* b : {&ctx->sn_cexp, &ctx->sn_cframe, &ctx->sn_ccrc}) b->release();
   ctx->sn_cdesc.release();
+  ctx->tbl_blk.release();
+  for (auto* b : {&ctx->idx_count, &ctx->idx_flag, &ctx->idx_pos, &ctx->idx_fpos}) b->release();
+  ctx->tbl_frames.release();
   ctx->sn_out.release();
   ctx->sn_status.release();
   ctx->tbl_descs.release();
@@ -513,6 +528,165 @@ int lcrc_snappy_frames(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc* fram
 }
 
 // ---- whole-table verify scan ----
+// Whole-table scan with the index block walked on the device (one thread per restart segment). Returns
+// TBL_FALLBACK when the index block is not one the segmented walk can vouch for; the host walk then
+// repeats it sequentially with the reference's messages.
+static constexpr int TBL_FALLBACK = 1000;
+
+static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
+                             const lcrc_tbl::Handle& meta_h, const lcrc_tbl::Handle& index_h, lcrc_tblk* blocks,
+                             size_t max_blocks, size_t* n_blocks, const std::function<int(const char*)>& corrupt) {
+  using namespace lcrc_tbl;
+  hipStream_t st = ctx->stream;
+  int rc;
+  if (index_h.offset > file_len || index_h.size + BLOCK_TRAILER_SIZE > file_len - index_h.offset ||
+      index_h.size + 1 > 0x7FFFFFFFull)
+    return TBL_FALLBACK;
+  // Table::open: read_block_from_file(index, verify_checksum = paranoid_checks) -- the checksum and the
+  // type byte on the device
+  lcrc_desc_dev idesc;
+  idesc.offset = index_h.offset;
+  idesc.length = (uint32_t)(index_h.size + 1);
+  idesc.expect_rel = (int32_t)(index_h.size + 1);
+  const uint64_t tpos = index_h.offset + index_h.size;
+  if ((rc = ctx->tbl_descs.ensure(1)) || (rc = ctx->tbl_crcs.ensure(1)) || (rc = ctx->tbl_mm.ensure(1)) ||
+      (rc = ctx->tbl_pos.ensure(1)) || (rc = ctx->tbl_types.ensure(1)))
+    return rc;
+  HIPCHK(hipMemcpyAsync(ctx->tbl_descs.p, &idesc, sizeof(idesc), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(ctx->tbl_pos.p, &tpos, sizeof(tpos), hipMemcpyHostToDevice, st));
+  if ((rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->tbl_descs.p, 1, ctx->tbl_crcs.p, ctx->tbl_mm.p, st)))
+    return rc;
+  HIPCHK(lcrc_launch_gather_u8(file, ctx->tbl_pos.p, 1, ctx->tbl_types.p, st));
+  uint32_t imm = 0;
+  uint8_t itype = 0;
+  HIPCHK(hipMemcpyAsync(&imm, ctx->tbl_mm.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&itype, ctx->tbl_types.p, 1, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (imm & 1) return corrupt("block checksum mismatch");
+  const uint8_t* contents = file + index_h.offset;
+  uint64_t clen = index_h.size;
+  if (itype == 1) {  // Snappy-framed index block, decoded on the device
+    if ((rc = ctx->sn_out_off.ensure(2)) || (rc = ctx->sn_status.ensure(1))) return rc;
+    idesc.length = (uint32_t)index_h.size;
+    idesc.expect_rel = LCRC_NO_EXPECT_DEV;
+    HIPCHK(hipMemcpyAsync(ctx->tbl_descs.p, &idesc, sizeof(idesc), hipMemcpyHostToDevice, st));
+    uint64_t total = 0;
+    rc = snappy_frames_impl(ctx, file, ctx->tbl_descs.p, 1, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
+                            ctx->sn_status.p, &total, st);
+    if (rc == LCRC_ERANGE) {
+      if ((rc = ctx->sn_out.ensure(total))) return rc;
+      rc = snappy_frames_impl(ctx, file, ctx->tbl_descs.p, 1, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
+                              ctx->sn_status.p, &total, st);
+    }
+    if (rc) return rc;
+    uint8_t fst = 0;
+    HIPCHK(hipMemcpy(&fst, ctx->sn_status.p, 1, hipMemcpyDeviceToHost));
+    if (fst) return corrupt("corrupted compressed block content");
+    contents = ctx->sn_out.p;
+    clen = total;
+  } else if (itype != 0) {
+    return corrupt("bad block type");
+  }
+  // Block::from_content (block.rs:21-41)
+  if (clen < 4) return corrupt("bad block contents, size smaller than u32");
+  if (clen > 0xFFFFFFFFull) return TBL_FALLBACK;
+  uint32_t nres = 0;
+  HIPCHK(hipMemcpy(&nres, contents + clen - 4, 4, hipMemcpyDeviceToHost));
+  if ((uint64_t)nres > (clen - 4) / 4) return corrupt("bad block contents");
+  // entries without restart points, or segments so long that one thread per segment would be slower than
+  // the host (the reference's index blocks restart at every entry, table.rs:272): the sequential walk
+  if (nres == 0 || (clen - 4) / nres > 4096) return TBL_FALLBACK;
+  const uint32_t len = (uint32_t)clen;
+  // entries per restart segment -> their positions
+  if ((rc = ctx->idx_count.ensure(nres)) || (rc = ctx->idx_flag.ensure(nres)) || (rc = ctx->idx_pos.ensure(nres + 1)) ||
+      (rc = ctx->idx_fpos.ensure(nres + 1)) || (rc = ctx->sn_part.ensure(2 * ((nres + 255) / 256))))
+    return rc;
+  HIPCHK(lcrc_launch_idx_parse(false, contents, len, nres, file_len, ctx->idx_count.p, ctx->idx_flag.p, nullptr, nullptr,
+                               nullptr, st));
+  HIPCHK(lcrc_launch_scan2(ctx->idx_count.p, ctx->idx_flag.p, nres, ctx->idx_pos.p, ctx->idx_fpos.p, ctx->sn_part.p,
+                           st));
+  uint64_t tot[2];
+  HIPCHK(hipMemcpyAsync(&tot[0], ctx->idx_pos.p + nres, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&tot[1], ctx->idx_fpos.p + nres, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (tot[1]) return TBL_FALLBACK;
+  const uint64_t nd = tot[0];
+  // read_meta: only with a filter policy, and its errors are not propagated (table.rs:81-103); the
+  // metaindex block is small and walked on the host
+  std::vector<lcrc_tblk> extra;
+  auto add = [&](const Handle& h, uint8_t kind) {
+    lcrc_tblk b;
+    memset(&b, 0, sizeof(b));
+    b.offset = h.offset;
+    b.size = h.size;
+    b.kind = kind;
+    extra.push_back(b);
+  };
+  if (filter_name && meta_h.offset <= file_len && meta_h.size + BLOCK_TRAILER_SIZE <= file_len - meta_h.offset) {
+    std::vector<uint8_t> raw(meta_h.size + BLOCK_TRAILER_SIZE), mc;
+    HIPCHK(hipMemcpy(raw.data(), file + meta_h.offset, raw.size(), hipMemcpyDeviceToHost));
+    if (!block_contents(raw.data(), meta_h.size, true, ctx->mode, ctx->flags, mc)) {
+      const std::string want = std::string("filter") + filter_name;
+      block_entries(mc, [&](const std::string& key, const uint8_t* v, uint32_t vn) {
+        if (key < want) return true;  // seek: first key >= want
+        Handle h;
+        const uint8_t* p = v;
+        if (key == want && !decode_handle(p, v + vn, h)) add(h, LCRC_TBLK_FILTER);
+        return false;
+      });
+    }
+  }
+  add(meta_h, LCRC_TBLK_METAINDEX);
+  add(index_h, LCRC_TBLK_INDEX);
+  const size_t n = nd + extra.size();
+  *n_blocks = n;
+  if (!blocks || max_blocks < n) return LCRC_ERANGE;
+  if ((rc = ctx->tbl_blk.ensure(n)) || (rc = ctx->tbl_descs.ensure(n)) || (rc = ctx->tbl_crcs.ensure(n)) ||
+      (rc = ctx->tbl_mm.ensure((n + 31) / 32)) || (rc = ctx->tbl_frames.ensure(n)) ||
+      (rc = ctx->sn_out_off.ensure(n + 1)) || (rc = ctx->sn_status.ensure(n)))
+    return rc;
+  HIPCHK(lcrc_launch_idx_parse(true, contents, len, nres, file_len, nullptr, nullptr, ctx->idx_pos.p, ctx->tbl_blk.p,
+                               ctx->tbl_descs.p, st));
+  std::vector<lcrc_desc_dev> xd(extra.size());
+  for (size_t k = 0; k < extra.size(); ++k) {
+    lcrc_tblk& b = extra[k];
+    const bool in = b.offset <= file_len && b.size + BLOCK_TRAILER_SIZE <= file_len - b.offset &&
+                    b.size + 1 <= 0x7FFFFFFFull;
+    xd[k].offset = in ? b.offset : 0;
+    xd[k].length = in ? (uint32_t)(b.size + 1) : 0;
+    xd[k].expect_rel = in ? (int32_t)(b.size + 1) : LCRC_NO_EXPECT_DEV;
+    if (!in) {
+      b.status = LCRC_TBLK_TRUNCATED;
+      b.type = 0xFF;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(ctx->tbl_blk.p + nd, extra.data(), extra.size() * sizeof(lcrc_tblk), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(ctx->tbl_descs.p + nd, xd.data(), xd.size() * sizeof(lcrc_desc_dev), hipMemcpyHostToDevice, st));
+  // ONE batched verify of every block, then read_block_from_file's type dispatch: Snappy frames decoded and
+  // checked on the device
+  if ((rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->tbl_descs.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, st)))
+    return rc;
+  HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, st));
+  uint64_t total = 0;
+  rc = snappy_frames_impl(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
+                          ctx->sn_status.p, &total, st);
+  if (rc == LCRC_ERANGE) {
+    if ((rc = ctx->sn_out.ensure(total))) return rc;
+    rc = snappy_frames_impl(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
+                            ctx->sn_status.p, &total, st);
+  }
+  if (rc) return rc;
+  HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, st));
+  HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  // sorted by offset (a well-formed table already is)
+  bool sorted = true;
+  for (size_t k = 1; k < n && sorted; ++k) sorted = blocks[k - 1].offset <= blocks[k].offset;
+  if (!sorted)
+    std::stable_sort(blocks, blocks + n, [](const lcrc_tblk& a, const lcrc_tblk& b) { return a.offset < b.offset; });
+  return LCRC_OK;
+}
+
 int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
                     lcrc_tblk* blocks, size_t max_blocks, size_t* n_blocks, char* err, size_t err_cap) {
   using namespace lcrc_tbl;
@@ -542,6 +716,11 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
   HIPCHK(hipMemcpy(footer, file + file_len - FOOTER_ENCODED_LENGTH, FOOTER_ENCODED_LENGTH, hipMemcpyDeviceToHost));
   Handle meta_h, index_h;
   if (const char* e = decode_footer(footer, meta_h, index_h)) return corrupt(e);
+  rc = table_scan_device(ctx, file, file_len, filter_name, meta_h, index_h, blocks, max_blocks, n_blocks,
+                         [&](const char* m) { return corrupt(m); });
+  if (rc != TBL_FALLBACK) return rc;
+  *n_blocks = 0;
+  // the host walk (an index block the segmented device walk cannot vouch for: the reference's messages)
 
   std::vector<lcrc_tblk> found;
   auto add = [&](const Handle& h, uint8_t kind) {

@@ -28,6 +28,13 @@ struct lcrc_desc_dev {  // == lcrc_desc
 };
 #define LCRC_NO_EXPECT_DEV ((int32_t)0x80000000)
 
+struct lcrc_tblk_dev {  // == lcrc_tblk
+  uint64_t offset;
+  uint64_t size;
+  uint32_t crc;
+  uint8_t kind, type, status, reserved;
+};
+
 struct lcrc_wal_rec_dev {  // == lcrc_wal_rec
   uint64_t header;
   uint32_t length;

@@ -1196,6 +1196,137 @@ __global__ void __launch_bounds__(256) k_snappy_check(const uint32_t* __restrict
 }
 
 // ---------------------------------------------------------------------------------------------------
+// SSTable index block on the device (lcrc_table_scan): one thread per restart segment walks its entries
+// (src/sstable/block.rs: entry = varint32 shared, non_shared, value_len, key delta, value; the value is a
+// BlockHandle = varint64 offset, size, src/sstable/format.rs:24-61). Anything the segmented walk cannot
+// vouch for -- a restart entry with shared != 0, an entry crossing the next restart, a malformed varint
+// or handle -- sets the segment's fallback flag and the host repeats the walk sequentially (for the
+// reference's exact error message).
+// ---------------------------------------------------------------------------------------------------
+// varint32 (BITS 32: shifts 0..28) / varint64 (BITS 64: shifts 0..63), as the host's get_varint32/64.
+// Returns the position after it, or ~0u when it is malformed or runs past lim.
+template <int BITS>
+__device__ __forceinline__ uint32_t dev_varint(const uint8_t* __restrict__ d, uint32_t p, uint32_t lim,
+                                               uint64_t* __restrict__ out) {
+  uint64_t result = 0;
+  for (int shift = 0; shift <= (BITS == 32 ? 28 : 63); shift += 7) {
+    if (p >= lim) return ~0u;
+    const uint64_t b = d[p];
+    p += 1;
+    result |= (b & 127) << shift;
+    if (!(b & 128)) {
+      *out = BITS == 32 ? (uint64_t)(uint32_t)result : result;  // the host decoder keeps 32 bits
+      return p;
+    }
+  }
+  return ~0u;
+}
+
+// PASS 1: count[i] = entries of segment i, flag[i] = 1 if the host must walk. PASS 2: writes the handles
+// (tblk offset/size, kind DATA) at pos[i] .. and their verify descriptors; a handle past the end of the file
+// gets an empty descriptor and status TRUNCATED.
+template <bool PASS2>
+__global__ void __launch_bounds__(256) k_idx_parse(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
+                                                   uint64_t file_len, uint64_t* __restrict__ count,
+                                                   uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos,
+                                                   lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nres) return;
+  const uint32_t restarts = len - (1 + nres) * 4;
+  auto rst = [&](uint32_t k) { return load_le32(d + restarts + 4 * k); };
+  const uint32_t start = rst((uint32_t)i);
+  const uint32_t end = i + 1 < nres ? rst((uint32_t)i + 1) : restarts;
+  bool bad = (i == 0 && start != 0) || start > end || end > restarts;
+  uint64_t n = 0;
+  uint32_t off = start;
+  for (uint32_t guard = 0; !bad && off < end; ++guard) {
+    if (guard > len || restarts - off < 3) {  // an entry takes >= 3 bytes: at most len of them
+      bad = true;
+      break;
+    }
+    uint64_t shared = 0, non_shared = 0, vlen = 0;
+    uint32_t p = dev_varint<32>(d, off, restarts, &shared);
+    if (p != ~0u) p = dev_varint<32>(d, p, restarts, &non_shared);
+    if (p != ~0u) p = dev_varint<32>(d, p, restarts, &vlen);
+    if (p == ~0u || (uint64_t)restarts - p < non_shared + vlen || (off == start && shared != 0) ||
+        p + non_shared + vlen > end) {
+      bad = true;
+      break;
+    }
+    const uint32_t qe = (uint32_t)(p + non_shared + vlen);
+    uint64_t hoff = 0, hsize = 0;
+    uint32_t q = dev_varint<64>(d, (uint32_t)(p + non_shared), qe, &hoff);
+    if (q != ~0u) q = dev_varint<64>(d, q, qe, &hsize);
+    if (q == ~0u) {
+      bad = true;
+      break;
+    }
+    if (PASS2) {
+      const uint64_t o = pos[i] + n;
+      lcrc_tblk_dev b;
+      b.offset = hoff;
+      b.size = hsize;
+      b.crc = 0;
+      b.kind = 0;
+      b.type = 0;
+      b.status = 0;
+      b.reserved = 0;
+      lcrc_desc_dev dd;
+      const bool in = hoff <= file_len && hsize + 5 <= file_len - hoff && hsize + 1 <= 0x7FFFFFFFull;
+      dd.offset = in ? hoff : 0;
+      dd.length = in ? (uint32_t)(hsize + 1) : 0;
+      dd.expect_rel = in ? (int32_t)(hsize + 1) : LCRC_NO_EXPECT_DEV;
+      if (!in) {
+        b.status = 2;  // LCRC_TBLK_TRUNCATED
+        b.type = 0xFF;
+      }
+      out[o] = b;
+      descs[o] = dd;
+    }
+    ++n;
+    off = (uint32_t)(p + non_shared + vlen);
+  }
+  if (!PASS2) {
+    count[i] = bad ? 0 : n;
+    flag[i] = bad ? 1 : 0;
+  }
+}
+
+// per block: computed crc, stored type, status (mismatch / bad type), and the Snappy frame to check when
+// the checksum holds and the type is 1 (length 0 otherwise)
+__global__ void __launch_bounds__(256) k_tbl_finish(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
+                                                    const uint32_t* __restrict__ crc,
+                                                    const uint32_t* __restrict__ mismatch,
+                                                    const uint8_t* __restrict__ file,
+                                                    lcrc_desc_dev* __restrict__ frames) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  lcrc_tblk_dev b = blk[i];
+  lcrc_desc_dev f;
+  f.offset = 0;
+  f.length = 0;
+  f.expect_rel = LCRC_NO_EXPECT_DEV;
+  if (b.status != 2) {
+    b.crc = crc[i];
+    b.type = file[b.offset + b.size];
+    b.status = (mismatch[i >> 5] >> (i & 31)) & 1;
+    if (b.status == 0 && b.type > 1) b.status = 4;  // LCRC_TBLK_BAD_TYPE
+    if (b.status == 0 && b.type == 1) {
+      f.offset = b.offset;
+      f.length = (uint32_t)b.size;
+    }
+  }
+  blk[i] = b;
+  frames[i] = f;
+}
+
+__global__ void __launch_bounds__(256) k_tbl_content(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
+                                                     const uint8_t* __restrict__ fstatus) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && fstatus[i]) blk[i].status = 3;  // LCRC_TBLK_BAD_CONTENT
+}
+
+// ---------------------------------------------------------------------------------------------------
 // small helpers of the table scan and the writer-side seal
 // ---------------------------------------------------------------------------------------------------
 // out[i] = base[pos[i]] (the type bytes of a table's blocks)
@@ -1343,6 +1474,34 @@ hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, c
   if (nch_bound == 0) return hipSuccess;
   hipLaunchKernelGGL(lcrc_dev::k_snappy_check, dim3((unsigned)((nch_bound + 255) / 256)), dim3(256), 0, st, crc, cexp,
                      cframe, nch, status);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
+                                 uint64_t* count, uint64_t* flag, const uint64_t* pos, lcrc_tblk_dev* out,
+                                 lcrc_desc_dev* descs, hipStream_t st) {
+  if (nres == 0) return hipSuccess;
+  const dim3 g((nres + 255) / 256);
+  if (pass2)
+    hipLaunchKernelGGL(lcrc_dev::k_idx_parse<true>, g, dim3(256), 0, st, d, len, nres, file_len, count, flag, pos, out,
+                       descs);
+  else
+    hipLaunchKernelGGL(lcrc_dev::k_idx_parse<false>, g, dim3(256), 0, st, d, len, nres, file_len, count, flag, pos, out,
+                       descs);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
+                                  const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_tbl_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, crc, mismatch,
+                     file, frames);
+  return hipGetLastError();
+}
+
+hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_tbl_content, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, fstatus);
   return hipGetLastError();
 }
 

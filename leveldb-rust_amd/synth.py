@@ -90,3 +90,63 @@ def wal_lengths(total_bytes, seed=SEED_WAL):
         out.append(n)
         tot += n + 7
     return out
+
+
+SEED_TABLE, SEED_SNAPPY = 0x5EED0004, 0x5EED0005
+TABLE_MAGIC = 0xdb4775248b80fb57  # src/sstable/format.rs:20
+
+
+def _varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def table_layout(nblk, blen, seed=SEED_TABLE):
+    """A synthetic SSTable for the whole-table scan bench: nblk raw data blocks of blen random bytes, each
+    followed by its 5-byte trailer slot [type 0][crc: zero, to be sealed], then an (empty) metaindex block and
+    an index block with one entry per data block (shared = 0, one restart), trailer slots likewise, and the
+    48-byte footer. The index block restarts at every entry, as the reference's (table.rs:272). Returns (file bytes as numpy u8, [(offset, size)] of every block needing a trailer)."""
+    import numpy as np
+    stride = blen + 5
+    data = np.zeros(nblk * stride, np.uint8)
+    body = splitmix_bytes(seed, nblk * blen).reshape(nblk, blen)
+    data.reshape(nblk, stride)[:, :blen] = body
+    blocks = [(i * stride, blen) for i in range(nblk)]
+    meta = (0).to_bytes(4, "little") + (1).to_bytes(4, "little")  # restart [0], one restart
+    idx = bytearray()
+    restarts = []
+    for i in range(nblk):  # restart interval 1, as the reference's index blocks (table.rs:272)
+        key = i.to_bytes(8, "big")
+        val = _varint(i * stride) + _varint(blen)
+        restarts.append(len(idx))
+        idx += b"\x00" + _varint(len(key)) + _varint(len(val)) + key + val
+    idx += np.asarray(restarts, "<u4").tobytes() + len(restarts).to_bytes(4, "little")
+    moff = len(data)
+    tail = bytearray(meta) + bytes(5)
+    ioff = moff + len(tail)
+    tail += idx + bytes(5)
+    foot = _varint(moff) + _varint(len(meta)) + _varint(ioff) + _varint(len(idx))
+    foot += bytes(40 - len(foot)) + TABLE_MAGIC.to_bytes(8, "little")
+    tail += foot
+    blocks += [(moff, len(meta)), (ioff, len(idx))]
+    return np.concatenate([data, np.frombuffer(bytes(tail), np.uint8)]), blocks
+
+
+def snappy_frame_synthetic(seed=SEED_SNAPPY, unit=64, reps=64):
+    """One Snappy frame (stream identifier + one compressed data chunk) of `unit` random bytes repeated
+    `reps` times, Snappy-encoded as one literal and reps - 1 two-byte-offset copies; the chunk CRC slot is
+    zero (to be filled with the masked CRC-32C of the uncompressed bytes). Returns (frame bytes, raw bytes,
+    offset of the CRC slot)."""
+    lit = bytes(splitmix_bytes(seed, unit))
+    raw = lit * reps
+    z = bytearray(_varint(len(raw)))
+    z += bytes([60 << 2, unit - 1]) + lit if unit > 60 else bytes([(unit - 1) << 2]) + lit
+    for _ in range(reps - 1):
+        z += bytes([((unit - 1) << 2) | 2, unit & 0xFF, unit >> 8])
+    body = bytes(4) + bytes(z)
+    frame = b"\xff\x06\x00\x00sNaPpY" + bytes([0]) + len(body).to_bytes(3, "little") + body
+    return frame, raw, 14

@@ -386,7 +386,7 @@ def snappy_frame_encode(data):
 
 
 def table_build(kvs, block_size=4096, restart_interval=16, compression=0, filter_name=None, filter_block=b"",
-                mode=0, masked=False):
+                mode=0, masked=False, index_restart_interval=1):
     """TableBuilder over sorted kvs -> (file bytes, [(offset, size, kind)]); kind 0 data, 1 filter,
     2 metaindex, 3 index. Trailer CRCs in `mode` (0 = crc32fast, the reference), optionally masked."""
     f = bytearray()
@@ -430,7 +430,8 @@ def table_build(kvs, block_size=4096, restart_interval=16, compression=0, filter
     mh = write_block(block_build(meta, restart_interval), 2)
     if pending is not None:
         index.append((short_successor(last_key), varint(pending[0]) + varint(pending[1])))
-    ih = write_block(block_build(index, restart_interval), 3)
+    # the reference's index block restarts at every entry (table.rs:272); other intervals for tests
+    ih = write_block(block_build(index, index_restart_interval), 3)
     foot = bytearray(varint(mh[0]) + varint(mh[1]) + varint(ih[0]) + varint(ih[1]))
     foot += bytes(40 - len(foot)) + _le32(TABLE_MAGIC & 0xFFFFFFFF) + _le32(TABLE_MAGIC >> 32)
     f += foot

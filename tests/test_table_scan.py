@@ -366,3 +366,15 @@ def test_table_scan_compressed_content(lcrc, orc, engines):
     assert err is None and werr is None and _as_tuples(got) == want
     st = {int(b["offset"]): int(b["status"]) for b in got}
     assert [st[b[0]] for b in comp[:3]] == [3, 3, 4]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("interval", [1, 16, 1000])
+def test_table_scan_index_restart_intervals(lcrc, orc, engines, interval):
+    """Index blocks with several entries per restart segment (walked per segment on the device) and one
+    with a single huge segment (the host walk)."""
+    f, _ = orc.table_build(_kvs(6000, 41), block_size=512, compression=1, index_restart_interval=interval)
+    got, err = _scan(lcrc, engines[lcrc.MODE_REF], f)
+    want, werr = orc.table_scan_expect(f)
+    assert err is None and werr is None and _as_tuples(got) == want
+    assert (got["status"] == 0).all()
