@@ -1182,6 +1182,202 @@ __global__ void __launch_bounds__(256) k_snappy_decode(const uint8_t* __restrict
   }
 }
 
+// pass 2, wave per frame: the compressed chunk is staged in LDS and decoded there, each Snappy element
+// copied by the 64 lanes at once (a copy whose offset is shorter than its length repeats the last `off`
+// bytes: lane k takes byte (k mod off) of them); the decoded chunk is then written out with 16 B per lane.
+// Chunks larger than the LDS staging (SN_CAP) take the lane-serial path of k_snappy_decode.
+constexpr uint32_t SN_CAP = 8192;
+
+__device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// decode Snappy raw data in[0, n) (LDS) into o[0, ulen) (LDS); false when malformed
+__device__ bool snappy_wave_decode(const uint8_t* in, uint32_t n, uint8_t* o, uint32_t ulen, uint32_t lane) {
+  uint32_t q = 0;
+  // length preamble (already validated by pass 1): skip it
+  for (uint32_t i = 0; i < 5 && q < n; ++i) {
+    const uint32_t b = in[q++];
+    if (!(b & 128)) break;
+  }
+  uint32_t w = 0;  // bytes written
+  while (q < n) {
+    const uint32_t tag = bcast(in[q]);
+    ++q;
+    uint32_t ln, off = 0;
+    if ((tag & 3) == 0) {  // literal
+      ln = tag >> 2;
+      if (ln >= 60) {
+        const uint32_t nb = ln - 59;
+        if (n - q < nb) return false;
+        ln = 0;
+        for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)in[q + k] << (8 * k);
+        ln = bcast(ln);
+        q += nb;
+      }
+      ln += 1;
+      if (n - q < ln || ulen - w < ln) return false;
+      for (uint32_t k = lane; k < ln; k += 64) o[w + k] = in[q + k];
+      w += ln;
+      q += ln;
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (q >= n) return false;
+      ln = 4 + ((tag >> 2) & 7);
+      off = ((tag >> 5) << 8) | in[q];
+      q += 1;
+    } else if ((tag & 3) == 2) {
+      if (n - q < 2) return false;
+      ln = 1 + (tag >> 2);
+      off = in[q] | ((uint32_t)in[q + 1] << 8);
+      q += 2;
+    } else {
+      if (n - q < 4) return false;
+      ln = 1 + (tag >> 2);
+      off = in[q] | ((uint32_t)in[q + 1] << 8) | ((uint32_t)in[q + 2] << 16) | ((uint32_t)in[q + 3] << 24);
+      q += 4;
+    }
+    off = bcast(off);
+    if (off == 0 || off > w || ulen - w < ln) return false;
+    // ln <= 64: one pass; the source byte of lane k is w - off + (k mod off), always already written
+    if (lane < ln) {
+      const uint32_t src = w - off + (off >= ln ? lane : lane % off);
+      const uint8_t v = o[src];
+      __builtin_amdgcn_wave_barrier();
+      o[w + lane] = v;
+    } else {
+      __builtin_amdgcn_wave_barrier();
+    }
+    w += ln;
+  }
+  return w == ulen;
+}
+
+__global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __restrict__ base,
+                                                           const lcrc_desc_dev* __restrict__ frames, uint64_t n,
+                                                           const uint64_t* __restrict__ out_off,
+                                                           const uint64_t* __restrict__ chunk_off,
+                                                           uint8_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                           lcrc_desc_dev* __restrict__ cdesc,
+                                                           uint32_t* __restrict__ cexp, uint32_t* __restrict__ cframe) {
+  __shared__ __attribute__((aligned(16))) uint8_t lin[SN_CAP];
+  __shared__ __attribute__((aligned(16))) uint8_t lout[SN_CAP];
+  const uint32_t lane = __lane_id();
+  for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
+    if (status[f]) continue;
+    const uint8_t* p = base + frames[f].offset;
+    const uint32_t len = frames[f].length;
+    uint64_t o = out_off[f];
+    uint64_t c = chunk_off[f];
+    bool ok = true;
+    uint32_t at = 0;
+    while (ok && at < len) {
+      const uint32_t type = bcast(p[at]);
+      const uint32_t cl = bcast(p[at + 1] | ((uint32_t)p[at + 2] << 8) | ((uint32_t)p[at + 3] << 16));
+      at += 4;
+      const uint8_t* body = p + at;
+      at += cl;
+      if (type > 1) continue;  // stream identifiers and skippable chunks (validated by pass 1)
+      const uint32_t want = bcast(body[0] | ((uint32_t)body[1] << 8) | ((uint32_t)body[2] << 16) |
+                                  ((uint32_t)body[3] << 24));
+      const uint64_t start = o;
+      if (type == 1) {
+        for (uint32_t k = 4 + lane; k < cl; k += 64) out[o + k - 4] = body[k];
+        o += cl - 4;
+      } else {
+        // preamble = uncompressed length (validated by pass 1)
+        uint32_t ulen = 0;
+        for (uint32_t i = 0, sh = 0; i < 5 && 4 + i < cl; ++i, sh += 7) {
+          const uint32_t b = body[4 + i];
+          ulen |= (b & 127u) << sh;
+          if (!(b & 128)) break;
+        }
+        ulen = bcast(ulen);
+        const uint32_t zn = cl - 4;
+        if (zn <= SN_CAP && ulen <= SN_CAP) {
+          for (uint32_t k = lane; k < zn; k += 64) lin[k] = body[4 + k];
+          __builtin_amdgcn_s_waitcnt(0);
+          __builtin_amdgcn_wave_barrier();
+          ok = snappy_wave_decode(lin, zn, lout, ulen, lane);
+          __builtin_amdgcn_wave_barrier();
+          if (ok) {
+            for (uint32_t k = lane; k < ulen; k += 64) out[o + k] = lout[k];
+            o += ulen;
+          }
+        } else if (lane == 0) {  // too large for the staging: lane-serial, from and to global memory
+          const uint8_t* q = body + 4;
+          const uint8_t* qe = body + cl;
+          for (uint32_t i = 0; i < 5; ++i)
+            if (!(*q++ & 128)) break;
+          const uint64_t lim = start + ulen;
+          while (ok && q < qe) {
+            const uint32_t tag = *q++;
+            uint32_t ln, off;
+            if ((tag & 3) == 0) {
+              ln = tag >> 2;
+              if (ln >= 60) {
+                const uint32_t nb = ln - 59;
+                if ((uint64_t)(qe - q) < nb) { ok = false; break; }
+                ln = 0;
+                for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)q[k] << (8 * k);
+                q += nb;
+              }
+              ln += 1;
+              if ((uint64_t)(qe - q) < ln || o + ln > lim) { ok = false; break; }
+              for (uint32_t k = 0; k < ln; ++k) out[o + k] = q[k];
+              o += ln;
+              q += ln;
+              continue;
+            }
+            if ((tag & 3) == 1) {
+              if (q >= qe) { ok = false; break; }
+              ln = 4 + ((tag >> 2) & 7);
+              off = ((tag >> 5) << 8) | *q++;
+            } else if ((tag & 3) == 2) {
+              if (qe - q < 2) { ok = false; break; }
+              ln = 1 + (tag >> 2);
+              off = q[0] | ((uint32_t)q[1] << 8);
+              q += 2;
+            } else {
+              if (qe - q < 4) { ok = false; break; }
+              ln = 1 + (tag >> 2);
+              off = q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+              q += 4;
+            }
+            if (off == 0 || off > o - start || o + ln > lim) { ok = false; break; }
+            for (uint32_t k = 0; k < ln; ++k, ++o) out[o] = out[o - off];
+          }
+          if (ok && o != lim) ok = false;
+        }
+        ok = bcast(ok ? 1u : 0u) != 0;
+        o = ((uint64_t)bcast((uint32_t)(o >> 32)) << 32) | bcast((uint32_t)o);
+      }
+      if (!ok) break;
+      if (lane == 0) {
+        lcrc_desc_dev d;
+        d.offset = start;
+        d.length = (uint32_t)(o - start);
+        d.expect_rel = LCRC_NO_EXPECT_DEV;
+        cdesc[c] = d;
+        cexp[c] = want;
+        cframe[c] = (uint32_t)f;
+      }
+      ++c;
+    }
+    if (!ok && lane == 0) {
+      status[f] = 1;
+      for (const uint64_t ce = chunk_off[f + 1]; c < ce; ++c) {
+        lcrc_desc_dev d;
+        d.offset = 0;
+        d.length = 0;
+        d.expect_rel = LCRC_NO_EXPECT_DEV;
+        cdesc[c] = d;
+        cexp[c] = 0;
+        cframe[c] = (uint32_t)f;
+      }
+    }
+  }
+}
+
 // a chunk whose masked CRC-32C differs from the stored one marks its frame corrupt (frames already
 // marked corrupt by the decode are skipped: their empty placeholder chunks carry no CRC)
 __global__ void __launch_bounds__(256) k_snappy_check(const uint32_t* __restrict__ crc,
@@ -1464,8 +1660,9 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_snappy_decode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, frames, n,
-                     out_off, chunk_off, out, status, cdesc, cexp, cframe);
+  const uint64_t g = n < 8192 ? n : 8192;  // one wave per frame, grid-stride
+  hipLaunchKernelGGL(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), 0, st, base, frames, n, out_off,
+                     chunk_off, out, status, cdesc, cexp, cframe);
   return hipGetLastError();
 }
 
