@@ -221,6 +221,14 @@ int lcrc_device_sync(void);
 int lcrc_timer_start(lcrc_ctx* ctx);
 int lcrc_timer_stop(lcrc_ctx* ctx, float* ms);
 
+/* HIP graphs of the context's own stream: lcrc_graph_begin starts capturing the calls made on the context
+ * with stream NULL (they must allocate nothing: reserve first), lcrc_graph_end instantiates them as one
+ * replayable graph; lcrc_graph_launch replays it on the context stream. */
+int lcrc_graph_begin(lcrc_ctx* ctx);
+int lcrc_graph_end(lcrc_ctx* ctx, void** graph_exec);
+int lcrc_graph_launch(lcrc_ctx* ctx, void* graph_exec);
+int lcrc_graph_destroy(void* graph_exec);
+
 /* Last HIP error string for this thread ("" if none). */
 const char* lcrc_last_error(void);
 /* Library build identification (kernel arch, version). */

@@ -85,6 +85,7 @@ ABI_SYMBOLS = [
     "lcrc_table_scan", "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
+    "lcrc_graph_begin", "lcrc_graph_end", "lcrc_graph_launch", "lcrc_graph_destroy",
     "lcrc_last_error", "lcrc_version",
 ]
 
@@ -141,6 +142,10 @@ def lib():
     sig("lcrc_device_sync", i32)
     sig("lcrc_timer_start", i32, vp)
     sig("lcrc_timer_stop", i32, vp, ctypes.POINTER(ctypes.c_float))
+    sig("lcrc_graph_begin", i32, vp)
+    sig("lcrc_graph_end", i32, vp, ctypes.POINTER(vp))
+    sig("lcrc_graph_launch", i32, vp, vp)
+    sig("lcrc_graph_destroy", i32, vp)
     sig("lcrc_last_error", cp)
     sig("lcrc_version", cp)
     # C++ restatement of the reference call sites (lcrc_leveldb.cpp)
@@ -482,6 +487,24 @@ class Engine:
         for b in (off, st) + ((out,) if own else ()):
             b.close()
         return frames_out, status
+
+    def graph_capture(self, fn):
+        """Capture the context-stream calls made by fn() into a replayable HIP graph (returns a handle)."""
+        _check(lib().lcrc_graph_begin(self.ctx), "lcrc_graph_begin")
+        try:
+            fn()
+        finally:
+            ge = ctypes.c_void_p()
+            rc = lib().lcrc_graph_end(self.ctx, ctypes.byref(ge))
+        _check(rc, "lcrc_graph_end")
+        return ge.value
+
+    def graph_launch(self, graph):
+        _check(lib().lcrc_graph_launch(self.ctx, graph), "lcrc_graph_launch")
+
+    @staticmethod
+    def graph_destroy(graph):
+        lib().lcrc_graph_destroy(graph)
 
     def timer_start(self):
         _check(lib().lcrc_timer_start(self.ctx), "lcrc_timer_start")

@@ -901,6 +901,35 @@ int lcrc_device_sync(void) {
   HIPCHK(hipDeviceSynchronize());
   return LCRC_OK;
 }
+int lcrc_graph_begin(lcrc_ctx* ctx) {
+  if (!ctx) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+  return LCRC_OK;
+}
+int lcrc_graph_end(lcrc_ctx* ctx, void** graph_exec) {
+  if (!ctx || !graph_exec) return LCRC_EINVAL;
+  *graph_exec = nullptr;
+  hipGraph_t g = nullptr;
+  HIPCHK(hipStreamEndCapture(ctx->stream, &g));
+  hipGraphExec_t ge = nullptr;
+  hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) return fail_hip(e, "hipGraphInstantiate");
+  *graph_exec = (void*)ge;
+  return LCRC_OK;
+}
+int lcrc_graph_launch(lcrc_ctx* ctx, void* graph_exec) {
+  if (!ctx || !graph_exec) return LCRC_EINVAL;
+  HIPCHK(hipGraphLaunch((hipGraphExec_t)graph_exec, ctx->stream));
+  return LCRC_OK;
+}
+int lcrc_graph_destroy(void* graph_exec) {
+  if (graph_exec) HIPCHK(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
+  return LCRC_OK;
+}
+
 int lcrc_timer_start(lcrc_ctx* ctx) {
   if (!ctx) return LCRC_EINVAL;
   HIPCHK(hipEventRecord(ctx->t0, ctx->stream));

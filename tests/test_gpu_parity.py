@@ -269,3 +269,31 @@ def test_wal_scan_async_matches_sync(lcrc, orc, engines):
     # an empty log
     empty = lcrc.DeviceBuffer(16)
     assert len(engines[1].wal_scan(empty, 0)) == 0
+
+
+def test_graph_replay_matches_direct(lcrc, orc):
+    """lcrc_graph_begin/end/launch: two reserved uniform batches captured once, replayed twice; the replay
+    rewrites the outputs with the same CRCs as the direct calls."""
+    eng = lcrc.Engine(0, lcrc.MODE_C)
+    n = 3000
+    data = [orc.splitmix_bytes(0x6A0 + k, n * 4096) for k in range(2)]
+    bufs = [lcrc.DeviceBuffer.from_host(d) for d in data]
+    outs = [lcrc.DeviceBuffer(4 * n) for _ in range(2)]
+    want = [orc.crc_ranges(d, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096), 1) for d in data]
+    for k in range(2):  # direct calls first (the fast path allocates nothing)
+        eng.batch_uniform(bufs[k], n, 4096, 4096, outs[k])
+    eng.sync()
+    for k in range(2):
+        assert np.array_equal(outs[k].download(np.uint32, n), want[k])
+    g = eng.graph_capture(lambda: [eng.batch_uniform(bufs[k], n, 4096, 4096, outs[k]) for k in range(2)])
+    try:
+        for _ in range(2):
+            for o in outs:
+                o.zero()
+            eng.graph_launch(g)
+            eng.sync()
+            for k in range(2):
+                assert np.array_equal(outs[k].download(np.uint32, n), want[k])
+    finally:
+        eng.graph_destroy(g)
+    eng.close()
