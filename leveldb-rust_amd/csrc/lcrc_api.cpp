@@ -33,12 +33,13 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
-                                   uint64_t* nchunks, uint8_t* status, hipStream_t st);
+                                   uint64_t* nchunks, uint8_t* status, uint32_t* maxes, hipStream_t st);
 hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
                              uint64_t* part, hipStream_t st);
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
-                                     lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, hipStream_t st);
+                                     lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
+                                     uint32_t max_out, hipStream_t st);
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
 hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
@@ -123,6 +124,7 @@ struct lcrc_ctx {
   // Snappy frames: chunk CRCs are CRC-32C whatever the context's mode
   uint32_t* d_tab_c = nullptr;  // CRC-32C image when mode != C (created on first use)
   DevBuf<uint64_t> sn_size, sn_nch, sn_choff, sn_part;
+  DevBuf<uint32_t> sn_max;  // largest compressed / decoded chunk of a batch (sizes the decode's LDS)
   DevBuf<lcrc_desc_dev> sn_cdesc;
   DevBuf<uint32_t> sn_cexp, sn_cframe, sn_ccrc;
   DevBuf<uint64_t> sn_out_off;  // table scan: frame output offsets
@@ -255,6 +257,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   if (ctx->d_tab_c) (void)hipFree(ctx->d_tab_c);
   for (auto* b : {&ctx->sn_size, &ctx->sn_nch, &ctx->sn_choff, &ctx->sn_part, &ctx->sn_out_off}) b->release();
+  ctx->sn_max.release();
   for (auto* b : {&ctx->sn_cexp, &ctx->sn_cframe, &ctx->sn_ccrc}) b->release();
   ctx->sn_cdesc.release();
   ctx->tbl_blk.release();
@@ -488,13 +491,16 @@ static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_des
   if (n == 0) return LCRC_OK;
   const size_t nparts = (n + 255) / 256;
   if ((rc = ctx->sn_size.ensure(n)) || (rc = ctx->sn_nch.ensure(n)) || (rc = ctx->sn_choff.ensure(n + 1)) ||
-      (rc = ctx->sn_part.ensure(2 * nparts)))
+      (rc = ctx->sn_part.ensure(2 * nparts)) || (rc = ctx->sn_max.ensure(2)))
     return rc;
-  HIPCHK(lcrc_launch_snappy_size(base, frames, n, ctx->sn_size.p, ctx->sn_nch.p, status, st));
+  HIPCHK(hipMemsetAsync(ctx->sn_max.p, 0, 8, st));
+  HIPCHK(lcrc_launch_snappy_size(base, frames, n, ctx->sn_size.p, ctx->sn_nch.p, status, ctx->sn_max.p, st));
   HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, n, out_off, ctx->sn_choff.p, ctx->sn_part.p, st));
   uint64_t tot[2];
   HIPCHK(hipMemcpyAsync(&tot[0], out_off + n, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], ctx->sn_choff.p + n, 8, hipMemcpyDeviceToHost, st));
+  uint32_t mx[2];
+  HIPCHK(hipMemcpyAsync(mx, ctx->sn_max.p, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   *total_out = tot[0];
   if (tot[0] > out_cap || (tot[0] && !out)) return LCRC_ERANGE;
@@ -506,7 +512,7 @@ static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_des
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
-                                   ctx->sn_cexp.p, ctx->sn_cframe.p, st));
+                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], st));
   // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
   HIPCHK(lcrc_launch_windows(false, ctx->grid_a, out, tot[0], tab_c, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
   HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, out, tot[0], ctx->sn_cdesc.p, nch, 0, 0, nullptr, ctx->win.p, tab_c,

@@ -943,12 +943,13 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
 __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__ base,
                                                      const lcrc_desc_dev* __restrict__ frames, uint64_t n,
                                                      uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
-                                                     uint8_t* __restrict__ status) {
+                                                     uint8_t* __restrict__ status, uint32_t* __restrict__ maxes) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n) return;
   const uint8_t* p = base + frames[f].offset;
   const uint32_t len = frames[f].length;
   uint64_t total = 0, chunks = 0;
+  uint32_t max_in = 0, max_out = 0;  // largest compressed data (after the crc) / decoded chunk
   bool ok = true, seen_id = false;
   uint32_t at = 0;
   while (ok && at < len) {
@@ -974,6 +975,8 @@ __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__
       if (cl < 4) ok = false;
       else if (type == 0) ok = snappy_ulen(p + at + 4, cl - 4, ulen, used);
       if (ulen > 65536) ok = false;
+      if (type == 0 && cl - 4 > max_in) max_in = cl - 4;
+      if (ulen > max_out) max_out = ulen;
       total += ulen;
       ++chunks;
     } else if (type <= 0x7f) {
@@ -984,6 +987,8 @@ __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__
   size[f] = ok ? total : 0;
   nchunks[f] = ok ? chunks : 0;
   status[f] = ok ? 0 : 1;
+  if (ok && max_in) atomicMax(&maxes[0], max_in);
+  if (ok && max_out) atomicMax(&maxes[1], max_out);
 }
 
 // exclusive scans of two u64 arrays (n entries): per-workgroup part, then every element adds the totals
@@ -1065,191 +1070,158 @@ __global__ void __launch_bounds__(256) k_scan2_add(uint64_t n, uint64_t* __restr
   }
 }
 
-// pass 2: decode frame f into out[out_off[f] ..) and describe its data chunks for the CRC pass:
-// cdesc (offset into out, length), cexp (stored masked CRC-32C), cframe (frame index)
-__global__ void __launch_bounds__(256) k_snappy_decode(const uint8_t* __restrict__ base,
-                                                       const lcrc_desc_dev* __restrict__ frames, uint64_t n,
-                                                       const uint64_t* __restrict__ out_off,
-                                                       const uint64_t* __restrict__ chunk_off,
-                                                       uint8_t* __restrict__ out, uint8_t* __restrict__ status,
-                                                       lcrc_desc_dev* __restrict__ cdesc, uint32_t* __restrict__ cexp,
-                                                       uint32_t* __restrict__ cframe) {
-  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n || status[f]) return;
-  const uint8_t* p = base + frames[f].offset;
-  const uint32_t len = frames[f].length;
-  uint64_t o = out_off[f];
-  const uint64_t o_end = out_off[f + 1];
-  uint64_t c = chunk_off[f];
-  bool ok = true;
-  uint32_t at = 0;
-  while (ok && at < len) {
-    const uint32_t type = ld_u8(p + at);
-    const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
-    at += 4;
-    const uint8_t* body = p + at;
-    at += cl;
-    if (type > 1) continue;  // stream identifiers and skippable chunks (validated by pass 1)
-    const uint32_t want = ld_u8(body) | (ld_u8(body + 1) << 8) | (ld_u8(body + 2) << 16) | (ld_u8(body + 3) << 24);
-    const uint64_t start = o;
-    if (type == 1) {
-      for (uint32_t k = 4; k < cl; ++k) out[o++] = body[k];
-    } else {
-      uint32_t ulen, used;
-      snappy_ulen(body + 4, cl - 4, ulen, used);
-      const uint8_t* q = body + 4 + used;
-      const uint8_t* qe = body + cl;
-      const uint64_t lim = start + ulen;
-      while (ok && q < qe) {
-        const uint32_t tag = *q++;
-        uint32_t ln, off;
-        if ((tag & 3) == 0) {  // literal
-          ln = tag >> 2;
-          if (ln >= 60) {
-            const uint32_t nb = ln - 59;
-            if ((uint64_t)(qe - q) < nb) {
-              ok = false;
-              break;
-            }
-            ln = 0;
-            for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)q[k] << (8 * k);
-            q += nb;
-          }
-          ln += 1;
-          if ((uint64_t)(qe - q) < ln || o + ln > lim) {
-            ok = false;
-            break;
-          }
-          for (uint32_t k = 0; k < ln; ++k) out[o + k] = q[k];
-          o += ln;
-          q += ln;
-          continue;
-        }
-        if ((tag & 3) == 1) {
-          if (q >= qe) {
-            ok = false;
-            break;
-          }
-          ln = 4 + ((tag >> 2) & 7);
-          off = ((tag >> 5) << 8) | *q++;
-        } else if ((tag & 3) == 2) {
-          if (qe - q < 2) {
-            ok = false;
-            break;
-          }
-          ln = 1 + (tag >> 2);
-          off = q[0] | ((uint32_t)q[1] << 8);
-          q += 2;
-        } else {
-          if (qe - q < 4) {
-            ok = false;
-            break;
-          }
-          ln = 1 + (tag >> 2);
-          off = q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-          q += 4;
-        }
-        if (off == 0 || off > o - start || o + ln > lim) {
-          ok = false;
-          break;
-        }
-        for (uint32_t k = 0; k < ln; ++k, ++o) out[o] = out[o - off];  // overlapping copies byte by byte
-      }
-      if (ok && o != lim) ok = false;
-    }
-    if (!ok || o > o_end) break;
-    lcrc_desc_dev d;
-    d.offset = start;
-    d.length = (uint32_t)(o - start);
-    d.expect_rel = LCRC_NO_EXPECT_DEV;
-    cdesc[c] = d;
-    cexp[c] = want;
-    cframe[c] = (uint32_t)f;
-    ++c;
-  }
-  if (!ok) {
-    status[f] = 1;
-    // the chunk slots this frame did not fill: empty ranges that match by construction
-    for (const uint64_t ce = chunk_off[f + 1]; c < ce; ++c) {
-      lcrc_desc_dev d;
-      d.offset = 0;
-      d.length = 0;
-      d.expect_rel = LCRC_NO_EXPECT_DEV;
-      cdesc[c] = d;
-      cexp[c] = 0;
-      cframe[c] = (uint32_t)f;
-    }
-  }
-}
-
-// pass 2, wave per frame: the compressed chunk is staged in LDS and decoded there, each Snappy element
-// copied by the 64 lanes at once (a copy whose offset is shorter than its length repeats the last `off`
-// bytes: lane k takes byte (k mod off) of them); the decoded chunk is then written out with 16 B per lane.
-// Chunks larger than the LDS staging (SN_CAP) take the lane-serial path of k_snappy_decode.
-constexpr uint32_t SN_CAP = 8192;
+// pass 2, one wave per frame: decode frame f into out[out_off[f] ..) and describe its data chunks for the
+// CRC pass -- cdesc (offset into out, length), cexp (stored masked CRC-32C), cframe (frame index).
+// Chunk headers are read through two 256 B register windows (lane j holds dword j; a byte is one
+// v_readlane with a scalar index). A compressed chunk is staged into LDS with dword loads, decoded in LDS
+// (snappy_wave_decode) and leaves LDS with 16 B per lane. Chunks over the LDS staging take a lane-serial
+// path from and to global memory.
+// LDS staging per wave (dynamic, sized by the launcher from the batch's largest chunk): in_lim compressed
+// bytes + SN_SLACK for the parse windows' header reads, then out_cap decoded bytes; each at most SN_MAX
+constexpr uint32_t SN_SLACK = 128;
+constexpr uint32_t SN_MAX = 16384;
 
 __device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// decode Snappy raw data in[0, n) (LDS) into o[0, ulen) (LDS); false when malformed
-__device__ bool snappy_wave_decode(const uint8_t* in, uint32_t n, uint8_t* o, uint32_t ulen, uint32_t lane) {
-  uint32_t q = 0;
-  // length preamble (already validated by pass 1): skip it
-  for (uint32_t i = 0; i < 5 && q < n; ++i) {
-    const uint32_t b = in[q++];
-    if (!(b & 128)) break;
+struct sn_reader {
+  const uint8_t* a;  // 4-byte aligned start (positions are relative to it)
+  uint32_t lim;      // readable bytes from a
+  uint32_t k;        // cur covers [256 k, 256 k + 256), nxt the next 256 B
+  uint32_t cur, nxt;
+
+  __device__ __forceinline__ uint32_t load(uint32_t w, uint32_t lane) const {
+    const uint32_t i = 256u * w + 4u * lane;
+    return i < lim ? *(const uint32_t*)(a + i) : 0u;  // the aligned dword of a readable byte is mapped
   }
-  uint32_t w = 0;  // bytes written
-  while (q < n) {
-    const uint32_t tag = bcast(in[q]);
-    ++q;
-    uint32_t ln, off = 0;
-    if ((tag & 3) == 0) {  // literal
-      ln = tag >> 2;
-      if (ln >= 60) {
-        const uint32_t nb = ln - 59;
-        if (n - q < nb) return false;
-        ln = 0;
-        for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)in[q + k] << (8 * k);
-        ln = bcast(ln);
-        q += nb;
+  __device__ __forceinline__ void init(const uint8_t* p, uint32_t len, uint32_t lane) {
+    a = p - ((uintptr_t)p & 3);  // pointer arithmetic keeps the global address space (no flat loads)
+    lim = (uint32_t)(p - a) + len;
+    k = 0;
+    cur = load(0, lane);
+    nxt = load(1, lane);
+  }
+  __device__ __forceinline__ void ensure(uint32_t i, uint32_t lane) {  // cur covers i (i never decreases)
+    const uint32_t w = i >> 8;
+    if (w == k + 1) {
+      cur = nxt;
+      k = w;
+      nxt = load(w + 1, lane);
+    } else if (w != k) {
+      k = w;
+      cur = load(w, lane);
+      nxt = load(w + 1, lane);
+    }
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t i) const {  // i in [256 k, 256 k + 512)
+    const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)((i >> 8) == k ? cur : nxt), (int)((i >> 2) & 63));
+    return (dw >> ((i & 3) * 8)) & 255u;
+  }
+  __device__ __forceinline__ uint32_t le(uint32_t i, uint32_t nb) const {  // nb <= 4 bytes little-endian
+    uint32_t v = 0;
+    for (uint32_t t = 0; t < nb; ++t) v |= byte(i + t) << (8 * t);
+    return v;
+  }
+};
+
+// Decode the Snappy elements staged at in[q, qe) (LDS) into o[0, ulen) (LDS); false when malformed.
+// Parsing is data-parallel: for a window of 64 candidate start positions base + lane, every lane decodes
+// the element that WOULD start at its byte (tag, header size, output length, offset or literal source)
+// and where the next one would start; the real starts are then the chain from lane 0, followed with one
+// v_readlane per element. A masked wave scan gives every element its output position, one ballot
+// validates the window, and the elements are executed in order: a literal is an LDS -> LDS copy, a copy
+// moves up to 64 bytes in one pass (a copy whose offset is shorter than its length repeats the last `off`
+// bytes: lane k takes byte k mod off of them). The next window starts where the chain left this one.
+// (Executing several elements per LDS round trip when their sources are outside the batch's output was
+// tried: the hazard bookkeeping is scalar work per element and lost 2.5x on chained copies.)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+  return v + (lane >= 16 ? r0 : 0u) + (lane >= 32 ? r1 : 0u) + (lane >= 48 ? r2 : 0u);
+}
+
+// x mod a for x < 64, 1 <= a <= 64: (x + 1/2) / a is at least 1/(2a) away from an integer, far beyond
+// the error of v_rcp_f32, so the floored quotient is exact
+__device__ __forceinline__ uint32_t small_mod(uint32_t x, uint32_t a) {
+  const float q = __builtin_floorf(((float)x + 0.5f) * __builtin_amdgcn_rcpf((float)a));
+  return x - (uint32_t)q * a;
+}
+
+__device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, uint8_t* o, uint32_t ulen,
+                                   uint32_t lane) {
+#if defined(LCRC_SN_PROBE) && LCRC_SN_PROBE == 1
+  return true;  // probe: frame overhead only
+#endif
+  uint32_t w0 = 0;  // bytes written before this window
+  for (uint32_t base = q; base < qe;) {
+    const uint32_t i = base + lane;  // candidate start (reads stay inside the staging's slack)
+    const uint32_t t = in[i], b1 = in[i + 1], b2 = in[i + 2], b3 = in[i + 3], b4 = in[i + 4];
+    const uint32_t typ = t & 3;
+    const uint32_t room = qe > i ? qe - i : 0;  // input bytes from the candidate start
+    uint32_t hdr, outlen, a;                     // a: copy offset, or the literal's source position
+    bool good;
+    if (typ == 0) {
+      const uint32_t L = t >> 2;
+      const uint32_t nb = L >= 60 ? L - 59 : 0;
+      const uint32_t ext = b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+      const uint32_t lm1 = nb ? (nb == 4 ? ext : ext & ((1u << (8 * nb)) - 1)) : L;
+      hdr = 1 + nb;
+      outlen = lm1 + 1;
+      a = i + hdr;
+      good = room >= hdr && lm1 < room - hdr;  // literal bytes inside the input (no u32 wrap)
+    } else {
+      hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
+      outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
+      a = typ == 1 ? ((t >> 5) << 8) | b1 : typ == 2 ? b1 | (b2 << 8) : b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+      good = room >= hdr;
+    }
+    const uint32_t size = typ == 0 ? hdr + outlen : hdr;
+    const uint32_t nxt = good ? lane + size : 0x7FFFFFFFu;
+    // the chain of real element starts in this window
+    const uint32_t lim = qe - base < 64 ? qe - base : 64;
+    uint64_t mask = 0;
+    uint32_t cur = 0;
+    while (cur < lim) {
+      mask |= 1ull << cur;
+      cur = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)cur);
+    }
+    const bool sel = (mask >> lane) & 1;
+    const uint32_t v = sel ? outlen : 0u;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    const uint32_t w = w0 + incl - v;
+    const bool bad = sel && (!good || w > ulen || outlen > ulen - w || (typ != 0 && (a == 0 || a > w)));
+    if (__builtin_amdgcn_ballot_w64(bad)) return false;
+    const uint32_t pw = (w & 0xFFFFu) | ((outlen - 1) << 16);   // w < ulen <= SN_MAX, outlen <= SN_MAX
+    const uint32_t pa = typ == 0 ? (0x80000000u | a) : a;       // valid offsets are <= w
+    // execute in order: a literal is an LDS -> LDS copy, a copy moves its <= 64 bytes in one pass
+    for (uint64_t m = mask; m; m &= m - 1) {
+      const int j = (int)__builtin_ctzll(m);
+      const uint32_t ew = (uint32_t)__builtin_amdgcn_readlane((int)pw, j);
+      const uint32_t ea = (uint32_t)__builtin_amdgcn_readlane((int)pa, j);
+      const uint32_t eo = ew & 0xFFFFu, eln = (ew >> 16) + 1;
+#if defined(LCRC_SN_PROBE) && LCRC_SN_PROBE == 2
+      if (eln) continue;  // probe: parse only
+#endif
+      if (ea & 0x80000000u) {
+        const uint32_t a = ea & 0x7FFFFFFFu;
+        for (uint32_t k = lane; k < eln; k += 64) o[eo + k] = in[a + k];
+      } else if (lane < eln) {  // the source byte of lane k is always already written
+        const uint32_t src = eo - ea + (ea >= eln ? lane : small_mod(lane, ea));
+        const uint8_t b = o[src];
+        __builtin_amdgcn_wave_barrier();
+        o[eo + lane] = b;
+      } else {
+        __builtin_amdgcn_wave_barrier();
       }
-      ln += 1;
-      if (n - q < ln || ulen - w < ln) return false;
-      for (uint32_t k = lane; k < ln; k += 64) o[w + k] = in[q + k];
-      w += ln;
-      q += ln;
-      continue;
     }
-    if ((tag & 3) == 1) {
-      if (q >= n) return false;
-      ln = 4 + ((tag >> 2) & 7);
-      off = ((tag >> 5) << 8) | in[q];
-      q += 1;
-    } else if ((tag & 3) == 2) {
-      if (n - q < 2) return false;
-      ln = 1 + (tag >> 2);
-      off = in[q] | ((uint32_t)in[q + 1] << 8);
-      q += 2;
-    } else {
-      if (n - q < 4) return false;
-      ln = 1 + (tag >> 2);
-      off = in[q] | ((uint32_t)in[q + 1] << 8) | ((uint32_t)in[q + 2] << 16) | ((uint32_t)in[q + 3] << 24);
-      q += 4;
-    }
-    off = bcast(off);
-    if (off == 0 || off > w || ulen - w < ln) return false;
-    // ln <= 64: one pass; the source byte of lane k is w - off + (k mod off), always already written
-    if (lane < ln) {
-      const uint32_t src = w - off + (off >= ln ? lane : lane % off);
-      const uint8_t v = o[src];
-      __builtin_amdgcn_wave_barrier();
-      o[w + lane] = v;
-    } else {
-      __builtin_amdgcn_wave_barrier();
-    }
-    w += ln;
+    w0 += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    base += cur;
   }
-  return w == ulen;
+  return w0 == ulen;
 }
 
 __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __restrict__ base,
@@ -1258,9 +1230,11 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
                                                            const uint64_t* __restrict__ chunk_off,
                                                            uint8_t* __restrict__ out, uint8_t* __restrict__ status,
                                                            lcrc_desc_dev* __restrict__ cdesc,
-                                                           uint32_t* __restrict__ cexp, uint32_t* __restrict__ cframe) {
-  __shared__ __attribute__((aligned(16))) uint8_t lin[SN_CAP];
-  __shared__ __attribute__((aligned(16))) uint8_t lout[SN_CAP];
+                                                           uint32_t* __restrict__ cexp, uint32_t* __restrict__ cframe,
+                                                           uint32_t in_lim, uint32_t out_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sn_lds[];
+  uint8_t* const lin = sn_lds;
+  uint8_t* const lout = sn_lds + in_lim + SN_SLACK;
   const uint32_t lane = __lane_id();
   for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
     if (status[f]) continue;
@@ -1268,80 +1242,92 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
     const uint32_t len = frames[f].length;
     uint64_t o = out_off[f];
     uint64_t c = chunk_off[f];
+    sn_reader rd;
+    rd.init(p, len, lane);
+    const uint32_t end = rd.lim;
     bool ok = true;
-    uint32_t at = 0;
-    while (ok && at < len) {
-      const uint32_t type = bcast(p[at]);
-      const uint32_t cl = bcast(p[at + 1] | ((uint32_t)p[at + 2] << 8) | ((uint32_t)p[at + 3] << 16));
-      at += 4;
-      const uint8_t* body = p + at;
-      at += cl;
-      if (type > 1) continue;  // stream identifiers and skippable chunks (validated by pass 1)
-      const uint32_t want = bcast(body[0] | ((uint32_t)body[1] << 8) | ((uint32_t)body[2] << 16) |
-                                  ((uint32_t)body[3] << 24));
+    uint32_t at = (uint32_t)(p - rd.a);
+    // the framing was validated by pass 1: chunk headers and lengths are in bounds, preambles are sane
+    while (ok && at < end) {
+      rd.ensure(at, lane);
+      const uint32_t type = rd.byte(at);
+      const uint32_t cl = rd.le(at + 1, 3);
+      const uint32_t body = at + 4;
+      at = body + cl;
+      if (type > 1) continue;  // stream identifiers and skippable chunks
+      rd.ensure(body, lane);
+      const uint32_t want = rd.le(body, 4);
       const uint64_t start = o;
       if (type == 1) {
-        for (uint32_t k = 4 + lane; k < cl; k += 64) out[o + k - 4] = body[k];
+        const uint8_t* src = rd.a + body + 4;
+        for (uint32_t k = lane; k < cl - 4; k += 64) out[o + k] = src[k];
         o += cl - 4;
       } else {
-        // preamble = uncompressed length (validated by pass 1)
-        uint32_t ulen = 0;
-        for (uint32_t i = 0, sh = 0; i < 5 && 4 + i < cl; ++i, sh += 7) {
-          const uint32_t b = body[4 + i];
+        uint32_t ulen = 0, q = body + 4;  // preamble = uncompressed length
+        for (uint32_t i = 0, sh = 0; i < 5 && q < at; ++i, sh += 7) {
+          const uint32_t b = rd.byte(q++);
           ulen |= (b & 127u) << sh;
           if (!(b & 128)) break;
         }
-        ulen = bcast(ulen);
-        const uint32_t zn = cl - 4;
-        if (zn <= SN_CAP && ulen <= SN_CAP) {
-          for (uint32_t k = lane; k < zn; k += 64) lin[k] = body[4 + k];
+        if (ulen <= out_cap && at - q + 4 <= in_lim) {
+          // stage the elements: aligned dwords from the one holding the first byte
+          const uint8_t* zs = rd.a + q;
+          const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
+          const uint32_t* za = (const uint32_t*)(zs - d);
+          const uint32_t ndw = (d + (at - q) + 3) >> 2;
+          for (uint32_t k = lane; k < ndw; k += 64) ((uint32_t*)lin)[k] = za[k];
           __builtin_amdgcn_s_waitcnt(0);
           __builtin_amdgcn_wave_barrier();
-          ok = snappy_wave_decode(lin, zn, lout, ulen, lane);
+          ok = snappy_wave_decode(lin, d, d + (at - q), lout, ulen, lane);
           __builtin_amdgcn_wave_barrier();
           if (ok) {
-            for (uint32_t k = lane; k < ulen; k += 64) out[o + k] = lout[k];
+            if ((o & 15) == 0) {
+              uint32_t k = 16 * lane;
+              for (; k + 16 <= ulen; k += 1024)
+                *(uint4*)(out + o + k) = *(const uint4*)(lout + k);
+              for (; k < ulen; ++k) out[o + k] = lout[k];  // the lane holding the tail (< 16 B)
+            } else {
+              for (uint32_t k = lane; k < ulen; k += 64) out[o + k] = lout[k];
+            }
             o += ulen;
           }
         } else if (lane == 0) {  // too large for the staging: lane-serial, from and to global memory
-          const uint8_t* q = body + 4;
-          const uint8_t* qe = body + cl;
-          for (uint32_t i = 0; i < 5; ++i)
-            if (!(*q++ & 128)) break;
+          const uint8_t* qp = rd.a + q;
+          const uint8_t* qe = rd.a + at;
           const uint64_t lim = start + ulen;
-          while (ok && q < qe) {
-            const uint32_t tag = *q++;
+          while (ok && qp < qe) {
+            const uint32_t tag = *qp++;
             uint32_t ln, off;
             if ((tag & 3) == 0) {
               ln = tag >> 2;
               if (ln >= 60) {
                 const uint32_t nb = ln - 59;
-                if ((uint64_t)(qe - q) < nb) { ok = false; break; }
+                if ((uint64_t)(qe - qp) < nb) { ok = false; break; }
                 ln = 0;
-                for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)q[k] << (8 * k);
-                q += nb;
+                for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)qp[k] << (8 * k);
+                qp += nb;
               }
               ln += 1;
-              if ((uint64_t)(qe - q) < ln || o + ln > lim) { ok = false; break; }
-              for (uint32_t k = 0; k < ln; ++k) out[o + k] = q[k];
+              if ((uint64_t)(qe - qp) < ln || o + ln > lim) { ok = false; break; }
+              for (uint32_t k = 0; k < ln; ++k) out[o + k] = qp[k];
               o += ln;
-              q += ln;
+              qp += ln;
               continue;
             }
             if ((tag & 3) == 1) {
-              if (q >= qe) { ok = false; break; }
+              if (qp >= qe) { ok = false; break; }
               ln = 4 + ((tag >> 2) & 7);
-              off = ((tag >> 5) << 8) | *q++;
+              off = ((tag >> 5) << 8) | *qp++;
             } else if ((tag & 3) == 2) {
-              if (qe - q < 2) { ok = false; break; }
+              if (qe - qp < 2) { ok = false; break; }
               ln = 1 + (tag >> 2);
-              off = q[0] | ((uint32_t)q[1] << 8);
-              q += 2;
+              off = qp[0] | ((uint32_t)qp[1] << 8);
+              qp += 2;
             } else {
-              if (qe - q < 4) { ok = false; break; }
+              if (qe - qp < 4) { ok = false; break; }
               ln = 1 + (tag >> 2);
-              off = q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-              q += 4;
+              off = qp[0] | ((uint32_t)qp[1] << 8) | ((uint32_t)qp[2] << 16) | ((uint32_t)qp[3] << 24);
+              qp += 4;
             }
             if (off == 0 || off > o - start || o + ln > lim) { ok = false; break; }
             for (uint32_t k = 0; k < ln; ++k, ++o) out[o] = out[o - off];
@@ -1365,6 +1351,7 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
     }
     if (!ok && lane == 0) {
       status[f] = 1;
+      // the chunk slots this frame did not fill: empty ranges that match by construction
       for (const uint64_t ce = chunk_off[f + 1]; c < ce; ++c) {
         lcrc_desc_dev d;
         d.offset = 0;
@@ -1639,10 +1626,10 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
 }
 
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
-                                   uint64_t* nchunks, uint8_t* status, hipStream_t st) {
+                                   uint64_t* nchunks, uint8_t* status, uint32_t* maxes, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(lcrc_dev::k_snappy_size, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, frames, n, size,
-                     nchunks, status);
+                     nchunks, status, maxes);
   return hipGetLastError();
 }
 
@@ -1658,11 +1645,17 @@ hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, u
 
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
-                                     lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, hipStream_t st) {
+                                     lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
+                                     uint32_t max_out, hipStream_t st) {
+  using lcrc_dev::SN_MAX;
   if (n == 0) return hipSuccess;
-  const uint64_t g = n < 8192 ? n : 8192;  // one wave per frame, grid-stride
-  hipLaunchKernelGGL(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), 0, st, base, frames, n, out_off,
-                     chunk_off, out, status, cdesc, cexp, cframe);
+  const uint64_t g = n < 16384 ? n : 16384;  // one wave per frame, grid-stride
+  // LDS sized to the batch's largest chunk (bigger ones take the lane-serial path): small staging, many waves
+  const uint32_t in_lim = max_in + 4 < SN_MAX ? (max_in + 4 + 15) & ~15u : SN_MAX;
+  const uint32_t out_cap = max_out < SN_MAX ? (max_out + 15) & ~15u : SN_MAX;
+  const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
+  hipLaunchKernelGGL(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
+                     chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap);
   return hipGetLastError();
 }
 

@@ -378,3 +378,73 @@ def test_table_scan_index_restart_intervals(lcrc, orc, engines, interval):
     want, werr = orc.table_scan_expect(f)
     assert err is None and werr is None and _as_tuples(got) == want
     assert (got["status"] == 0).all()
+
+
+def _snappy_elements(rng, target):
+    """A valid Snappy raw stream of random elements in every encoding the format has (literals with 0-4
+    extra length bytes, 1-, 2- and 4-byte-offset copies, overlapping copies with offsets 1..8); returns
+    (compressed, decoded)."""
+    out, z = bytearray(), bytearray()
+    while len(out) < target:
+        if not out or rng.random() < 0.25:
+            n = int(rng.choice([rng.integers(1, 61), rng.integers(61, 300), rng.integers(256, 2000)]))
+            need = 0 if n <= 60 else 1 if n <= 256 else 2
+            nb = need if rng.random() < 0.6 else int(rng.integers(max(need, 1), 5))
+            if nb == 0:
+                z.append((n - 1) << 2)
+            else:
+                z.append((59 + nb) << 2)
+                z += (n - 1).to_bytes(nb, "little")
+            lit = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            z += lit
+            out += lit
+            continue
+        kind = int(rng.integers(1, 4))
+        near = rng.random() < 0.3
+        if kind == 1:
+            n = int(rng.integers(4, 12))
+            off = int(rng.integers(1, min(len(out), 8 if near else 2047) + 1))
+            z += bytes([((off >> 8) << 5) | ((n - 4) << 2) | 1, off & 0xFF])
+        else:
+            n = int(rng.integers(1, 65))
+            off = int(rng.integers(1, min(len(out), 8 if near else 65535) + 1))
+            z += bytes([((n - 1) << 2) | kind]) + off.to_bytes(2 if kind == 2 else 4, "little")
+        for _ in range(n):
+            out.append(out[-off])
+    return orc_varint(len(out)) + bytes(z), bytes(out)
+
+
+def orc_varint(v):
+    b = bytearray()
+    while v >= 128:
+        b.append((v & 127) | 128)
+        v >>= 7
+    b.append(v)
+    return bytes(b)
+
+
+@pytest.mark.gpu
+def test_snappy_frames_device_all_element_forms(lcrc, orc, engines):
+    """Every element encoding, overlapping copies, chunks on both sides of the LDS staging (8 KiB), and
+    random single-byte corruptions: status and contents against the oracle's decoder."""
+    rng = np.random.default_rng(2024)
+    streams, want = [], []
+    for k in range(400):
+        target = int(rng.integers(1, 20000)) if k % 7 == 0 else int(rng.integers(1, 6000))
+        z, raw = _snappy_elements(rng, target)
+        assert orc._snappy_raw(z) == raw
+        body = orc.mask(orc.crc(raw, 1)).to_bytes(4, "little") + z
+        s = bytearray(b"\xff\x06\x00\x00sNaPpY" + bytes([0, len(body) & 0xFF, (len(body) >> 8) & 0xFF,
+                                                          len(body) >> 16]) + body)
+        if k % 3 == 2:  # corrupt one element byte (the oracle says whether the frame still decodes)
+            p = 18 + int(rng.integers(0, len(z)))
+            s[p] ^= 1 << int(rng.integers(0, 8))
+        streams.append(bytes(s))
+        want.append(orc.snappy_frame_decode(bytes(s)))
+    base, dd = _frames_on_device(lcrc, streams)
+    got, status = engines[lcrc.MODE_C].snappy_frames(base, dd, len(streams))
+    assert [int(x != 0) for x in status] == [int(w is None) for w in want]
+    for g_, w_ in zip(got, want):
+        if w_ is not None:
+            assert g_ == w_
+    assert sum(w is None for w in want) > 20
