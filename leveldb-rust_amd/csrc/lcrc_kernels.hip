@@ -560,27 +560,27 @@ __device__ __forceinline__ uint32_t row_bcast0(uint32_t v, uint32_t lane) {
 // Must be called by all 64 lanes (contains cross-lane ops).
 __device__ uint32_t row_walk(const uint32_t* L, const RowPiece& p, bool empty_range, uint32_t R0, uint32_t g,
                              uint32_t lane) {
-  uint32_t cv = 0;
-  if (p.kind == 1) {
-    uint32_t rr = p.at_a ? R0 : 0u;
-    rr = step4(L, rr, p.w.x);
-    rr = step4(L, rr, p.w.y);
-    rr = step4(L, rr, p.w.z);
-    rr = step4(L, rr, p.w.w);
-    cv = rr;
-  } else if (p.kind == 2) {
-    // bytes [first, 16) walked from R0 (1..15 of them): the bytes up to the next word boundary one at a
-    // time, then whole words -- at most 3 + 3 dependent steps instead of 15
-    uint32_t rr = R0;
-    const uint32_t fw = (p.first + 3) >> 2;  // first whole word
+  // Branch-free for every kind: the bytes of the piece before the range are zeroed (a zero prefix walked
+  // from register 0 stays 0, so every piece is a whole 16 B unit of the tree), and the register R0 at the
+  // range start is injected into the first bytes: walk(R0, M) = walk(0, M ^ LE(R0)[0, k)) ^ (R0 >> 8k)
+  // with k = min(|M|, 4) (the high part of R0 just shifts out when fewer than 4 bytes follow).
+  const uint32_t f = p.kind == 2 ? p.first : 0u;  // bytes of the piece before the range
+  const bool inj = p.kind == 2 || (p.kind == 1 && p.at_a);
+  const uint32_t k = 16 - f < 4 ? 16 - f : 4u;
+  const uint32_t rl = !inj ? 0u : k == 4 ? R0 : R0 & ((1u << (8 * k)) - 1);
+  const uint32_t rh = inj && k < 4 ? R0 >> (8 * k) : 0u;
+  const uint64_t sh = (uint64_t)rl << (8 * (f & 3));
+  const uint32_t qf = f >> 2;
+  uint32_t wq[4];
 #pragma unroll
-    for (int i = 1; i < 16; ++i)
-      if ((uint32_t)i >= p.first && (uint32_t)i < 4 * fw) rr = byte_step(L, rr, (p.w[i >> 2] >> (8 * (i & 3))) & 0xff);
-#pragma unroll
-    for (int q = 1; q < 4; ++q)
-      if ((uint32_t)q >= fw) rr = step4(L, rr, p.w[q]);
-    cv = rr;
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint32_t m = 4 * q + 4 <= f ? 0u : 4 * q >= f ? ~0u : ~0u << (8 * (f - 4 * q));
+    wq[q] = (p.w[q] & m) ^ (q == qf ? (uint32_t)sh : q == qf + 1 ? (uint32_t)(sh >> 32) : 0u);
   }
+  uint32_t cv = step4(L, 0u, wq[0]);
+  cv = step4(L, cv, wq[1]);
+  cv = step4(L, cv, wq[2]);
+  cv = step4(L, cv, wq[3]) ^ rh;
   // row tree: level m joins lane g with g + 2^m, shifting the left part by 16*2^m bytes
 #pragma unroll
   for (int m = 0; m < 4; ++m) {  // only the combining lanes look up (exec-masked: fewer bank conflicts)
