@@ -82,3 +82,17 @@ def test_batched_api_fails_loudly_without_device(lcrc):
     with pytest.raises(lcrc.NoDeviceError):
         lcrc.Engine(0, lcrc.MODE_C)
     assert lcrc.lib().lcrc_batch(None, None, 0, None, 0, None, None, None) == lcrc.EINVAL
+
+
+def test_scalar_extend_every_length_and_register(lcrc, orc):
+    """The host CRCs (carry-less-multiply folding from 64 bytes on, tables / crc32 below) against zlib and the
+    oracle for every length 0..700, large sizes, unaligned starts and arbitrary running values."""
+    rng = np.random.default_rng(77)
+    buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
+    for n in list(range(0, 700)) + [1023, 1024, 1025, 4096, 4097, 65536 + 13, (1 << 20) - 5]:
+        off = int(rng.integers(0, 5))
+        d = buf[off:off + n]
+        init = int(rng.integers(0, 1 << 32))
+        assert lcrc.extend(init, d, lcrc.MODE_REF) == zlib.crc32(d, init)
+        if n < 5000:
+            assert lcrc.extend(init, d, lcrc.MODE_C) == orc.crc(d, 1, init)

@@ -102,3 +102,31 @@ def test_uniform_mt_matches(orc):
     want_r = orc.crc_ranges(data, np.arange(256) * 4096, np.full(256, 4096), 0)
     got, _ = orc.crc_uniform_mt(data, 256, 4096, 4096, 3, orc.ALGO_PCLMUL_REF)
     assert np.array_equal(got, want_r)
+
+
+def test_host_clmul_constants():
+    """The carry-less-multiply folding constants of csrc/lcrc_scalar.cpp, recomputed from P."""
+
+    def xmod(e, P):
+        r = 1
+        for _ in range(e):
+            r <<= 1
+            if r >> 32 & 1:
+                r ^= P
+        return r
+
+    def refl(v, bits):
+        return int(bin(v)[2:].zfill(bits)[::-1], 2)
+
+    for P, ks, mu, p in ((0x104C11DB7, (0x0154442bd4, 0x01c6e41596, 0x01751997d0, 0x00ccaa009e, 0x0163cd6124),
+                          0x01f7011641, 0x01db710641),
+                         (0x11EDC6F41, (0x00740eef02, 0x009e4addf8, 0x00f20c0dfe, 0x014cd00bd6, 0x00dd45aab8),
+                          0x00dea713f1, 0x0105ec76f1)):
+        for e, k in zip((128 * 4 + 32, 128 * 4 - 32, 128 + 32, 128 - 32, 64), ks):
+            assert refl(xmod(e, P), 32) << 1 == k
+        num, q = 1 << 64, 0
+        while num.bit_length() >= 33:
+            sh = num.bit_length() - 33
+            q |= 1 << sh
+            num ^= P << sh
+        assert refl(q, 33) == mu and refl(P, 33) == p
