@@ -340,7 +340,20 @@ def cpu_baseline(orc, sample, mode, seconds, device_crcs):
         total += s
         passes += 1
     gib = passes * nblk * blen / 2 ** 30
+    one, one_s = 0, 0.0  # the same restatement on one core (single thread and all cores)
+    while one_s < min(seconds, 1.0) or one < 1:
+        _, s1 = orc.crc_uniform_mt(data, nblk, blen, blen, 1, algo)
+        one_s += s1
+        one += 1
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": round(gib / total, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "single_thread": round(one * nblk * blen / 2 ** 30 / one_s, 2), "cpu_model": model,
+            "host_cpus": os.cpu_count(),
             "sample": f"{passes} passes over one 64K x 4 KiB batch ({gib:.1f} GiB), "
                       f"{'snap SSE4.2 crc32c' if mode == 'c' else 'crc32fast PCLMULQDQ'} restated in oracle/, "
                       f"{threads} threads",
