@@ -945,9 +945,8 @@ __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__
                                                      uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
                                                      uint8_t* __restrict__ status, uint32_t* __restrict__ maxes) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n) return;
-  const uint8_t* p = base + frames[f].offset;
-  const uint32_t len = frames[f].length;
+  const uint8_t* p = f < n ? base + frames[f].offset : base;
+  const uint32_t len = f < n ? frames[f].length : 0u;
   uint64_t total = 0, chunks = 0;
   uint32_t max_in = 0, max_out = 0;  // largest compressed data (after the crc) / decoded chunk
   bool ok = true, seen_id = false;
@@ -984,11 +983,21 @@ __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__
     }
     at += cl;
   }
-  size[f] = ok ? total : 0;
-  nchunks[f] = ok ? chunks : 0;
-  status[f] = ok ? 0 : 1;
-  if (ok && max_in) atomicMax(&maxes[0], max_in);
-  if (ok && max_out) atomicMax(&maxes[1], max_out);
+  if (f < n) {
+    size[f] = ok ? total : 0;
+    nchunks[f] = ok ? chunks : 0;
+    status[f] = ok ? 0 : 1;
+  }
+  // one atomic per wave (the build turns the compiler's atomic combining off for the hot kernels)
+  uint32_t mi = ok ? max_in : 0u, mo = ok ? max_out : 0u;
+  for (int d = 1; d < 64; d <<= 1) {
+    mi = max(mi, (uint32_t)__shfl_xor((int)mi, d, 64));
+    mo = max(mo, (uint32_t)__shfl_xor((int)mo, d, 64));
+  }
+  if (__lane_id() == 0) {
+    if (mi) atomicMax(&maxes[0], mi);
+    if (mo) atomicMax(&maxes[1], mo);
+  }
 }
 
 // exclusive scans of two u64 arrays (n entries): per-workgroup part, then every element adds the totals
