@@ -120,7 +120,8 @@ struct lcrc_ctx {
   DevBuf<uint64_t> wal_offsets;
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs;
-  uint64_t* h_count = nullptr;  // pinned: record count of the synchronous WAL scan
+  uint64_t* h_count = nullptr;  // pinned, 8 words: [0] record count of the synchronous WAL scan, [1..3] table
+                                // scan staging, [4..6] Snappy totals and maxima
   // Snappy frames: chunk CRCs are CRC-32C whatever the context's mode
   uint32_t* d_tab_c = nullptr;  // CRC-32C image when mode != C (created on first use)
   DevBuf<uint64_t> sn_size, sn_nch, sn_choff, sn_part;
@@ -225,7 +226,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
     if ((e = hipEventCreateWithFlags(&ctx->ev_copied[i], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming)) != hipSuccess)
       return bail(fail_hip(e, "hipEventCreate"));
-  if ((e = hipHostMalloc(&ctx->h_count, sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
+  if ((e = hipHostMalloc(&ctx->h_count, 8 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
     return bail(fail_hip(e, "hipHostMalloc"));
 
   // constant tables for this mode
@@ -496,10 +497,10 @@ static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_des
   HIPCHK(hipMemsetAsync(ctx->sn_max.p, 0, 8, st));
   HIPCHK(lcrc_launch_snappy_size(base, frames, n, ctx->sn_size.p, ctx->sn_nch.p, status, ctx->sn_max.p, st));
   HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, n, out_off, ctx->sn_choff.p, ctx->sn_part.p, st));
-  uint64_t tot[2];
+  uint64_t* tot = ctx->h_count + 4;  // pinned staging: totals, then the two maxima
+  uint32_t* mx = (uint32_t*)(ctx->h_count + 6);
   HIPCHK(hipMemcpyAsync(&tot[0], out_off + n, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], ctx->sn_choff.p + n, 8, hipMemcpyDeviceToHost, st));
-  uint32_t mx[2];
   HIPCHK(hipMemcpyAsync(mx, ctx->sn_max.p, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   *total_out = tot[0];
@@ -550,8 +551,9 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     return TBL_FALLBACK;
   // Table::open: read_block_from_file(index, verify_checksum = paranoid_checks) -- the checksum and the
   // type byte on the device
+  // the window pass spans the buffer it is given: verify the index block on its own bytes
   lcrc_desc_dev idesc;
-  idesc.offset = index_h.offset;
+  idesc.offset = 0;
   idesc.length = (uint32_t)(index_h.size + 1);
   idesc.expect_rel = (int32_t)(index_h.size + 1);
   const uint64_t tpos = index_h.offset + index_h.size;
@@ -560,19 +562,28 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     return rc;
   HIPCHK(hipMemcpyAsync(ctx->tbl_descs.p, &idesc, sizeof(idesc), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(ctx->tbl_pos.p, &tpos, sizeof(tpos), hipMemcpyHostToDevice, st));
-  if ((rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->tbl_descs.p, 1, ctx->tbl_crcs.p, ctx->tbl_mm.p, st)))
+  if ((rc = lcrc_batch(ctx, file + index_h.offset, index_h.size + BLOCK_TRAILER_SIZE,
+                       (const lcrc_desc*)ctx->tbl_descs.p, 1, ctx->tbl_crcs.p, ctx->tbl_mm.p, st)))
     return rc;
   HIPCHK(lcrc_launch_gather_u8(file, ctx->tbl_pos.p, 1, ctx->tbl_types.p, st));
-  uint32_t imm = 0;
-  uint8_t itype = 0;
-  HIPCHK(hipMemcpyAsync(&imm, ctx->tbl_mm.p, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&itype, ctx->tbl_types.p, 1, hipMemcpyDeviceToHost, st));
+  // one pinned round trip: the mismatch bit, the type byte and (for a raw index) its restart count
+  uint8_t* hs = (uint8_t*)(ctx->h_count + 1);
+  memset(hs, 0, 16);
+  HIPCHK(hipMemcpyAsync(hs, ctx->tbl_mm.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hs + 4, ctx->tbl_types.p, 1, hipMemcpyDeviceToHost, st));
+  if (index_h.size >= 4)
+    HIPCHK(hipMemcpyAsync(hs + 8, file + index_h.offset + index_h.size - 4, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  uint32_t imm, nres_raw;
+  memcpy(&imm, hs, 4);
+  memcpy(&nres_raw, hs + 8, 4);
+  const uint8_t itype = hs[4];
   if (imm & 1) return corrupt("block checksum mismatch");
   const uint8_t* contents = file + index_h.offset;
   uint64_t clen = index_h.size;
   if (itype == 1) {  // Snappy-framed index block, decoded on the device
     if ((rc = ctx->sn_out_off.ensure(2)) || (rc = ctx->sn_status.ensure(1))) return rc;
+    idesc.offset = index_h.offset;
     idesc.length = (uint32_t)index_h.size;
     idesc.expect_rel = LCRC_NO_EXPECT_DEV;
     HIPCHK(hipMemcpyAsync(ctx->tbl_descs.p, &idesc, sizeof(idesc), hipMemcpyHostToDevice, st));
@@ -596,8 +607,8 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
   // Block::from_content (block.rs:21-41)
   if (clen < 4) return corrupt("bad block contents, size smaller than u32");
   if (clen > 0xFFFFFFFFull) return TBL_FALLBACK;
-  uint32_t nres = 0;
-  HIPCHK(hipMemcpy(&nres, contents + clen - 4, 4, hipMemcpyDeviceToHost));
+  uint32_t nres = nres_raw;
+  if (itype == 1) HIPCHK(hipMemcpy(&nres, contents + clen - 4, 4, hipMemcpyDeviceToHost));
   if ((uint64_t)nres > (clen - 4) / 4) return corrupt("bad block contents");
   // entries without restart points, or segments so long that one thread per segment would be slower than
   // the host (the reference's index blocks restart at every entry, table.rs:272): the sequential walk
@@ -611,7 +622,7 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
                                nullptr, st));
   HIPCHK(lcrc_launch_scan2(ctx->idx_count.p, ctx->idx_flag.p, nres, ctx->idx_pos.p, ctx->idx_fpos.p, ctx->sn_part.p,
                            st));
-  uint64_t tot[2];
+  uint64_t* tot = ctx->h_count + 2;  // pinned
   HIPCHK(hipMemcpyAsync(&tot[0], ctx->idx_pos.p + nres, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], ctx->idx_fpos.p + nres, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
