@@ -485,11 +485,13 @@ int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wa
 }
 
 // ---- Snappy framing: decode + per-chunk masked CRC-32C verify ----
-static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* frames, size_t n, uint8_t* out,
-                              uint64_t out_cap, uint64_t* out_off, uint8_t* status, uint64_t* total_out, hipStream_t st) {
+// Snappy framing in two halves around the one host round trip it needs. plan: sizes, chunk counts and the
+// batch maxima on the device, their scans, and the totals queued for the pinned staging (h_count[4..6])
+// -- no synchronisation. run (after the caller synchronised): capacity check, decode, masked CRC-32C of
+// every chunk and the compare -- enqueued, no synchronisation.
+static int snappy_plan(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* frames, size_t n, uint64_t* out_off,
+                       uint8_t* status, hipStream_t st) {
   int rc;
-  *total_out = 0;
-  if (n == 0) return LCRC_OK;
   const size_t nparts = (n + 255) / 256;
   if ((rc = ctx->sn_size.ensure(n)) || (rc = ctx->sn_nch.ensure(n)) || (rc = ctx->sn_choff.ensure(n + 1)) ||
       (rc = ctx->sn_part.ensure(2 * nparts)) || (rc = ctx->sn_max.ensure(2)))
@@ -497,12 +499,18 @@ static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_des
   HIPCHK(hipMemsetAsync(ctx->sn_max.p, 0, 8, st));
   HIPCHK(lcrc_launch_snappy_size(base, frames, n, ctx->sn_size.p, ctx->sn_nch.p, status, ctx->sn_max.p, st));
   HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, n, out_off, ctx->sn_choff.p, ctx->sn_part.p, st));
-  uint64_t* tot = ctx->h_count + 4;  // pinned staging: totals, then the two maxima
-  uint32_t* mx = (uint32_t*)(ctx->h_count + 6);
+  uint64_t* tot = ctx->h_count + 4;  // pinned staging: decoded total, chunk total, then the two maxima
   HIPCHK(hipMemcpyAsync(&tot[0], out_off + n, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], ctx->sn_choff.p + n, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(mx, ctx->sn_max.p, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipMemcpyAsync(ctx->h_count + 6, ctx->sn_max.p, 8, hipMemcpyDeviceToHost, st));
+  return LCRC_OK;
+}
+
+static int snappy_run(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* frames, size_t n, uint8_t* out,
+                      uint64_t out_cap, uint64_t* out_off, uint8_t* status, uint64_t* total_out, hipStream_t st) {
+  int rc;
+  const uint64_t* tot = ctx->h_count + 4;
+  const uint32_t* mx = (const uint32_t*)(ctx->h_count + 6);
   *total_out = tot[0];
   if (tot[0] > out_cap || (tot[0] && !out)) return LCRC_ERANGE;
   const uint64_t nch = tot[1];
@@ -521,6 +529,17 @@ static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_des
                             st));
   HIPCHK(lcrc_launch_snappy_check(ctx->sn_ccrc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, ctx->sn_choff.p + n, nch, status,
                                   st));
+  return LCRC_OK;
+}
+
+static int snappy_frames_impl(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* frames, size_t n, uint8_t* out,
+                              uint64_t out_cap, uint64_t* out_off, uint8_t* status, uint64_t* total_out, hipStream_t st) {
+  int rc;
+  *total_out = 0;
+  if (n == 0) return LCRC_OK;
+  if ((rc = snappy_plan(ctx, base, frames, n, out_off, status, st))) return rc;
+  HIPCHK(hipStreamSynchronize(st));
+  if ((rc = snappy_run(ctx, base, frames, n, out, out_cap, out_off, status, total_out, st))) return rc;
   HIPCHK(hipStreamSynchronize(st));
   return LCRC_OK;
 }
@@ -684,18 +703,22 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
   if ((rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->tbl_descs.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, st)))
     return rc;
   HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, st));
-  uint64_t total = 0;
-  rc = snappy_frames_impl(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
-                          ctx->sn_status.p, &total, st);
-  if (rc == LCRC_ERANGE) {
-    if ((rc = ctx->sn_out.ensure(total))) return rc;
-    rc = snappy_frames_impl(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
-                            ctx->sn_status.p, &total, st);
-  }
-  if (rc) return rc;
+  // the Snappy frames' framing pass (a malformed frame is already status 3 here), then the results and the
+  // frame totals come back in ONE round trip; only a table with compressed blocks goes on to decode them
+  if ((rc = snappy_plan(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out_off.p, ctx->sn_status.p, st))) return rc;
   HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, st));
   HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (ctx->h_count[5]) {  // data chunks to decode and check
+    uint64_t total = 0;
+    if ((rc = ctx->sn_out.ensure(ctx->h_count[4]))) return rc;
+    if ((rc = snappy_run(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
+                         ctx->sn_status.p, &total, st)))
+      return rc;
+    HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, st));
+    HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   // sorted by offset (a well-formed table already is)
   bool sorted = true;
   for (size_t k = 1; k < n && sorted; ++k) sorted = blocks[k - 1].offset <= blocks[k].offset;
