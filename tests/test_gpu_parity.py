@@ -297,3 +297,47 @@ def test_graph_replay_matches_direct(lcrc, orc):
     finally:
         eng.graph_destroy(g)
     eng.close()
+
+
+def test_graph_replay_general_path_and_wal(lcrc, orc):
+    """The general path (k_windows + k_blocks over descriptors) and the device-only WAL scan captured in one
+    HIP graph after lcrc_ctx_reserve, replayed: the same CRCs, verdicts, records and counts as direct calls."""
+    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
+    rng = np.random.default_rng(91)
+    data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    offs = np.sort(rng.choice(len(data) - 70000, 500, replace=False)).astype(np.uint64)
+    lens = rng.integers(0, 70000, 500).astype(np.uint32)
+    d = np.zeros(500, lcrc.DESC_DTYPE)
+    d["offset"], d["length"], d["expect_rel"] = offs, lens, lcrc.NO_EXPECT
+    base = lcrc.DeviceBuffer.from_host(data)
+    dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8))
+    out = lcrc.DeviceBuffer(4 * 500)
+    recs = [rng.integers(0, 256, int(rng.integers(0, 1 << int(rng.integers(1, 15)))), dtype=np.uint8).tobytes()
+            for _ in range(200)]
+    log = orc.log_write(recs)
+    ldev = lcrc.DeviceBuffer.from_host(np.frombuffer(log, np.uint8))
+    cap = len(log) // 7 + 1
+    rd = lcrc.DeviceBuffer(cap * lcrc.WAL_REC_DTYPE.itemsize)
+    cnt = lcrc.DeviceBuffer(8)
+    eng.reserve(max(len(data), len(log)))
+    want_wal = eng.wal_scan(ldev, len(log))
+    want_crc = np.array([orc.mask(int(c)) for c in orc.crc_ranges(data.tobytes(), offs, lens, 1)], np.uint32)
+
+    def calls():
+        eng.batch(base, len(data), dd, 500, out)
+        eng.wal_scan_async(ldev, len(log), rd, cap, cnt)
+
+    g = eng.graph_capture(calls)
+    try:
+        for _ in range(2):
+            out.zero()
+            cnt.zero()
+            eng.graph_launch(g)
+            eng.sync()
+            assert np.array_equal(out.download(np.uint32, 500), want_crc)
+            n = int(cnt.download(np.uint64, 1)[0])
+            assert n == len(want_wal)
+            assert rd.download(lcrc.WAL_REC_DTYPE, n).tobytes() == want_wal.tobytes()
+    finally:
+        eng.graph_destroy(g)
+    eng.close()
