@@ -43,7 +43,7 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", choices=["fixed", "mixed", "wal", "table", "snappy"], default="fixed")
+    p.add_argument("--config", choices=["fixed", "mixed", "wal", "table", "snappy", "seal"], default="fixed")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=1.0, help="wall seconds of the CPU baseline sample")
@@ -285,6 +285,35 @@ def workload_table(m, synth, engs, rank, device):
     return step_on, int(sum(b[1] + 1 for b in blocks)), cfg, None, None
 
 
+def workload_seal(m, synth, engs, rank, device):
+    """Writer-side trailers in batch: the trailer of every block of a 64K x 4 KiB-block
+    SSTable computed over content||type and stored in place (write_raw_block, table.rs:507-529, for a whole
+    flush/compaction output at once); --mode ref gives the reference's crc32fast trailers."""
+    nblk, blen = 65536, 4096
+    f, blocks = synth.table_layout(nblk, blen, seed=synth.SEED_TABLE + rank)
+    dev = m.DeviceBuffer.from_host(f, device)
+    d = np.zeros(len(blocks), m.DESC_DTYPE)
+    d["offset"] = [b[0] for b in blocks]
+    d["length"] = [b[1] + 1 for b in blocks]
+    d["expect_rel"] = [b[1] + 1 for b in blocks]
+    dd = m.DeviceBuffer.from_host(d.view(np.uint8), device)
+    for e in engs:
+        e.reserve(len(f))
+    engs[0].batch_seal(dev, len(f), dd, len(blocks))
+    engs[0].sync()
+    out = np.zeros(len(blocks) + 8, m.TBLK_DTYPE)
+    if engs[0].table_scan_into(dev, len(f), out) != len(blocks) or (out["status"][:len(blocks)] != 0).any():
+        raise RuntimeError("seal bench: the sealed table does not scan clean")
+
+    def step_on(i, eng):  # enqueued: CRCs of every block, stored little-endian in the trailers
+        eng.batch_seal(dev, len(f), dd, len(blocks))
+
+    step_on.graphable = True
+    cfg = {"workload": "writer-side trailers: 64K x 4 KiB blocks of one SSTable sealed in place",
+           "blocks": len(blocks), "file_bytes": int(len(f))}
+    return step_on, int(sum(b[1] + 1 for b in blocks)), cfg, None, None
+
+
 def workload_snappy(m, synth, engs, rank, device):
     """Snappy-framed blocks: 64K frames of one compressed 4 KiB chunk each, decoded and
     every chunk's masked CRC-32C checked on the device. Bytes counted: decoded bytes."""
@@ -374,7 +403,7 @@ def main(argv=None):
         step_on, nbytes, cfg, sample, crcs = workload_host(m, synth, engs, rank, device, args.chunk_mib)
     else:
         step_on, nbytes, cfg, sample, crcs = {"fixed": workload_fixed, "mixed": workload_mixed, "wal": workload_wal,
-                                              "table": workload_table,
+                                              "table": workload_table, "seal": workload_seal,
                                               "snappy": workload_snappy}[args.config](m, synth, engs, rank, device)
 
     def step(i):

@@ -23,6 +23,11 @@ extern "C" {
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
                                uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
                                const uint32_t* expected, uint32_t* mismatch, hipStream_t st);
+hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
+                              const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
+                              const uint32_t* uexp, const uint32_t* gtab, uint32_t x4096, uint32_t poly,
+                              uint32_t init, uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
+                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st);
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
@@ -109,6 +114,8 @@ struct lcrc_ctx {
   hipEvent_t t0 = nullptr, t1 = nullptr;
   uint32_t* d_tab = nullptr;
   uint32_t init = lcrc::CRC_INIT, xorout = lcrc::CRC_XOROUT, fin4096 = 0;
+  uint32_t poly = 0, x4096 = 0;  // this mode's polynomial and x^(8*4096) mod P (k_ranges' chunk shift)
+  int general = 0;  // general path: 0 auto (k_ranges for uniform one-chunk layouts), 1 k_ranges, 2 k_windows + k_blocks
   int grid_a = 256, grid_b = 1024;
   DevBuf<uint32_t> win;       // window partials for the general path
   DevBuf<uint8_t> chunk[2];   // host-resident pipeline staging
@@ -156,6 +163,13 @@ int upload_tables(int mode, uint32_t** d_tab) {
                                  : TAB_ZWIN + (t - 8) * 256;              // Z256, Z512, Z1024
     for (int i = 0; i < 8; ++i) tab[TAB_COLS + t * 8 + i] = tab[src + (1u << i)];
   }
+  // inverses of the zero-byte shifts for k_ranges: x^-1 = (P - 1) / x, i.e. (poly << 1) | 1 reflected
+  const uint32_t xinv = (poly << 1) | 1u;
+  if (lcrc::multmodp(xinv, 1u << 30, poly) != (1u << 31)) return LCRC_EINVAL;  // x * x^-1 == 1
+  uint32_t xinv8 = 1u << 31;
+  for (int i = 0; i < 8; ++i) xinv8 = lcrc::multmodp(xinv8, xinv, poly);
+  tab[TAB_INV] = 1u << 31;
+  for (int k = 1; k <= 4096; ++k) tab[TAB_INV + k] = lcrc::multmodp(tab[TAB_INV + k - 1], xinv8, poly);
   HIPCHK(hipMalloc(d_tab, TAB_TOTAL * sizeof(uint32_t)));
   HIPCHK(hipMemcpy(*d_tab, tab.data(), TAB_TOTAL * sizeof(uint32_t), hipMemcpyHostToDevice));
   return LCRC_OK;
@@ -233,6 +247,9 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   const uint32_t poly = lcrc::poly_of(mode);
   if ((rc = upload_tables(mode, &ctx->d_tab)) != LCRC_OK) return bail(rc);
   ctx->fin4096 = lcrc::zshift(ctx->init, 4096, poly) ^ ctx->xorout;
+  ctx->poly = poly;
+  ctx->x4096 = lcrc::x8n(4096, poly);
+  if (const char* g = getenv("LCRC_GENERAL")) ctx->general = !strcmp(g, "ranges") ? 1 : !strcmp(g, "blocks") ? 2 : 0;
   *out = ctx;
   return LCRC_OK;
 }
@@ -306,6 +323,12 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
   if (out_mismatch && n) HIPCHK(hipMemsetAsync(out_mismatch, 0, ((n + 31) / 32) * sizeof(uint32_t), st));
   if (n == 0) return LCRC_OK;
   const bool direct = (ctx->flags & LCRC_FLAG_DIRECT) != 0;
+  if (!direct && ctx->general == 1) {
+    HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr,
+                              ctx->d_tab, ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
+                              out_crc, out_mismatch, nullptr, nullptr, st));
+    return LCRC_OK;
+  }
   const uint32_t* win = nullptr;
   if (!direct && base_len) {
     if ((rc = ctx->win.ensure(window_words(base_len))) != LCRC_OK) return rc;
@@ -333,6 +356,16 @@ static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint
     return LCRC_OK;
   }
   const uint64_t span = (uint64_t)(n - 1) * stride + length;
+  // k_ranges walks whole 4 KiB chunks: it wins when every range is one well-filled chunk (measured,
+  // tools/probe/ranges_time.py: 4092/4096 B 53 vs 65 us, sparse 4096/8192 B 31 vs 55 us per launch) and
+  // loses on short or multi-chunk ranges (512 B 50 vs 34, 4097 B 91 vs 67, 64 KiB 107 vs 54)
+  const bool one_chunk = length >= 2048 && length + (stride & 3 ? 3u : 0u) <= 4096;
+  if (!(ctx->flags & LCRC_FLAG_DIRECT) && (ctx->general == 1 || (ctx->general == 0 && one_chunk))) {
+    HIPCHK(lcrc_launch_ranges(true, ctx->grid_a, base, span, nullptr, n, stride, length, expected, ctx->d_tab,
+                              ctx->x4096, ctx->poly, ctx->init, ctx->xorout, mflags, out_crc, out_mismatch, nullptr,
+                              nullptr, st));
+    return LCRC_OK;
+  }
   const uint32_t* win = nullptr;
   if (!(ctx->flags & LCRC_FLAG_DIRECT) && span) {
     int rc = ctx->win.ensure(window_words(span));
@@ -461,7 +494,11 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   // walk slowed down ~3x and ended later.)
   HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local,
                                part, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, n_total, n_recs, st));
-  if (max_recs) {
+  if (max_recs && ctx->general == 1) {
+    HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, file, file_len, ctx->wal_descs.p, max_recs, 0, 0, nullptr,
+                              ctx->d_tab, ctx->x4096, ctx->poly, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr,
+                              n_total, (lcrc_wal_rec_dev*)recs, st));
+  } else if (max_recs) {
     HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
                                st));
     HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, file, file_len, ctx->wal_descs.p, max_recs, 0, 0, nullptr,
@@ -523,10 +560,17 @@ static int snappy_run(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* f
   HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
                                    ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], st));
   // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
-  HIPCHK(lcrc_launch_windows(false, ctx->grid_a, out, tot[0], tab_c, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
-  HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, out, tot[0], ctx->sn_cdesc.p, nch, 0, 0, nullptr, ctx->win.p, tab_c,
-                            lcrc::CRC_INIT, lcrc::CRC_XOROUT, LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr, nullptr, nullptr,
-                            st));
+  if (ctx->general == 1) {
+    static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
+    HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, out, tot[0], ctx->sn_cdesc.p, nch, 0, 0, nullptr, tab_c, x4096_c,
+                              lcrc::POLY_C, lcrc::CRC_INIT, lcrc::CRC_XOROUT, LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr,
+                              nullptr, nullptr, st));
+  } else {
+    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, out, tot[0], tab_c, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
+    HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, out, tot[0], ctx->sn_cdesc.p, nch, 0, 0, nullptr, ctx->win.p, tab_c,
+                              lcrc::CRC_INIT, lcrc::CRC_XOROUT, LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr, nullptr,
+                              nullptr, st));
+  }
   HIPCHK(lcrc_launch_snappy_check(ctx->sn_ccrc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, ctx->sn_choff.p + n, nch, status,
                                   st));
   return LCRC_OK;

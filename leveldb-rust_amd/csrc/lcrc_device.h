@@ -18,7 +18,8 @@ enum : int {
   TAB_Z4096 = 9216,   // Z4096
   TAB_COLS = 10240,   // k_windows' LDS image as columns: 20 byte tables x 8 columns (table[1 << i]):
                       // S0 T_p (p = 0..3), S1 Z64[3 - p], then Z256, Z512, Z1024 in TAB_ZWIN word order
-  TAB_TOTAL = 10400,
+  TAB_INV = 10400,    // x^(-8k) mod P for k = 0..4096 (k_ranges: undo the zero padding of a last chunk)
+  TAB_TOTAL = 14500,
 };
 
 struct lcrc_desc_dev {  // == lcrc_desc

@@ -58,6 +58,10 @@ constexpr int A_REP_BYTES = 65536;
 constexpr int A_ZT = A_REP_BYTES;
 constexpr int A_LDS_BYTES = A_ZT + 3 * 4096;
 constexpr int REGION = 16384;  // bytes per wave iteration: two 8 KiB half-tiles, 64 windows of 256 B
+#ifndef LCRC_R_WGCU
+#define LCRC_R_WGCU 2
+#endif
+constexpr int R_WG_PER_CU = LCRC_R_WGCU;  // k_ranges workgroups per CU (no refill pipeline: two resident)
 constexpr uint32_t SET_S1 = 1u << 7;
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt(0)) but not for its
@@ -196,6 +200,7 @@ __device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t 
 // Transpose + walk one half-tile already in registers, starting chain a from register value `init`:
 // returns walk(init, 128 B half of window l). As each register pair is consumed it is refilled from `rs`
 // (the same half of the next region), so every wave keeps between one and two half-tiles in flight.
+template <bool REFILL = true>
 __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4 (&v)[8], uint32_t init,
                                               __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
 #ifndef LCRC_PROBE_NOTRANSPOSE  // ablation build: walk the pieces as loaded (wrong CRCs, timing only)
@@ -230,7 +235,7 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     xb = step4x(L, R, xb, v[4 + j].w);
     xa = step4x(L, R, xa, j < 3 ? v[j + 1].x : 0u);
     xb = step4x(L, R, xb, j < 3 ? v[5 + j].x : 0u);
-    if (j - D >= 0) {
+    if (REFILL && j - D >= 0) {
       v[j - D] = LCRC_REFILL(rs, voff + (j - D) * 2048);
       v[4 + j - D] = LCRC_REFILL(rs, voff + (4 + j - D) * 2048);
     }
@@ -239,6 +244,7 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
   const uint32_t res = zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two quarters
 #pragma unroll
   for (int j = 4 - D; j < 4; ++j) {
+    if (!REFILL) break;
     v[j] = LCRC_REFILL(rs, voff + j * 2048);
     v[4 + j] = LCRC_REFILL(rs, voff + (4 + j) * 2048);
   }
@@ -763,6 +769,188 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
     lcrc_dbg_bstamp[gw * 4 + 3] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------------------------------
+// k_ranges: arbitrary ranges in ONE streaming pass (the general path without k_windows<false> +
+// k_blocks). A range is cut into 4 KiB chunks from its start; a wave walks four chunks at a time, one per
+// 16-lane row and one 256 B window per lane, with k_windows' coalesced loads (load j covers the windows
+// 8j..8j+7, all in row j/2, so each load has a wave-uniform buffer descriptor), transposes, LDS image and
+// row tree. Chunks start on the dword at or below the range start (byte-unaligned vector loads are far
+// slower); the d4 bytes before the range are zeroed (a zero prefix walked from register 0 stays 0) and the
+// start register is injected at byte d4: walk(R0, M) = walk(0, M ^ LE(R0)) for |M| >= 4, which holds for
+// the zero-padded message. The buffer descriptor's range check returns a dword only when it lies wholly
+// below num_records (tools/probe/probe_oob.hip), so past the last whole dword of a range everything reads
+// as zeros and every chunk is a whole 4 KiB unit of M' || 0^z, M' = M without its bytes V in a partial last
+// dword:
+//   acc = C_0;  acc = Z4096(acc) ^ C_k;  walk(R0, M) = acc * x^(-8 pad) mod P  ^  walk(0, V)
+// with pad = nchunks * 4096 - d4 - len (4097 precomputed inverses, one GF(2) multiply) and walk(0, V)
+// three independent slice-table lookups (T_{|V|-1-k}[V_k]). Rows take ranges independently from the workgroup's ticket
+// counter (ranges dealt round-robin over the workgroups), so a long range only holds its own row.
+// ---------------------------------------------------------------------------------------------------
+constexpr uint64_t NO_RANGE = ~0ull;
+
+// a * b mod P, reflected (bit 31 = x^0): zlib's multmodp recurrence without branches
+__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; --i) {
+    p ^= b & (0u - ((a >> i) & 1u));
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+template <bool UNIFORM>
+__global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict__ base, uint64_t base_len,
+                                                     const lcrc_desc_dev* __restrict__ descs, uint64_t n,
+                                                     uint64_t ustride, uint32_t ulen,
+                                                     const uint32_t* __restrict__ uexp,
+                                                     const uint32_t* __restrict__ gtab,
+                                                     const uint32_t* __restrict__ inv, uint32_t x4096,
+                                                     uint32_t poly, uint32_t init, uint32_t xorout,
+                                                     uint32_t flags, uint32_t* __restrict__ out,
+                                                     uint32_t* __restrict__ mismatch,
+                                                     const uint64_t* __restrict__ n_dev,
+                                                     lcrc_wal_rec_dev* __restrict__ recs) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
+  __shared__ uint32_t ticket;
+  const uint32_t lane = __lane_id(), g = lane & 15;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
+  build_tables(L, gtab, wv, lane);
+  if (tid == 0) ticket = 0;
+  lds_barrier();
+  const Rot R = make_rot(lane);
+  const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
+  const __amdgpu_buffer_rsrc_t no_rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0, 0x00020000);
+  // per-row state, uniform within the 16-lane row
+  uint64_t rng = NO_RANGE, cs = 0, e = 0;  // range, next chunk start, range end
+  uint32_t acc = 0, padinv = 0, expv = 0, tail = 0, ntail = 0, d4 = 0;  // tail: bytes of a partial last dword
+  bool first = false, has_exp = false, exp_ok = false, done = false;
+  while (true) {
+    // rows without a range take the next ticket
+    const bool need = rng == NO_RANGE && !done;
+    uint32_t v = 0;
+    if (need && g == 0) v = atomicAdd(&ticket, 1u);
+    v = row_bcast0(v, lane);
+    if (need) {
+      const uint64_t i = blockIdx.x + (uint64_t)v * gridDim.x;
+      if (i >= n) {
+        done = true;
+      } else {
+        uint64_t s;
+        uint32_t len;
+        int32_t xrel = LCRC_NO_EXPECT_DEV;
+        if (UNIFORM) {
+          s = i * ustride;
+          len = ulen;
+        } else {
+          const lcrc_desc_dev d = descs[i];
+          s = d.offset;
+          len = d.length;
+          xrel = d.expect_rel;
+        }
+        rng = i;
+        d4 = (uint32_t)(s & 3);  // chunks start on the dword at or below s: aligned loads
+        cs = s - d4;
+        e = s + len;
+        first = true;
+        const uint32_t span = len + d4;
+        const uint32_t nch = span ? ((span - 1) >> 12) + 1 : 1u;
+        padinv = inv[(uint64_t)nch * 4096 - span];  // pad in [0, 4096]
+        // the range's bytes in a last dword that is not whole read as zeros: walked separately
+        const uint64_t e4 = e & ~3ull;
+        ntail = (uint32_t)(e - (e4 > s ? e4 : s));
+        tail = 0;
+        if (g == 0)
+          for (uint32_t k = 0; k < ntail; ++k)
+            if (e - ntail + k < base_len) tail |= (uint32_t)base[e - ntail + k] << (8 * k);
+        has_exp = false;
+        exp_ok = false;
+        expv = 0;
+        if (UNIFORM) {
+          if (uexp) {
+            has_exp = exp_ok = true;
+            expv = uexp[i];
+          }
+        } else if (xrel != LCRC_NO_EXPECT_DEV && g == 0) {
+          has_exp = true;
+          const int64_t xp = (int64_t)s + xrel;
+          exp_ok = !(xp < 0 || (uint64_t)xp + 4 > base_len);
+          if (exp_ok) expv = load_le32(base + xp);
+        }
+      }
+    }
+    const bool act = rng != NO_RANGE;
+    if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+    // the rows' chunks; bytes past the range (or the buffer) end read as zeros
+    const uint64_t lim = act ? (e < base_len ? e : base_len) : 0;
+    u32x4 va[8], vb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t B = readlane64(cs, 16 * (j >> 1)) + 2048u * (j & 1);
+      const uint64_t lq = readlane64(lim, 16 * (j >> 1));
+      const uint32_t nrec = lq > B ? (lq - B < 2048 ? (uint32_t)(lq - B) : 2048u) : 0u;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(base + (nrec ? B : 0)), (short)0, (int)nrec, 0x00020000);
+      va[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_a, 0, LCRC_LOAD_AUX);
+      vb[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_b, 0, LCRC_LOAD_AUX);
+    }
+    // a first chunk: zero the d4 bytes before the range and inject the start register at byte d4. Before
+    // the transpose, window 0 of row q starts with register va[2q] of lane 0.
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)(first && act ? 1u : 0u), 16 * q);
+      if (f) {
+        const uint32_t dq = (uint32_t)__builtin_amdgcn_readlane((int)d4, 16 * q);
+        const uint64_t sh = (uint64_t)init << (8 * dq);
+        if (lane == 0) {
+          va[2 * q].x = (va[2 * q].x & (~0u << (8 * dq))) ^ (uint32_t)sh;
+          va[2 * q].y ^= (uint32_t)(sh >> 32);
+        }
+      }
+    }
+    const uint32_t x = walk_half<false>(L, R, va, 0u, no_rs, voff_a);
+    uint32_t p = walk_half<false>(L, R, vb, x, no_rs, voff_b);
+    p = tree_level<0>(L, R, p, lane);
+    p = tree_level<1>(L, R, p, lane);
+    p = tree_level<2>(L, R, p, lane);
+    p = tree_level<3>(L, R, p, lane);  // lane 0 of a row: the chunk's register
+    const bool more = act && !first;
+    if (__builtin_amdgcn_ballot_w64(more && g == 0)) {
+      const uint32_t z = gf_mul(x4096, acc, poly);
+      if (more) acc = z ^ p;
+    }
+    if (act && first) acc = p;
+    first = false;
+    cs += 4096;
+    const bool fin = act && cs >= e;
+    if (__builtin_amdgcn_ballot_w64(fin && g == 0)) {
+      uint32_t raw = gf_mul(padinv, acc, poly);
+      // + walk(0, V): slice table T_t at LDS byte 256 * entry + 32 * t (set S0, replica 0)
+      for (uint32_t k = 0; k < ntail; ++k)
+        raw ^= lds_u32(L, ((tail >> (8 * k)) & 255u) * 256u + 32u * (ntail - 1 - k));
+      if (fin && g == 0) {
+        uint32_t crc = raw ^ xorout;
+        if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
+        out[rng] = crc;
+        const bool bad = has_exp && (!exp_ok || expv != crc);
+        if (bad && mismatch) atomicOr(&mismatch[rng >> 5], 1u << (rng & 31));
+        if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
+          recs[rng].crc = crc;
+          recs[rng].status = bad ? 1 : 0;
+        }
+      }
+    }
+    if (fin) rng = NO_RANGE;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1614,6 +1802,27 @@ hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint6
   else
     hipLaunchKernelGGL(lcrc_dev::k_blocks<false>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs,
                        n, ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev, recs);
+  return hipGetLastError();
+}
+
+// general ranges in one pass (k_ranges); `grid` = CUs. inv: 4097 words x^(-8k) mod P (TAB_INV)
+hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
+                              const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
+                              const uint32_t* uexp, const uint32_t* gtab, uint32_t x4096, uint32_t poly,
+                              uint32_t init, uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
+                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  grid *= lcrc_dev::R_WG_PER_CU;
+  const uint64_t per_wg = lcrc_dev::A_THREADS / 16;  // rows per workgroup
+  const uint64_t need = (n + per_wg - 1) / per_wg;
+  const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
+  const uint32_t* inv = gtab + TAB_INV;
+  if (uniform)
+    hipLaunchKernelGGL(lcrc_dev::k_ranges<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, base_len, descs, n,
+                       ustride, ulen, uexp, gtab, inv, x4096, poly, init, xorout, flags, out, mismatch, n_dev, recs);
+  else
+    hipLaunchKernelGGL(lcrc_dev::k_ranges<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, base_len, descs,
+                       n, ustride, ulen, uexp, gtab, inv, x4096, poly, init, xorout, flags, out, mismatch, n_dev, recs);
   return hipGetLastError();
 }
 
