@@ -13,6 +13,10 @@
 //     final (optionally masked, optionally verified) CRC directly.
 //   * k_blocks finishes arbitrary ranges from the window values: each 16-lane row owns one range, walks
 //     its partial head/tail windows from the data, and folds the full windows in between.
+//   * k_ranges does arbitrary ranges in one pass instead: 4 KiB chunks per 16-lane row with k_windows'
+//     loads and walk, zero-padded by the buffer range check, the padding undone by one GF(2) multiply.
+//   * Snappy framing: k_snappy_size (framing walk), k_snappy_decode_wave (one wave per frame, LDS-staged,
+//     data-parallel element parse), k_snappy_check; table scan: k_idx_parse, k_tbl_finish, k_tbl_content.
 //   * k_wal_parse walks the 7-byte headers of every 32 KiB log block (src/db/log.rs:204-279) into
 //     record descriptors for k_blocks.
 #include <hip/hip_runtime.h>
