@@ -129,7 +129,8 @@ int lcrc_ctx_sync(lcrc_ctx* ctx);
 /* CRC of n ranges of the device buffer base[0, base_len). out_crc[i] (device) gets the CRC (masked if
  * LCRC_FLAG_MASK). out_mismatch (device, nullable, ceil(n/32) u32 words, zeroed by the call) gets bit i
  * set when descriptor i has an expected value and it differs. Ranges may be in any order and may
- * overlap; every byte of [0, base_len) is streamed once unless LCRC_FLAG_DIRECT is given. */
+ * overlap; every byte of [0, base_len) is streamed once unless LCRC_FLAG_DIRECT is given. A range that
+ * does not lie inside [0, base_len) is never read: its CRC is 0 and its mismatch bit is set. */
 int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
                uint32_t* out_crc, uint32_t* out_mismatch, void* stream);
 

@@ -54,7 +54,7 @@ hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t
                                   const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st);
 hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
-hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
+hipError_t lcrc_launch_store_crc(uint8_t* base, uint64_t base_len, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
 }
 
@@ -944,7 +944,7 @@ int lcrc_batch_seal(lcrc_ctx* ctx, uint8_t* base, uint64_t base_len, const lcrc_
     crc = ctx->tbl_crcs.p;
   }
   if ((rc = lcrc_batch(ctx, base, base_len, descs, n, crc, nullptr, st))) return rc;
-  HIPCHK(lcrc_launch_store_crc(base, (const lcrc_desc_dev*)descs, crc, n, st));
+  HIPCHK(lcrc_launch_store_crc(base, base_len, (const lcrc_desc_dev*)descs, crc, n, st));
   return LCRC_OK;
 }
 

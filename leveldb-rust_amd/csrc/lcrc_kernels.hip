@@ -629,10 +629,12 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
   const uint64_t nwaves = (uint64_t)gridDim.x * (B_THREADS / 64);
   const bool use_win = win != nullptr;
   // descriptors are loaded one iteration ahead of their use (the first one before the table fill)
-  auto load_desc = [&](uint64_t i, uint64_t& s, uint32_t& len, int32_t& xrel) {
+  // a range outside [0, base_len) is never read: it becomes empty, CRC 0, and is flagged as a mismatch
+  auto load_desc = [&](uint64_t i, uint64_t& s, uint32_t& len, int32_t& xrel, bool& oob) {
     s = 0;
     len = 0;
     xrel = LCRC_NO_EXPECT_DEV;
+    oob = false;
     if (i < n) {
       if (UNIFORM) {
         s = i * ustride;
@@ -642,13 +644,19 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
         s = d.offset;
         len = d.length;
         xrel = d.expect_rel;
+        if (s > base_len || len > base_len - s) {
+          oob = true;
+          s = 0;
+          len = 0;
+        }
       }
     }
   };
   uint64_t s_nx;
   uint32_t len_nx;
   int32_t xrel_nx;
-  load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx);
+  bool oob_nx;
+  load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx, oob_nx);
   for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS)
     ((u32x4*)L)[i] = ((const u32x4*)gtab)[i];
   __syncthreads();
@@ -662,7 +670,8 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
     const uint64_t s = s_nx;
     const uint32_t len = len_nx;
     const int32_t xrel = xrel_nx;
-    load_desc(i + nwaves * 4, s_nx, len_nx, xrel_nx);
+    const bool oob = oob_nx;
+    load_desc(i + nwaves * 4, s_nx, len_nx, xrel_nx, oob_nx);
     const uint64_t e = s + len;
     // the expected value, loaded with the data (bytewise: any alignment, and checked against the buffer)
     uint32_t expv = 0;
@@ -683,10 +692,12 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       const uint64_t wfull = ((e & 255) == 0) ? wl : wl - 1;
       // middle: virtual items [pad zeros..., head, win[ws+1 .. wfull]] folded 16 per round (Horner
       // with Z4096 per lane, then a 4-level tree)
-      const uint64_t items = single ? 0 : (wfull - ws) + 1;  // head + full windows
-      const uint64_t npad = (16 - (items & 15)) & 15;
-      const uint64_t rounds = single ? 0 : (npad + items) >> 4;
-      const uint32_t rr32 = (uint32_t)rounds;
+      const uint32_t items = single ? 0u : (uint32_t)(wfull - ws) + 1;  // head + full windows (< 2^24)
+      const uint32_t npad = (16 - (items & 15)) & 15;
+      const uint32_t rounds = single ? 0u : (npad + items) >> 4;
+      const uint32_t rr32 = rounds;
+      // lane g's window value of round q is wv[16 q] (the slots before the head are padding)
+      const uint32_t* wv = win + ws + g - npad;
       const uint32_t rmax = max(max(__builtin_amdgcn_readlane(rr32, 0), __builtin_amdgcn_readlane(rr32, 16)),
                                 max(__builtin_amdgcn_readlane(rr32, 32), __builtin_amdgcn_readlane(rr32, 48)));
 
@@ -695,10 +706,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       const RowPiece pt = row_load(base, ta, e, g);
       uint32_t vals[B_BATCH];
 #pragma unroll
-      for (int j = 0; j < B_BATCH; ++j) {
-        const uint64_t u = 16 * (uint64_t)j + g;
-        vals[j] = ((uint32_t)j < rounds && u > npad) ? win[ws + (u - npad)] : 0u;
-      }
+      for (int j = 0; j < B_BATCH; ++j) vals[j] = ((uint32_t)j < rounds && 16u * j + g > npad) ? wv[16 * j] : 0u;
 
       const uint32_t head = row_walk(L, ph, s == head_end, init, g, lane);
       uint32_t a = 0;
@@ -706,14 +714,14 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
         if (q0) {
 #pragma unroll
           for (int j = 0; j < B_BATCH; ++j) {
-            const uint64_t q = q0 + j, u = 16 * q + g;
-            vals[j] = (q < rounds && u > npad) ? win[ws + (u - npad)] : 0u;
+            const uint32_t q = q0 + j;
+            vals[j] = (q < rounds && 16u * q + g > npad) ? wv[16 * q] : 0u;
           }
         }
 #pragma unroll
         for (int j = 0; j < B_BATCH; ++j) {
-          const uint64_t q = q0 + j;
-          if (q < rounds) a = zl(L, TAB_Z4096, a) ^ (16 * q + g == npad ? head : vals[j]);
+          const uint32_t q = q0 + j;
+          if (q < rounds) a = zl(L, TAB_Z4096, a) ^ (16u * q + g == npad ? head : vals[j]);
         }
       }
 #pragma unroll
@@ -747,12 +755,13 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
     if (valid && g == 0) {
       uint32_t crc = acc ^ xorout;
       if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
+      if (oob) crc = 0;
       out[i] = crc;
-      bool bad = false;
+      bool bad = oob;
       if (UNIFORM) {
         if (uexp) bad = uexp[i] != crc;
       } else if (xrel != LCRC_NO_EXPECT_DEV) {
-        bad = !exp_ok || expv != crc;
+        bad = bad || !exp_ok || expv != crc;
       }
       if (bad && mismatch) atomicOr(&mismatch[i >> 5], 1u << (i & 31));
       if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
@@ -837,7 +846,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
   // per-row state, uniform within the 16-lane row
   uint64_t rng = NO_RANGE, cs = 0, e = 0;  // range, next chunk start, range end
   uint32_t acc = 0, padinv = 0, expv = 0, tail = 0, ntail = 0, d4 = 0;  // tail: bytes of a partial last dword
-  bool first = false, has_exp = false, exp_ok = false, done = false;
+  bool first = false, has_exp = false, exp_ok = false, done = false, oob = false;
   while (true) {
     // rows without a range take the next ticket
     const bool need = rng == NO_RANGE && !done;
@@ -852,6 +861,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
         uint64_t s;
         uint32_t len;
         int32_t xrel = LCRC_NO_EXPECT_DEV;
+        oob = false;
         if (UNIFORM) {
           s = i * ustride;
           len = ulen;
@@ -860,6 +870,11 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
           s = d.offset;
           len = d.length;
           xrel = d.expect_rel;
+          if (s > base_len || len > base_len - s) {  // never read: empty, CRC 0, flagged as a mismatch
+            oob = true;
+            s = 0;
+            len = 0;
+          }
         }
         rng = i;
         d4 = (uint32_t)(s & 3);  // chunks start on the dword at or below s: aligned loads
@@ -944,8 +959,9 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
       if (fin && g == 0) {
         uint32_t crc = raw ^ xorout;
         if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
+        if (oob) crc = 0;
         out[rng] = crc;
-        const bool bad = has_exp && (!exp_ok || expv != crc);
+        const bool bad = oob || (has_exp && (!exp_ok || expv != crc));
         if (bad && mismatch) atomicOr(&mismatch[rng >> 5], 1u << (rng & 31));
         if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
           recs[rng].crc = crc;
@@ -1722,13 +1738,16 @@ __global__ void __launch_bounds__(256) k_gather_u8(const uint8_t* __restrict__ b
 
 // base[offset_i + expect_rel_i .. +4) = crc_i, little-endian: the trailer of write_raw_block
 // (table.rs:519-527) or the header checksum of emit_physical_record (log.rs:61-70), in place
-__global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, const lcrc_desc_dev* __restrict__ descs,
+__global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, uint64_t base_len,
+                                                   const lcrc_desc_dev* __restrict__ descs,
                                                    const uint32_t* __restrict__ crc, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const lcrc_desc_dev d = descs[i];
   if (d.expect_rel == LCRC_NO_EXPECT_DEV) return;
-  uint8_t* p = base + (int64_t)d.offset + d.expect_rel;
+  const int64_t at = (int64_t)d.offset + d.expect_rel;
+  if (d.offset > base_len || at < 0 || (uint64_t)at + 4 > base_len) return;  // never written outside the buffer
+  uint8_t* p = base + at;
   const uint32_t c = crc[i];
   p[0] = (uint8_t)c;
   p[1] = (uint8_t)(c >> 8);
@@ -1923,10 +1942,11 @@ hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint6
   return hipGetLastError();
 }
 
-hipError_t lcrc_launch_store_crc(uint8_t* base, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
+hipError_t lcrc_launch_store_crc(uint8_t* base, uint64_t base_len, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_store_crc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, descs, crc, n);
+  hipLaunchKernelGGL(lcrc_dev::k_store_crc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, base_len, descs,
+                     crc, n);
   return hipGetLastError();
 }
 

@@ -380,3 +380,32 @@ def test_general_path_variants(lcrc, orc, path, monkeypatch):
     assert (got["status"] == 0).all()
     assert [int(c) for c in got["crc"]] == [orc.crc(log[h + 6:h + 7 + n], 0) for h, n, _ in want]
     eng.close()
+
+
+@pytest.mark.parametrize("path", ["ranges", "blocks"])
+def test_out_of_bounds_descriptors(lcrc, orc, path, monkeypatch):
+    """A range outside [0, base_len) is never read: CRC 0 and its mismatch bit set; in-bounds neighbours are
+    unaffected. The in-place store of lcrc_batch_seal never writes outside the buffer either."""
+    monkeypatch.setenv("LCRC_GENERAL", path)
+    data = bytes(orc.splitmix_bytes(99, 1 << 20))
+    n0 = len(data)
+    offs = np.array([0, 100, n0 - 10, n0, n0 + 5, 2 ** 40, 5000], np.uint64)
+    lens = np.array([4096, 300, 10, 0, 1, 16, 70000], np.uint32)
+    ok = (offs <= n0) & (lens.astype(np.uint64) <= n0 - np.minimum(offs, n0))
+    eng = lcrc.Engine(0, lcrc.MODE_C)
+    crcs, mm = eng.crc_ranges(data, offs, lens)
+    want = orc.crc_ranges(data, offs[ok], lens[ok], 1)
+    assert np.array_equal(crcs[ok], want)
+    assert (crcs[~ok] == 0).all()
+    assert mm.tolist() == (~ok).tolist()
+    # seal: the expected-value slot of descriptor 1 lies past the end -> not written
+    buf = lcrc.DeviceBuffer.from_host(np.frombuffer(data, np.uint8))
+    d = np.zeros(2, lcrc.DESC_DTYPE)
+    d["offset"], d["length"], d["expect_rel"] = [0, n0 - 8], [64, 8], [64, 6]
+    dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8))
+    eng.batch_seal(buf, n0, dd, 2)
+    eng.sync()
+    after = buf.download(np.uint8, n0).tobytes()
+    assert after[:64] == data[:64] and after[68:] == data[68:]
+    assert int.from_bytes(after[64:68], "little") == orc.crc(data[:64], 1)
+    eng.close()
