@@ -336,7 +336,11 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
                                st));
     win = ctx->win.p;
   }
-  HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / 2, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
+#ifndef LCRC_BATCH_GRID_DIV
+#define LCRC_BATCH_GRID_DIV 2  // half the grid: a full one cuts config 3 k_blocks alone 22.0 -> 18.0 us but
+                               // crowds a concurrent batch on another stream (2-stream wall 4.1-4.3K -> 3.8K GiB/s)
+#endif
+  HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_BATCH_GRID_DIV, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
                             ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK, out_crc,
                             out_mismatch, nullptr, nullptr, st));
   return LCRC_OK;
