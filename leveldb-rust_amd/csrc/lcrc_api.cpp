@@ -170,6 +170,9 @@ int upload_tables(int mode, uint32_t** d_tab) {
   for (int i = 0; i < 8; ++i) xinv8 = lcrc::multmodp(xinv8, xinv, poly);
   tab[TAB_INV] = 1u << 31;
   for (int k = 1; k <= 4096; ++k) tab[TAB_INV + k] = lcrc::multmodp(tab[TAB_INV + k - 1], xinv8, poly);
+  const uint32_t x4096 = lcrc::x8n(4096, poly);
+  tab[TAB_XCH] = 1u << 31;
+  for (int k = 1; k < 4096; ++k) tab[TAB_XCH + k] = lcrc::multmodp(tab[TAB_XCH + k - 1], x4096, poly);
   HIPCHK(hipMalloc(d_tab, TAB_TOTAL * sizeof(uint32_t)));
   HIPCHK(hipMemcpy(*d_tab, tab.data(), TAB_TOTAL * sizeof(uint32_t), hipMemcpyHostToDevice));
   return LCRC_OK;

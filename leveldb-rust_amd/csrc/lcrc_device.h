@@ -19,7 +19,8 @@ enum : int {
   TAB_COLS = 10240,   // k_windows' LDS image as columns: 20 byte tables x 8 columns (table[1 << i]):
                       // S0 T_p (p = 0..3), S1 Z64[3 - p], then Z256, Z512, Z1024 in TAB_ZWIN word order
   TAB_INV = 10400,    // x^(-8k) mod P for k = 0..4096 (k_ranges: undo the zero padding of a last chunk)
-  TAB_TOTAL = 14500,
+  TAB_XCH = 14497,    // x^(8 * 4096 * k) mod P for k = 0..4095 (k_ranges: place a shared range's chunk)
+  TAB_TOTAL = 18600,
 };
 
 struct lcrc_desc_dev {  // == lcrc_desc

@@ -801,7 +801,8 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 // three independent slice-table lookups (T_{|V|-1-k}[V_k]). Rows take ranges independently from the workgroup's ticket
 // counter (ranges dealt round-robin over the workgroups), so a long range only holds its own row.
 // ---------------------------------------------------------------------------------------------------
-constexpr uint64_t NO_RANGE = ~0ull;
+constexpr uint32_t R_SLOTS = 32;    // ranges shared by the rows of a workgroup at a time
+constexpr uint32_t R_KMAX = 4096;   // chunks of a shared range (x^(8 * 4096 * k) table); longer: private
 
 // a * b mod P, reflected (bit 31 = x^0): zlib's multmodp recurrence without branches
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
@@ -832,28 +833,71 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
                                                      const uint64_t* __restrict__ n_dev,
                                                      lcrc_wal_rec_dev* __restrict__ recs) {
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
-  __shared__ uint32_t ticket;
+  __shared__ uint32_t ticket, work_mask, free_mask;
+  // shared ranges (more than one chunk): chunks claimed by any row of the workgroup, their registers
+  // shifted into place and xored into the slot, the row completing the last chunk finishes the range.
+  // next / info carry a generation in bits 16+ so a claim that raced with the slot's reuse is recognised.
+  __shared__ uint32_t sl_next[R_SLOTS], sl_info[R_SLOTS], sl_left[R_SLOTS], sl_acc[R_SLOTS], sl_gen[R_SLOTS];
+  __shared__ uint32_t sl_rng[R_SLOTS], sl_padinv[R_SLOTS], sl_tail[R_SLOTS], sl_meta[R_SLOTS], sl_expv[R_SLOTS];
+  __shared__ uint64_t sl_cs0[R_SLOTS], sl_e[R_SLOTS];
   const uint32_t lane = __lane_id(), g = lane & 15;
   const uint32_t tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t* __restrict__ xch = inv + 4097;  // x^(8 * 4096 * k) mod P, k < R_KMAX
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
   build_tables(L, gtab, wv, lane);
-  if (tid == 0) ticket = 0;
+  if (tid < R_SLOTS) sl_gen[tid] = 0;
+  if (tid == 0) {
+    ticket = 0;
+    work_mask = 0;
+    free_mask = R_SLOTS == 32 ? ~0u : (1u << R_SLOTS) - 1;
+  }
   lds_barrier();
   const Rot R = make_rot(lane);
   const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
   const __amdgpu_buffer_rsrc_t no_rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0, 0x00020000);
-  // per-row state, uniform within the 16-lane row
-  uint64_t rng = NO_RANGE, cs = 0, e = 0;  // range, next chunk start, range end
+  // per-row state, uniform within the 16-lane row. mode 0: looking for work, 1: a private range (chunks
+  // walked in order by this row), 2: one chunk of shared range `sl`.
+  uint32_t mode = 0, sl = 0, xk = 0;
+  uint64_t rng = 0, cs = 0, e = 0;  // range, chunk start, range end
   uint32_t acc = 0, padinv = 0, expv = 0, tail = 0, ntail = 0, d4 = 0;  // tail: bytes of a partial last dword
   bool first = false, has_exp = false, exp_ok = false, done = false, oob = false;
   while (true) {
-    // rows without a range take the next ticket
-    const bool need = rng == NO_RANGE && !done;
+    // 1. rows without work claim a chunk of a shared range ...
+    const bool need = mode == 0 && !done;
+    uint32_t got = R_SLOTS, gc = 0;
+    if (need && g == 0) {
+      uint32_t m = *(volatile uint32_t*)&work_mask;
+      while (m) {
+        const uint32_t s = __builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t r = atomicAdd(&sl_next[s], 1u);
+        const uint32_t info = *(volatile uint32_t*)&sl_info[s];
+        if ((r >> 16) == (info >> 16) && (r & 0xFFFFu) < (info & 0xFFFFu)) {
+          if ((r & 0xFFFFu) == (info & 0xFFFFu) - 1) atomicAnd(&work_mask, ~(1u << s));  // the last chunk
+          got = s;
+          gc = r & 0xFFFFu;
+          break;
+        }
+      }
+    }
+    got = row_bcast0(got, lane);
+    gc = row_bcast0(gc, lane);
+    if (need && got < R_SLOTS) {
+      mode = 2;
+      sl = got;
+      const uint32_t nch = sl_info[sl] & 0xFFFFu;
+      cs = sl_cs0[sl] + 4096ull * gc;
+      e = sl_e[sl];
+      first = false;  // chunk 0 is walked by the row that shared the range
+      xk = xch[nch - 1 - gc];
+    }
+    // ... or take the next range
+    const bool need2 = need && got >= R_SLOTS;
     uint32_t v = 0;
-    if (need && g == 0) v = atomicAdd(&ticket, 1u);
+    if (need2 && g == 0) v = atomicAdd(&ticket, 1u);
     v = row_bcast0(v, lane);
-    if (need) {
+    if (need2) {
       const uint64_t i = blockIdx.x + (uint64_t)v * gridDim.x;
       if (i >= n) {
         done = true;
@@ -905,16 +949,56 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
           exp_ok = !(xp < 0 || (uint64_t)xp + 4 > base_len);
           if (exp_ok) expv = load_le32(base + xp);
         }
+        mode = 1;
+        // share a range of several chunks through a free slot (a range past R_KMAX chunks stays private)
+        uint32_t slot = R_SLOTS;
+        if (g == 0 && nch > 1 && nch <= R_KMAX) {
+          uint32_t fm = *(volatile uint32_t*)&free_mask;
+          while (fm) {
+            const uint32_t b = __builtin_ctz(fm);
+            const uint32_t old = atomicAnd(&free_mask, ~(1u << b));
+            if (old & (1u << b)) {
+              slot = b;
+              break;
+            }
+            fm = old & ~(1u << b);
+          }
+          if (slot < R_SLOTS) {
+            const uint32_t gen = (sl_gen[slot] + 1) & 0xFFFFu;
+            sl_gen[slot] = gen;
+            sl_rng[slot] = (uint32_t)i;
+            sl_cs0[slot] = cs;
+            sl_e[slot] = e;
+            sl_padinv[slot] = padinv;
+            sl_tail[slot] = tail;
+            sl_expv[slot] = expv;
+            sl_meta[slot] = ntail | (has_exp ? 0x100u : 0u) | (exp_ok ? 0x200u : 0u) | (oob ? 0x400u : 0u);
+            sl_acc[slot] = 0;
+            sl_left[slot] = nch;
+            sl_info[slot] = (gen << 16) | nch;
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // fields before the claim counter, counter before the bit
+            sl_next[slot] = (gen << 16) | 1u;  // chunk 0 is this row's
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            atomicOr(&work_mask, 1u << slot);
+          }
+        }
+        slot = row_bcast0(slot, lane);
+        if (slot < R_SLOTS) {
+          mode = 2;
+          sl = slot;
+          xk = xch[nch - 1];
+        }
       }
     }
-    const bool act = rng != NO_RANGE;
+    const bool act = mode != 0;
     if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-    // the rows' chunks; bytes past the range (or the buffer) end read as zeros
+    // 2. the rows' chunks; bytes past the range (or the buffer) end read as zeros
     const uint64_t lim = act ? (e < base_len ? e : base_len) : 0;
+    const uint64_t csl = act ? cs : 0;
     u32x4 va[8], vb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint64_t B = readlane64(cs, 16 * (j >> 1)) + 2048u * (j & 1);
+      const uint64_t B = readlane64(csl, 16 * (j >> 1)) + 2048u * (j & 1);
       const uint64_t lq = readlane64(lim, 16 * (j >> 1));
       const uint32_t nrec = lq > B ? (lq - B < 2048 ? (uint32_t)(lq - B) : 2048u) : 0u;
       const __amdgpu_buffer_rsrc_t rs =
@@ -922,8 +1006,8 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
       va[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_a, 0, LCRC_LOAD_AUX);
       vb[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_b, 0, LCRC_LOAD_AUX);
     }
-    // a first chunk: zero the d4 bytes before the range and inject the start register at byte d4. Before
-    // the transpose, window 0 of row q starts with register va[2q] of lane 0.
+    // a range's first chunk: zero the d4 bytes before the range and inject the start register at byte
+    // d4. Before the transpose, window 0 of row q starts with register va[2q] of lane 0.
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)(first && act ? 1u : 0u), 16 * q);
@@ -942,15 +1026,42 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
     p = tree_level<1>(L, R, p, lane);
     p = tree_level<2>(L, R, p, lane);
     p = tree_level<3>(L, R, p, lane);  // lane 0 of a row: the chunk's register
-    const bool more = act && !first;
-    if (__builtin_amdgcn_ballot_w64(more && g == 0)) {
-      const uint32_t z = gf_mul(x4096, acc, poly);
+    // 3. combine. Private: acc = Z4096(acc) ^ C. Shared: slot ^= Z_{4096 (nch - 1 - c)}(C).
+    const bool more = mode == 1 && !first;
+    const bool shr = mode == 2;
+    if (__builtin_amdgcn_ballot_w64((more || shr) && g == 0)) {
+      const uint32_t z = gf_mul(shr ? xk : x4096, shr ? p : acc, poly);
       if (more) acc = z ^ p;
+      if (shr) p = z;
     }
-    if (act && first) acc = p;
+    if (mode == 1 && first) acc = p;
     first = false;
-    cs += 4096;
-    const bool fin = act && cs >= e;
+    bool fin = false;
+    if (mode == 1) {
+      cs += 4096;
+      fin = cs >= e;
+    }
+    uint32_t fin_slot = R_SLOTS;
+    if (shr && g == 0) {
+      atomicXor(&sl_acc[sl], p);
+      if (atomicSub(&sl_left[sl], 1u) == 1u) fin_slot = sl;  // the range's last chunk: finish it here
+    }
+    fin_slot = row_bcast0(fin_slot, lane);
+    if (shr && fin_slot < R_SLOTS) {
+      fin = true;
+      acc = *(volatile uint32_t*)&sl_acc[fin_slot];
+      rng = sl_rng[fin_slot];
+      padinv = sl_padinv[fin_slot];
+      tail = sl_tail[fin_slot];
+      expv = sl_expv[fin_slot];
+      const uint32_t meta = sl_meta[fin_slot];
+      ntail = meta & 0xFFu;
+      has_exp = meta & 0x100u;
+      exp_ok = meta & 0x200u;
+      oob = meta & 0x400u;
+    }
+    if (shr) mode = 0;
+    // 4. finish: register = acc * x^(-8 pad) ^ walk(0, V)
     if (__builtin_amdgcn_ballot_w64(fin && g == 0)) {
       uint32_t raw = gf_mul(padinv, acc, poly);
       // + walk(0, V): slice table T_t at LDS byte 256 * entry + 32 * t (set S0, replica 0)
@@ -967,9 +1078,10 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
           recs[rng].crc = crc;
           recs[rng].status = bad ? 1 : 0;
         }
+        if (fin_slot < R_SLOTS) atomicOr(&free_mask, 1u << fin_slot);  // the slot's fields are read
       }
     }
-    if (fin) rng = NO_RANGE;
+    if (fin) mode = 0;
   }
 }
 
