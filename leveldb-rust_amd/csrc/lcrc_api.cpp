@@ -366,6 +366,7 @@ static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint
   // k_ranges walks whole 4 KiB chunks: it wins when every range is one well-filled chunk (measured,
   // tools/probe/ranges_time.py: 4092/4096 B 53 vs 65 us, sparse 4096/8192 B 31 vs 55 us per launch) and
   // loses on short or multi-chunk ranges (512 B 50 vs 34, 4097 B 91 vs 67, 64 KiB 107 vs 54)
+  // (a range just past one chunk -- 4,097 B blocks -- walks its last bytes on at the end: 71 vs 67 us, kept out)
   const bool one_chunk = length >= 2048 && length + (stride & 3 ? 3u : 0u) <= 4096;
   if (!(ctx->flags & LCRC_FLAG_DIRECT) && (ctx->general == 1 || (ctx->general == 0 && one_chunk))) {
     HIPCHK(lcrc_launch_ranges(true, ctx->grid_a, base, span, nullptr, n, stride, length, expected, ctx->d_tab,

@@ -803,6 +803,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 // ---------------------------------------------------------------------------------------------------
 constexpr uint32_t R_SLOTS = 32;    // ranges shared by the rows of a workgroup at a time
 constexpr uint32_t R_KMAX = 4096;   // chunks of a shared range (x^(8 * 4096 * k) table); longer: private
+constexpr uint32_t R_OVF = 16;      // bytes past one full chunk walked at the end instead of a second chunk
 
 // a * b mod P, reflected (bit 31 = x^0): zlib's multmodp recurrence without branches
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
@@ -859,8 +860,10 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
   // per-row state, uniform within the 16-lane row. mode 0: looking for work, 1: a private range (chunks
   // walked in order by this row), 2: one chunk of shared range `sl`.
   uint32_t mode = 0, sl = 0, xk = 0;
-  uint64_t rng = 0, cs = 0, e = 0;  // range, chunk start, range end
+  uint64_t rng = 0, cs = 0, e = 0, ce = 0;  // range, chunk start, range end, end of its chunked part
   uint32_t acc = 0, padinv = 0, expv = 0, tail = 0, ntail = 0, d4 = 0;  // tail: bytes of a partial last dword
+  uint32_t ovn = 0, ov0 = 0, ov1 = 0, ov2 = 0, ov3 = 0;  // whole dwords past a range's one full chunk
+  bool ovf = false;  // the range's bytes past its one full chunk are walked on at the end
   bool first = false, has_exp = false, exp_ok = false, done = false, oob = false;
   while (true) {
     // 1. rows without work claim a chunk of a shared range ...
@@ -889,6 +892,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
       const uint32_t nch = sl_info[sl] & 0xFFFFu;
       cs = sl_cs0[sl] + 4096ull * gc;
       e = sl_e[sl];
+      ce = e;
       first = false;  // chunk 0 is walked by the row that shared the range
       xk = xch[nch - 1 - gc];
     }
@@ -926,8 +930,21 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
         e = s + len;
         first = true;
         const uint32_t span = len + d4;
-        const uint32_t nch = span ? ((span - 1) >> 12) + 1 : 1u;
-        padinv = inv[(uint64_t)nch * 4096 - span];  // pad in [0, 4096]
+        // a range just past one chunk (a 4 KiB block and its type byte): one full chunk, the <= 16 bytes
+        // after it walked on from the chunk's register at the end
+        ovf = span > 4096 && span <= 4096 + R_OVF;
+        const uint32_t nch = ovf ? 1u : span ? ((span - 1) >> 12) + 1 : 1u;
+        padinv = inv[ovf ? 0 : (uint64_t)nch * 4096 - span];  // pad in [0, 4096]
+        ce = ovf ? cs + 4096 : e;
+        ovn = ovf ? (span - 4096) >> 2 : 0u;
+        ov0 = ov1 = ov2 = ov3 = 0;
+        if (ovn && g == 0) {
+          const uint32_t* ow = (const uint32_t*)(base + cs + 4096);  // dword-aligned like cs
+          ov0 = ow[0];
+          if (ovn > 1) ov1 = ow[1];
+          if (ovn > 2) ov2 = ow[2];
+          if (ovn > 3) ov3 = ow[3];
+        }
         // the range's bytes in a last dword that is not whole read as zeros: walked separately
         const uint64_t e4 = e & ~3ull;
         ntail = (uint32_t)(e - (e4 > s ? e4 : s));
@@ -993,7 +1010,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
     const bool act = mode != 0;
     if (__builtin_amdgcn_ballot_w64(act) == 0) break;
     // 2. the rows' chunks; bytes past the range (or the buffer) end read as zeros
-    const uint64_t lim = act ? (e < base_len ? e : base_len) : 0;
+    const uint64_t lim = act ? (ce < base_len ? ce : base_len) : 0;
     const uint64_t csl = act ? cs : 0;
     u32x4 va[8], vb[8];
 #pragma unroll
@@ -1039,7 +1056,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
     bool fin = false;
     if (mode == 1) {
       cs += 4096;
-      fin = cs >= e;
+      fin = cs >= ce;
     }
     uint32_t fin_slot = R_SLOTS;
     if (shr && g == 0) {
@@ -1059,14 +1076,26 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
       has_exp = meta & 0x100u;
       exp_ok = meta & 0x200u;
       oob = meta & 0x400u;
+      ovn = 0;
+      ovf = false;
     }
     if (shr) mode = 0;
     // 4. finish: register = acc * x^(-8 pad) ^ walk(0, V)
     if (__builtin_amdgcn_ballot_w64(fin && g == 0)) {
       uint32_t raw = gf_mul(padinv, acc, poly);
-      // + walk(0, V): slice table T_t at LDS byte 256 * entry + 32 * t (set S0, replica 0)
-      for (uint32_t k = 0; k < ntail; ++k)
-        raw ^= lds_u32(L, ((tail >> (8 * k)) & 255u) * 256u + 32u * (ntail - 1 - k));
+      // slice table T_t at LDS byte 256 * entry + 32 * t (set S0, replica 0)
+      if (ovf) {  // walk on over the dwords and bytes past the full chunk
+        for (uint32_t k = 0; k < ovn; ++k) {
+          const uint32_t xw = raw ^ (k == 0 ? ov0 : k == 1 ? ov1 : k == 2 ? ov2 : ov3);
+          raw = lds_u32(L, (xw & 255u) * 256u + 96u) ^ lds_u32(L, ((xw >> 8) & 255u) * 256u + 64u) ^
+                lds_u32(L, ((xw >> 16) & 255u) * 256u + 32u) ^ lds_u32(L, (xw >> 24) * 256u);
+        }
+        for (uint32_t k = 0; k < ntail; ++k)
+          raw = (raw >> 8) ^ lds_u32(L, ((raw ^ (tail >> (8 * k))) & 255u) * 256u);
+      } else {  // + walk(0, V)
+        for (uint32_t k = 0; k < ntail; ++k)
+          raw ^= lds_u32(L, ((tail >> (8 * k)) & 255u) * 256u + 32u * (ntail - 1 - k));
+      }
       if (fin && g == 0) {
         uint32_t crc = raw ^ xorout;
         if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
