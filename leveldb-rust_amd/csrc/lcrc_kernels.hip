@@ -373,10 +373,10 @@ __device__ __forceinline__ void build_tables(uint32_t* L, const uint32_t* __rest
 }
 
 #ifdef LCRC_PROBE_CLOCK  // diagnostic build: per-workgroup shader/real clock stamps around the tile loop
-__device__ unsigned long long lcrc_dbg_clock[4096];
-__device__ unsigned long long lcrc_dbg_stamp[4096 * 8];
-__device__ unsigned long long lcrc_dbg_bstamp[8192 * 4];  // k_blocks per wave: entry, tables, first range, end  // per wave: entry, tables ready, first half, end,
-                                                         // table source loaded, staged
+__device__ unsigned long long lcrc_dbg_clock[4096];   // k_windows per workgroup: shader and real clock
+__device__ unsigned long long lcrc_dbg_stamp[4096 * 8];  // k_windows per wave: entry, tables ready, first half,
+                                                        // end, table source loaded, staged, HW_ID, XCC_ID
+__device__ unsigned long long lcrc_dbg_bstamp[8192 * 4];  // k_blocks per wave: entry, tables, first range, end
 #endif
 
 template <bool FINAL>
