@@ -851,7 +851,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
   if (tid == 0) {
     ticket = 0;
     work_mask = 0;
-    free_mask = R_SLOTS == 32 ? ~0u : (1u << R_SLOTS) - 1;
+    free_mask = ~0u >> (32 - R_SLOTS);
   }
   lds_barrier();
   const Rot R = make_rot(lane);
