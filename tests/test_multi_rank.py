@@ -1,4 +1,4 @@
-"""N>1 path on the CPU: two gloo ranks through bench.py's barrier / max-over-ranks / aggregate logic, each on
+"""N>1 path on the CPU: 2 and 4 gloo ranks through bench.py's barrier / max-over-ranks / aggregate logic, each on
 an independent shard (the path shards with no data-path collective)."""
 import json
 import os
@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -19,20 +20,21 @@ def _free_port():
     return p
 
 
-def test_two_rank_gloo(orc, synth, tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_multi_rank_gloo(orc, synth, tmp_path, world):
     env = dict(os.environ, OMP_NUM_THREADS="1", LCRC_DIST_OUT=str(tmp_path))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tests", "_dist_worker.py")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
-    rows = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(2)]
-    assert sorted(x["rank"] for x in rows) == [0, 1]
+    rows = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
+    assert sorted(x["rank"] for x in rows) == list(range(world))
     # every rank sees the same max-over-ranks time, so the same aggregate value
-    assert rows[0]["elapsed_max"] == rows[1]["elapsed_max"]
-    assert abs(rows[0]["value"] - 2 * 256 * 4096 * 3 / rows[0]["elapsed_max"] / 2 ** 30) < 1e-6
+    assert len({x["elapsed_max"] for x in rows}) == 1
+    assert abs(rows[0]["value"] - world * 256 * 4096 * 3 / rows[0]["elapsed_max"] / 2 ** 30) < 1e-6
     # each rank checksummed its own shard (weak scaling: independent seeds, no exchange)
     for x in rows:
         data = synth.splitmix_bytes(synth.SEED_FIXED + x["rank"], 256 * 4096)
         want = orc.crc_ranges(data, np.arange(256) * 4096, np.full(256, 4096), 1)
         assert x["xor"] == int(np.bitwise_xor.reduce(want))
-    assert rows[0]["xor"] != rows[1]["xor"]
+    assert len({x["xor"] for x in rows}) == world
