@@ -497,17 +497,22 @@ constexpr int B_THREADS = 512;
 constexpr int B_LDS_DWORDS = TAB_COLS;  // slice and shift tables (not the column block)
 constexpr int B_BATCH = 8;  // window values per lane loaded ahead of the fold
 
+#ifdef LCRC_PROBE_BLOCKS_NOCONFLICT  // ablation build: every k_blocks lookup reads entry r & 0x3 (wrong CRCs)
+#define KB_IDX(x) ((x) & 3u)
+#else
+#define KB_IDX(x) (x)
+#endif
 __device__ __forceinline__ uint32_t byte_step(const uint32_t* L, uint32_t r, uint32_t b) {
-  return (r >> 8) ^ L[TAB_SLICE + ((r ^ b) & 0xff)];
+  return (r >> 8) ^ L[TAB_SLICE + KB_IDX((r ^ b) & 0xff)];
 }
 __device__ __forceinline__ uint32_t step4(const uint32_t* L, uint32_t r, uint32_t w) {
   uint32_t x = r ^ w;
-  return L[TAB_SLICE + 768 + (x & 0xff)] ^ L[TAB_SLICE + 512 + ((x >> 8) & 0xff)] ^
-         L[TAB_SLICE + 256 + ((x >> 16) & 0xff)] ^ L[TAB_SLICE + (x >> 24)];
+  return L[TAB_SLICE + 768 + KB_IDX(x & 0xff)] ^ L[TAB_SLICE + 512 + KB_IDX((x >> 8) & 0xff)] ^
+         L[TAB_SLICE + 256 + KB_IDX((x >> 16) & 0xff)] ^ L[TAB_SLICE + KB_IDX(x >> 24)];
 }
 __device__ __forceinline__ uint32_t zl(const uint32_t* L, int off, uint32_t r) {
-  return L[off + (r & 0xff)] ^ L[off + 256 + ((r >> 8) & 0xff)] ^ L[off + 512 + ((r >> 16) & 0xff)] ^
-         L[off + 768 + (r >> 24)];
+  return L[off + KB_IDX(r & 0xff)] ^ L[off + 256 + KB_IDX((r >> 8) & 0xff)] ^
+         L[off + 512 + KB_IDX((r >> 16) & 0xff)] ^ L[off + 768 + KB_IDX(r >> 24)];
 }
 
 // Lane g's share of a row walk over [a, e) (0 <= e - a <= 256): the 16 B piece ending at
