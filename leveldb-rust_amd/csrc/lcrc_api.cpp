@@ -485,10 +485,10 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   if (rc) return rc;
   hipStream_t st = pick_stream(ctx, stream);
   const uint64_t nblocks = (file_len + 32767) / 32768;
-  // wal_offsets: [0] the total, then per block the in-workgroup offset (u32) and per 256 blocks a total
+  // wal_offsets: [0] the total, then per block the in-workgroup offset (u32) and per 64 blocks a total
   if ((rc = ctx->wal_counts.ensure(nblocks + 1)) || (rc = ctx->wal_slots.ensure(nblocks * 64 + 1)) ||
       (rc = ctx->wal_stops.ensure(nblocks + 1)) ||
-      (rc = ctx->wal_offsets.ensure(1 + (nblocks + 1) / 2 + (nblocks + 255) / 256 + 1)))
+      (rc = ctx->wal_offsets.ensure(1 + (nblocks + 1) / 2 + (nblocks + 63) / 64 + 1)))
     return rc;
   if (max_recs && ((rc = ctx->wal_descs.ensure(max_recs)) || (rc = ctx->wal_crcs.ensure(max_recs)) ||
                    (rc = ctx->win.ensure(window_words(file_len)))))

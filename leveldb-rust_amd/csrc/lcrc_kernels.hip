@@ -1137,51 +1137,105 @@ __device__ __forceinline__ void wal_header(const uint8_t* __restrict__ blk, uint
 }
 
 // one lane per block: record count, stop reason and the first WAL_SLOTS records as (offset | length << 16,
-// type)
-// ... and the workgroup's exclusive scan of the counts: local[b] (u32) and part[workgroup] (the total)
-__global__ void __launch_bounds__(256) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                   uint64_t nblocks, uint32_t* __restrict__ counts,
-                                                   uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                                   uint32_t* __restrict__ local, uint64_t* __restrict__ part) {
-  __shared__ uint32_t wsum[4];
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+// type), and the wave's exclusive scan of the counts: local[b] (u32) and part[wave] (the total). One wave
+// per workgroup, so the waves spread over the CUs instead of sharing one CU's address units four apiece.
+//
+// The walk is one dependent memory round trip per record, so the block with the most records sets the
+// kernel's time. With WIN > 0 each lane stages WIN bytes of its block at the current header into its own
+// LDS window (one round trip) and follows the chain inside the window at LDS latency, refilling only when
+// the next header lies past it. Header bytes the window loads cannot return (the file's last partial
+// dword: buffer loads are range-checked per dword) come from direct byte loads.
+constexpr uint32_t WAL_PARTB = 64;  // blocks per parse workgroup (= per part total)
+#ifndef LCRC_WAL_WIN
+#define LCRC_WAL_WIN 0
+#endif
+
+template <uint32_t WIN>
+__global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                  uint64_t nblocks, uint32_t* __restrict__ counts,
+                                                  uint2* __restrict__ slots, uint8_t* __restrict__ stops,
+                                                  uint32_t* __restrict__ local, uint64_t* __restrict__ part) {
+  __shared__ u32x4 wwin[WIN ? 64 * (WIN / 16) : 1];
+  const uint64_t b = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint32_t lane = threadIdx.x;
   const uint8_t* blk = file + b * 32768ull;
   const uint64_t rem = b < nblocks ? file_len - b * 32768ull : 0;
   const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
   uint32_t consumed = 0, nrec = 0, stop = LCRC_WAL_STOP_TRAILER_DEV;
-  while (cap - consumed >= 7) {
-    uint32_t length, type;
-    wal_header(blk, consumed, length, type);
-    if (7 + length > cap - consumed) {
-      stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
-      break;
+  if constexpr (WIN == 0) {
+    while (cap - consumed >= 7) {
+      uint32_t length, type;
+      wal_header(blk, consumed, length, type);
+      if (7 + length > cap - consumed) {
+        stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
+        break;
+      }
+      if (type == 0 && length == 0) {
+        stop = LCRC_WAL_STOP_ZERO_DEV;
+        break;
+      }
+      if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type);
+      ++nrec;
+      consumed += 7 + length;
     }
-    if (type == 0 && length == 0) {
-      stop = LCRC_WAL_STOP_ZERO_DEV;
-      break;
+  } else {
+    // the wave's 64 blocks (2 MiB) through one wave-uniform buffer descriptor
+    const uint64_t wbase = (b - lane) * 32768ull;
+    const uint64_t wrem = wbase < file_len ? file_len - wbase : 0;
+    const uint32_t wn = wrem < (64ull << 15) ? (uint32_t)wrem : (64u << 15);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(file + wbase), (short)0, (int)wn,
+                                                                        0x00020000);
+    const uint32_t rel = lane << 15, safe = wn & ~3u;
+    u32x4* mine = wwin + lane * (WIN / 16);
+    const uint8_t* wb = (const uint8_t*)mine;
+    bool more = cap >= 7;
+    while (more) {
+      const uint32_t wlo = consumed & ~15u;
+#pragma unroll
+      for (uint32_t k = 0; k < WIN / 16; ++k)
+        mine[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, rel + wlo + 16 * k, 0, 0);
+      do {
+        uint32_t length, type;
+        if (rel + consumed + 7 <= safe) {
+          const uint32_t at = consumed - wlo;
+          length = wb[at + 4] | ((uint32_t)wb[at + 5] << 8);
+          type = wb[at + 6];
+        } else {
+          wal_header(blk, consumed, length, type);
+        }
+        if (7 + length > cap - consumed) {
+          stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
+          more = false;
+          break;
+        }
+        if (type == 0 && length == 0) {
+          stop = LCRC_WAL_STOP_ZERO_DEV;
+          more = false;
+          break;
+        }
+        if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type);
+        ++nrec;
+        consumed += 7 + length;
+        if (cap - consumed < 7) {
+          more = false;
+          break;
+        }
+      } while (consumed + 7 <= wlo + WIN);
     }
-    if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type);
-    ++nrec;
-    consumed += 7 + length;
   }
-  // workgroup exclusive scan: wave inclusive scan by shuffles, then the wave totals
+  // wave exclusive scan by shuffles
   uint32_t inc = nrec;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t v = __shfl_up(inc, d, 64);
     if (lane >= (uint32_t)d) inc += v;
   }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  uint32_t base = 0;
-  for (uint32_t k = 0; k < w; ++k) base += wsum[k];
   if (b < nblocks) {
     counts[b] = nrec;
     stops[b] = (uint8_t)stop;
-    local[b] = base + inc - nrec;
+    local[b] = inc - nrec;
   }
-  if (threadIdx.x == 255) part[blockIdx.x] = base + inc;
+  if (lane == 63) part[blockIdx.x] = inc;
 }
 
 __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcrc_desc_dev* __restrict__ descs,
@@ -1219,11 +1273,12 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
-  const uint64_t nparts = (nblocks + 255) / 256;
+  const uint64_t nparts = (nblocks + WAL_PARTB - 1) / WAL_PARTB;
   // sum of the parse workgroups' totals before this workgroup's blocks (all of them for workgroup 0's
-  // total); 256 | 256 / WAL_SLOTS blocks, so one parse workgroup covers every block here
-  const uint64_t upto = blockIdx.x == 0 ? nparts : ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / 256;
-  const uint64_t mine = ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / 256;
+  // total); 256 / WAL_SLOTS divides WAL_PARTB, so one parse workgroup covers every block here
+  static_assert(WAL_PARTB % (256 / WAL_SLOTS) == 0, "an emit workgroup's blocks lie in one part");
+  const uint64_t upto = blockIdx.x == 0 ? nparts : ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / WAL_PARTB;
+  const uint64_t mine = ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / WAL_PARTB;
   uint64_t acc = 0, accm = 0;
   for (uint64_t w = threadIdx.x; w < upto; w += 256) {
     acc += part[w];
@@ -2001,9 +2056,9 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  uint2* slots, uint8_t* stops, uint32_t* local, uint64_t* part,
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st) {
-  const uint64_t nparts = (nblocks + 255) / 256;
+  const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
   if (nparts)
-    hipLaunchKernelGGL(lcrc_dev::k_wal_parse, dim3((unsigned)nparts), dim3(256), 0, st, file, file_len, nblocks, counts,
+    hipLaunchKernelGGL(lcrc_dev::k_wal_parse<LCRC_WAL_WIN>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
                        slots, stops, local, part);
   const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
   const uint64_t g = (nt + 255) / 256;

@@ -251,6 +251,28 @@ def test_wal_scan_many_records_per_block(lcrc, orc, engines):
     assert small.download(lcrc.WAL_REC_DTYPE, 10)["header"].tolist() == [h for h, _, _ in want[:10]]
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_wal_scan_file_tail_and_unaligned_base(lcrc, orc, engines, shift):
+    """Files cut at every length over the last record headers (the file's last partial dword comes from
+    direct loads, not the staged window), with the log at an unaligned device address."""
+    import ctypes
+    rng = np.random.default_rng(79)
+    recs = [rng.integers(0, 256, int(rng.integers(0, 1 << int(rng.integers(1, 10)))), dtype=np.uint8).tobytes()
+            for _ in range(400)]
+    full = orc.log_write(recs)
+    for cut in range(len(full) - 40, len(full) + 1):
+        data = full[:cut]
+        dev = lcrc.DeviceBuffer.from_host(np.frombuffer(b"\x5a" * shift + data + b"\xa5" * 5, np.uint8))
+        cap = len(data) // 7 + 1
+        out = lcrc.DeviceBuffer(cap * lcrc.WAL_REC_DTYPE.itemsize)
+        n = ctypes.c_size_t(0)
+        rc = lcrc.lib().lcrc_wal_scan(engines[0].ctx, ctypes.c_void_p(dev.ptr + shift), len(data), out.ptr, cap,
+                                      ctypes.byref(n), None)
+        assert rc == 0
+        got = out.download(lcrc.WAL_REC_DTYPE, n.value)
+        assert [(int(r["header"]), int(r["length"]), int(r["type"])) for r in got] == _wal_expect(orc, data), cut
+
+
 def test_wal_scan_async_matches_sync(lcrc, orc, engines):
     rng = np.random.default_rng(78)
     recs = [rng.integers(0, 256, int(rng.integers(0, 1 << int(rng.integers(1, 17)))), dtype=np.uint8).tobytes()
