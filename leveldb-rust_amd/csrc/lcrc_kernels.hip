@@ -1128,10 +1128,12 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
 constexpr uint32_t WAL_SLOTS = 64;  // records per block kept by the parse (a block with more is re-walked)
 
 // header of the record at in-block offset `at`: length (bytes 4..5) and type (byte 6), three independent
-// byte loads (one memory round trip per hop of the walk)
+// byte loads in ONE memory round trip per hop of the walk (left alone, the compiler sinks the type load
+// below the length check: two dependent round trips per record)
 __device__ __forceinline__ void wal_header(const uint8_t* __restrict__ blk, uint32_t at, uint32_t& length,
                                            uint32_t& type) {
-  const uint32_t l0 = blk[at + 4], l1 = blk[at + 5], ty = blk[at + 6];
+  uint32_t l0 = blk[at + 4], l1 = blk[at + 5], ty = blk[at + 6];
+  __asm__ volatile("" : "+v"(l0), "+v"(l1), "+v"(ty));
   length = l0 | (l1 << 8);
   type = ty;
 }
