@@ -271,7 +271,11 @@ def workload_table(m, synth, engs, rank, device):
     seal.batch_seal(dev, len(f), dd, len(blocks))
     seal.sync()
     seal.close()
-    out = np.zeros(len(blocks) + 8, m.TBLK_DTYPE)
+    # the results land in pinned host memory (lcrc_host_alloc_pinned), as a caller that scans often would
+    # keep them: the 1.5 MB copy then runs at the PCIe rate instead of through a pageable staging copy
+    pinned = m.PinnedBuffer((len(blocks) + 8) * m.TBLK_DTYPE.itemsize)
+    out = pinned.array.view(m.TBLK_DTYPE)
+    out[:] = 0
     scanners = [m.Engine(device, m.MODE_REF) for _ in engs]
     got = scanners[0].table_scan_into(dev, len(f), out)
     if got != len(blocks) or (out["status"][:got] != 0).any():
@@ -279,6 +283,8 @@ def workload_table(m, synth, engs, rank, device):
 
     def step_on(i, eng):  # synchronous: host footer/index parse, device verify, results back on the host
         scanners[engs.index(eng)].table_scan_into(dev, len(f), out)
+
+    step_on.keep = pinned  # the pinned buffer lives as long as the step
 
     cfg = {"workload": "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)",
            "blocks": len(blocks), "file_bytes": int(len(f))}

@@ -51,7 +51,8 @@ hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uin
                                  uint64_t* count, uint64_t* flag, const uint64_t* pos, lcrc_tblk_dev* out,
                                  lcrc_desc_dev* descs, hipStream_t st);
 hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
-                                  const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st);
+                                  const uint8_t* file, lcrc_desc_dev* frames, uint32_t* unsorted, uint32_t gen,
+                                  hipStream_t st);
 hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
 hipError_t lcrc_launch_store_crc(uint8_t* base, uint64_t base_len, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
@@ -128,7 +129,7 @@ struct lcrc_ctx {
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs;
   uint64_t* h_count = nullptr;  // pinned, 8 words: [0] record count of the synchronous WAL scan, [1..3] table
-                                // scan staging, [4..6] Snappy totals and maxima
+                                // scan staging, [4..6] Snappy totals and maxima, [7] table scan order flag
   // Snappy frames: chunk CRCs are CRC-32C whatever the context's mode
   uint32_t* d_tab_c = nullptr;  // CRC-32C image when mode != C (created on first use)
   DevBuf<uint64_t> sn_size, sn_nch, sn_choff, sn_part;
@@ -137,6 +138,8 @@ struct lcrc_ctx {
   DevBuf<uint32_t> sn_cexp, sn_cframe, sn_ccrc;
   DevBuf<uint64_t> sn_out_off;  // table scan: frame output offsets
   DevBuf<lcrc_tblk_dev> tbl_blk;  // table scan on the device: the blocks being assembled
+  DevBuf<uint32_t> tbl_flag;      // = tbl_gen when that scan's blocks are out of offset order
+  uint32_t tbl_gen = 0;
   DevBuf<uint64_t> idx_count, idx_flag, idx_pos, idx_fpos;
   DevBuf<lcrc_desc_dev> tbl_frames;
   DevBuf<uint8_t> sn_out, sn_status;
@@ -282,6 +285,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   for (auto* b : {&ctx->sn_cexp, &ctx->sn_cframe, &ctx->sn_ccrc}) b->release();
   ctx->sn_cdesc.release();
   ctx->tbl_blk.release();
+  ctx->tbl_flag.release();
   for (auto* b : {&ctx->idx_count, &ctx->idx_flag, &ctx->idx_pos, &ctx->idx_fpos}) b->release();
   ctx->tbl_frames.release();
   ctx->sn_out.release();
@@ -757,13 +761,22 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
   // checked on the device
   if ((rc = lcrc_batch(ctx, file, file_len, (const lcrc_desc*)ctx->tbl_descs.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, st)))
     return rc;
-  HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, st));
+  if (!ctx->tbl_flag.p) {
+    if ((rc = ctx->tbl_flag.ensure(1))) return rc;
+    HIPCHK(hipMemsetAsync(ctx->tbl_flag.p, 0, sizeof(uint32_t), st));
+  }
+  if (++ctx->tbl_gen == 0) ctx->tbl_gen = 1;
+  HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p,
+                                ctx->tbl_flag.p, ctx->tbl_gen, st));
   // the Snappy frames' framing pass (a malformed frame is already status 3 here), then the results and the
   // frame totals come back in ONE round trip; only a table with compressed blocks goes on to decode them
   if ((rc = snappy_plan(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out_off.p, ctx->sn_status.p, st))) return rc;
   HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, st));
   HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
+  uint32_t* h_unsorted = (uint32_t*)(ctx->h_count + 7);  // pinned
+  HIPCHK(hipMemcpyAsync(h_unsorted, ctx->tbl_flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const bool sorted = *h_unsorted != ctx->tbl_gen;
   if (ctx->h_count[5]) {  // data chunks to decode and check
     uint64_t total = 0;
     if ((rc = ctx->sn_out.ensure(ctx->h_count[4]))) return rc;
@@ -774,9 +787,7 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
-  // sorted by offset (a well-formed table already is)
-  bool sorted = true;
-  for (size_t k = 1; k < n && sorted; ++k) sorted = blocks[k - 1].offset <= blocks[k].offset;
+  // sorted by offset (a well-formed table already is; the order was checked by k_tbl_finish)
   if (!sorted)
     std::stable_sort(blocks, blocks + n, [](const lcrc_tblk& a, const lcrc_tblk& b) { return a.offset < b.offset; });
   return LCRC_OK;
