@@ -4,26 +4,36 @@
 Metric (BASELINE.json): GiB/s of CRC32C over device-resident 4 KiB blocks, and the fraction of HBM3E read
 bandwidth. A "step" is one batched checksum pass over one 64K x 4 KiB batch (256 MiB, BASELINE.json
 configs[1]) already resident in HBM; four such batches rotate so every step reads from HBM rather than the
-256 MiB Infinity Cache. N>1: one process per GPU (torch.distributed.run), each rank checksums its own
-independent batches (no collective on the data path); `value` = all ranks' bytes / max-over-ranks time.
+256 MiB Infinity Cache.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed|mixed|wal] [--mode c|ref]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed|mixed|wal|table|seal|snappy]
+                    [--mode c|ref] [--queue Q] [--streams S]
 
-Steps are submitted round-robin to --streams engines (default 2: two contexts, each with its own HIP
-stream and workspace), the way a storage server keeps more than one verify batch in flight: batch i+1's
-workgroups start on the CUs that batch i's tail has already left. Every step is a complete, independent
-launch over its own batch; nothing is skipped or cached.
+Submission (fixed config). By default the K timed steps are submitted through lcrc_batch_uniform_queue, the
+way a storage server hands over its pending verify batches: each step is its own complete batch (own
+buffer, own CRC output), and the engine streams up to 32 of them per launch of the fast-path kernel, so the
+LDS table image and the end-of-launch spread are paid once per launch instead of once per batch.
+`--queue 1` submits one lcrc_batch_uniform launch per step instead (rotated over --streams contexts).
 
-Prints ONE JSON line on rank 0. `roofline.achieved` = payload bytes per launch / average duration of the
-SAME launch run alone: a second timed phase launches it back to back on ONE stream, bracketed by HIP
-events on that stream (this is the figure the rocprofv3 kernel trace in profiles/ must agree with, taken
-with --streams 1). `traffic` comes from the rocprofv3 PMC summary in profiles/ when one exists for this
-workload (tools/profile_round.sh), else null. `cpu_baseline` times the oracle's restatement of the
-reference's CPU CRC on this host (rank 0, N=1 only).
+N GPUs (BASELINE configs[4]): one process per GPU. Under torch.distributed.run the ranks come from the
+environment; `python bench.py --gpus N` without it spawns the N rank processes itself (before anything
+touches a GPU). Each rank checksums its own independent batches on device LOCAL_RANK; there is no
+collective on the data path -- gloo carries only the barrier, the max-over-ranks time and the per-rank
+figures. `value` = all ranks' bytes / max-over-ranks time (weak scaling).
+
+Prints ONE JSON line on rank 0. `roofline.achieved` = algorithmic bytes per launch / average launch duration,
+where the average comes from HIP events recorded on the engine stream around the timed region itself
+(queued submission: one stream; the same launches rocprofv3's kernel trace reports -- tools/profile_round.sh
+profiles this exact command). `roofline.profile` repeats the figure from the committed rocprofv3 summary in
+profiles/ for the same config. `cpu_baseline` times the oracle's restatement of the reference's CPU CRC on
+this host's usable cores (rank 0, N=1 only) and cross-checks the device CRCs against it.
 """
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,6 +46,7 @@ import __graft_entry__ as entry  # noqa: E402
 METRIC = "GiB/s CRC32C over device-resident 4 KiB blocks; % of HBM3E read BW"
 PEAK_GBS = 8000.0  # MI355X HBM3E peak, GB/s (MI355X_MICROARCH.md chip table, spec)
 NBUF = 4
+QMAX = 32  # batches per queued launch (MAX_QJOBS in lcrc_kernels.hip)
 
 
 def parse(argv=None):
@@ -45,6 +56,16 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", choices=["fixed", "mixed", "wal", "table", "snappy", "seal"], default="fixed")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
+    p.add_argument("--queue", type=int, default=5,
+                   help="fixed config: steps per lcrc_batch_uniform_queue submission (default 5 = the driver's warmup, so "
+                        "every launch -- warmup and timed -- has the same shape; 0: all timed steps in one "
+                        "submission, <= 32 per launch, launches balanced; 1: one lcrc_batch_uniform per step)")
+    p.add_argument("--streams", type=int, default=0,
+                   help="engines (context + HIP stream) the submissions rotate over (0: 1 queued, 2 per-step)")
+    p.add_argument("--blocks", type=int, default=65536, help="fixed config: 4 KiB blocks per batch")
+    p.add_argument("--engine", choices=["device", "host"], default="device",
+                   help="host: the library's scalar host path instead of the device (device-free test of the "
+                        "N-rank launcher; never a headline figure)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=1.0, help="wall seconds of the CPU baseline sample")
     p.add_argument("--extra-out", default=None, help="also write the result dict to this file")
@@ -52,14 +73,41 @@ def parse(argv=None):
                    help="fixed config starting and ending in (pinned) host memory: H2D + kernel + D2H per step "
                         "(the PCIe-inclusive end-to-end rate reported in DESIGN.md, never the headline value)")
     p.add_argument("--chunk-mib", type=int, default=32, help="host-resident pipeline chunk size")
-    p.add_argument("--streams", type=int, default=2, help="engines (context + HIP stream) steps rotate over")
     return p.parse_args(argv)
 
 
-class Dist:
-    """torch.distributed wrapper (barrier + max-over-ranks); single-process when WORLD_SIZE is unset."""
+# ---------------------------------------------------------------------------------------------------
+# N ranks
+# ---------------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
-    def __init__(self, backend=None):
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` outside torch.distributed.run: start N rank processes (RANK = LOCAL_RANK = r,
+    WORLD_SIZE = N, rendezvous on 127.0.0.1) running this same command, and exit with the worst status.
+    Nothing here touches a GPU: the parent only waits; rank 0 prints the line."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+class Dist:
+    """torch.distributed over gloo (barrier, max-over-ranks, per-rank figures); single-process when
+    WORLD_SIZE is unset. The data path has no collective, so no RCCL communicator is ever created."""
+
+    def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -67,102 +115,55 @@ class Dist:
         if self.world > 1:
             import torch
             import torch.distributed as dist
-            if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
-            if backend == "nccl":
-                torch.cuda.set_device(self.local_rank)
-            dist.init_process_group(backend)
-            self.dist, self.torch, self.backend = dist, torch, backend
+            dist.init_process_group("gloo")
+            self.dist, self.torch = dist, torch
 
     def barrier(self):
         if self.dist is not None:
-            if self.backend == "nccl":
-                self.dist.barrier(device_ids=[self.local_rank])
-            else:
-                self.dist.barrier()
+            self.dist.barrier()
 
     def max(self, x):
         if self.dist is None:
             return x
-        dev = f"cuda:{self.local_rank}" if self.backend == "nccl" else "cpu"
-        t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=dev)
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
+
+    def gather(self, values):
+        """Every rank's `values` (a list of floats), indexed by rank, on every rank."""
+        if self.dist is None:
+            return [list(values)]
+        t = self.torch.tensor([float(v) for v in values], dtype=self.torch.float64)
+        out = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [o.tolist() for o in out]
 
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()
 
 
-def cuda_sync():
-    try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-    except ImportError:
-        pass
-
-
-def timed_run(dist, step, steps, warmup, engines=()):
+def timed_run(dist, prepare, steps, warmup, engines=()):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
-    Returns the max-over-ranks wall seconds."""
-    for i in range(warmup):
-        step(i)
+    `prepare(first, count)` returns a callable that submits steps first .. first+count-1 (argument
+    marshalling done before the clock starts). Returns the max-over-ranks wall seconds, this rank's wall
+    seconds and its GPU milliseconds of the timed region from HIP events on the first engine's stream."""
+    if warmup:
+        prepare(0, warmup)()
+    go = prepare(warmup, steps)
     for e in engines:
         e.sync()
-    cuda_sync()
     dist.barrier()
-    cuda_sync()
+    if engines:
+        engines[0].timer_start()
     t0 = time.perf_counter()
-    for i in range(steps):
-        step(warmup + i)
+    go()
     for e in engines:
         e.sync()
-    cuda_sync()
-    dist.barrier()
-    cuda_sync()
     elapsed = time.perf_counter() - t0
-    return dist.max(elapsed), None
-
-
-def launch_ms(step_on, eng, reps, windows=3):
-    """Average duration of one launch run alone: `reps` launches back to back on ONE engine's stream,
-    bracketed by HIP events recorded on that stream; the median of `windows` such windows (the chip's
-    clock under this load wanders by ~10% from one window to the next)."""
-    step_on(0, eng)
-    eng.sync()
-    per = []
-    for _ in range(windows):
-        eng.timer_start()
-        for i in range(reps):
-            step_on(i, eng)
-        per.append(eng.timer_stop() / reps)
-        eng.sync()
-    return float(np.median(per))
-
-
-def launch_ms_graph(step_on, eng, reps, windows=3):
-    """Same as launch_ms with the `reps` launches captured once into a HIP graph and the graph replayed:
-    the per-launch dispatch gap of the stream path mostly disappears, so the figure is close to the
-    kernel's own duration (what rocprofv3's kernel trace reports). None if the step cannot be captured."""
-    step_on(0, eng)
-    eng.sync()
-    try:
-        g = eng.graph_capture(lambda: [step_on(i, eng) for i in range(reps)])
-    except RuntimeError:
-        return None
-    try:
-        eng.graph_launch(g)
-        eng.sync()
-        per = []
-        for _ in range(windows):
-            eng.timer_start()
-            eng.graph_launch(g)
-            per.append(eng.timer_stop() / reps)
-            eng.sync()
-    finally:
-        eng.graph_destroy(g)
-    return float(np.median(per))
+    gpu_ms = engines[0].timer_stop() if engines else None
+    dist.barrier()
+    return dist.max(elapsed), elapsed, gpu_ms
 
 
 def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
@@ -170,67 +171,154 @@ def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
     return bytes_per_step * steps * world / elapsed_max / 2 ** 30
 
 
+def groups(first, count, q):
+    """Split steps [first, first + count) into submissions of at most q steps, launches of <= QMAX balanced."""
+    q = count if q <= 0 else q
+    out = []
+    i = first
+    while i < first + count:
+        n = min(q, first + count - i)
+        out.append((i, n))
+        i += n
+    return out
+
+
+def launches_of(n):
+    return (n + QMAX - 1) // QMAX
+
+
+def balanced_jobs(jobs):
+    """Cut a submission into ceil(n/32) launches of near-equal size (32 + 18 would leave a short launch)."""
+    k = launches_of(len(jobs))
+    if k <= 1:
+        return [jobs]
+    per = (len(jobs) + k - 1) // k
+    return [jobs[i:i + per] for i in range(0, len(jobs), per)]
+
+
+class Workload:
+    """run(first, count, engs): submit steps; nbytes: algorithmic bytes per step; launches(count): kernel
+    launches the dominant kernel makes for `count` steps; sample / crcs: the CPU baseline's sample and the
+    device's CRCs of that sample; xor(): xor of the device CRCs of step 0 (per-rank shard fingerprint)."""
+
+    def __init__(self, run, nbytes, cfg, launches=None, sample=None, crcs=None, per_step_sync=False):
+        self.run, self.nbytes, self.cfg = run, nbytes, cfg
+        self.launches = launches or (lambda count: count)
+        self.sample, self.crcs = sample, crcs
+        self.per_step_sync = per_step_sync
+
+
 # ---------------------------------------------------------------------------------------------------
-# workloads: each returns (step(i) callable, payload bytes per step, config dict, host sample for the CPU
-# baseline, verify(i) callable giving the device crcs of step i for the baseline cross-check)
+# workloads
 # ---------------------------------------------------------------------------------------------------
-def workload_fixed(m, synth, engs, rank, device):
-    nblk, blen = 65536, 4096
+def workload_fixed(m, synth, engs, rank, device, args):
+    nblk, blen = args.blocks, 4096
     host = [synth.splitmix_bytes(synth.SEED_FIXED + rank * NBUF + i, nblk * blen) for i in range(NBUF)]
     bufs = [m.DeviceBuffer.from_host(h, device) for h in host]
-    outs = [m.DeviceBuffer(nblk * 4, device) for _ in engs]
+    outs = [[m.DeviceBuffer(nblk * 4, device) for _ in range(NBUF)] for _ in engs]
+    q = args.queue
 
-    def step_on(i, eng):
-        eng.batch_uniform(bufs[i % NBUF], nblk, blen, blen, outs[engs.index(eng)])
+    if q == 1:  # one lcrc_batch_uniform launch per step, rotated over the engines
+        def run(first, count):
+            for i in range(first, first + count):
+                k = i % len(engs)
+                engs[k].batch_uniform(bufs[i % NBUF], nblk, blen, blen, outs[k][i % NBUF])
 
-    step_on.graphable = True
+        launches = lambda count: count  # noqa: E731
+        sub = "one lcrc_batch_uniform launch per step"
+    else:
+        def run(first, count):
+            subs = []
+            for g, (i0, n) in enumerate(groups(first, count, q)):
+                k = g % len(engs)
+                jobs = [(bufs[i % NBUF], nblk, outs[k][i % NBUF]) for i in range(i0, i0 + n)]
+                subs += [(engs[k], m.ujobs(part)) for part in balanced_jobs(jobs)]
+
+            def go():
+                for e, arr in subs:
+                    e.batch_uniform_queue(arr, blen, blen)
+            return go
+        run.prepares = True
+
+        launches = lambda count: sum(launches_of(n) for _, n in groups(0, count, q))  # noqa: E731
+        sub = ("lcrc_batch_uniform_queue: the timed steps in one submission" if q <= 0 else
+               f"lcrc_batch_uniform_queue: {q} steps per submission") + f", <= {QMAX} batches per launch"
 
     def crcs():  # device result for batch 0 (the CPU baseline's sample)
-        step_on(0, engs[0])
+        engs[0].batch_uniform(bufs[0], nblk, blen, blen, outs[0][0])
         engs[0].sync()
-        return outs[0].download(np.uint32, nblk)
+        return outs[0][0].download(np.uint32, nblk)
 
-    cfg = {"workload": "64K x 4 KiB blocks, device-resident (BASELINE configs[1])", "blocks": nblk,
-           "block_bytes": blen, "batches_rotated": NBUF, "layout": "back-to-back"}
-    return step_on, nblk * blen, cfg, (host[0], nblk, blen), crcs
+    cfg = {"workload": f"{nblk // 1024}K x 4 KiB blocks, device-resident (BASELINE configs[1])", "blocks": nblk,
+           "block_bytes": blen, "batches_rotated": NBUF, "layout": "back-to-back", "submission": sub}
+    return Workload(run, nblk * blen, cfg, launches, ("uniform", host[0], nblk, blen), crcs)
 
 
-def workload_host(m, synth, engs, rank, device, chunk_mib=32):
-    nblk, blen = 65536, 4096
+def workload_fixed_host(m, synth, rank, args):
+    """--engine host: the same batches through the library's scalar host path (device-free test)."""
+    nblk, blen = args.blocks, 4096
+    host = [synth.splitmix_bytes(synth.SEED_FIXED + rank * NBUF + i, nblk * blen) for i in range(NBUF)]
+    mode = m.MODE_C if args.mode == "c" else m.MODE_REF
+    last = {}
+
+    def one(i):
+        d = host[i % NBUF]
+        c = np.array([m.value(d[b * blen:(b + 1) * blen], mode) for b in range(nblk)], np.uint32)
+        return np.array([m.mask(int(x)) for x in c], np.uint32) if mode == m.MODE_C else c
+
+    def run(first, count):
+        for i in range(first, first + count):
+            last[i % NBUF] = one(i)
+
+    cfg = {"workload": f"{nblk} x 4 KiB blocks on the HOST scalar path (launcher test, not a GPU figure)",
+           "blocks": nblk, "block_bytes": blen}
+    return Workload(run, nblk * blen, cfg, None, None, lambda: one(0))
+
+
+def workload_host(m, synth, engs, rank, device, args):
+    nblk, blen = args.blocks, 4096
     pinned = m.PinnedBuffer(nblk * blen)
     pinned.array[:] = synth.splitmix_bytes(synth.SEED_FIXED + rank * NBUF, nblk * blen)
 
-    def step_on(i, eng):
-        eng.batch_host_uniform(pinned, nblk, blen, blen, chunk_bytes=chunk_mib << 20)
+    def run(first, count):
+        for i in range(first, first + count):
+            engs[i % len(engs)].batch_host_uniform(pinned, nblk, blen, blen, chunk_bytes=args.chunk_mib << 20)
 
+    run.keep = pinned
     cfg = {"workload": "64K x 4 KiB blocks, HOST-resident pinned buffer: H2D + kernel + D2H (end-to-end)",
-           "blocks": nblk, "block_bytes": blen, "chunk_mib": chunk_mib}
-    return step_on, nblk * blen, cfg, None, None
+           "blocks": nblk, "block_bytes": blen, "chunk_mib": args.chunk_mib}
+    return Workload(run, nblk * blen, cfg, None, None, None, per_step_sync=True)
 
 
-def workload_mixed(m, synth, engs, rank, device):
+def workload_mixed(m, synth, engs, rank, device, args):
     sizes = synth.mixed_sizes(256 << 20, seed=synth.SEED_MIXED + rank)
     offs, total = synth.sstable_layout(sizes)
     data = synth.splitmix_bytes(synth.SEED_MIXED + 1000 + rank, total)
+    lens = sizes.astype(np.uint64) + 1
     d = np.zeros(len(sizes), m.DESC_DTYPE)
-    d["offset"], d["length"], d["expect_rel"] = offs, sizes.astype(np.uint64) + 1, m.NO_EXPECT
+    d["offset"], d["length"], d["expect_rel"] = offs, lens, m.NO_EXPECT
     bufs = [m.DeviceBuffer.from_host(data, device) for _ in range(2)]
     dd = m.DeviceBuffer.from_host(d.view(np.uint8), device)
     outs = [m.DeviceBuffer(4 * len(sizes), device) for _ in engs]
     for e in engs:
         e.reserve(total)
 
-    def step_on(i, eng):
-        eng.batch(bufs[i % 2], total, dd, len(sizes), outs[engs.index(eng)])
+    def run(first, count):
+        for i in range(first, first + count):
+            k = i % len(engs)
+            engs[k].batch(bufs[i % 2], total, dd, len(sizes), outs[k])
 
-    step_on.graphable = True
+    def crcs():
+        engs[0].batch(bufs[0], total, dd, len(sizes), outs[0])
+        engs[0].sync()
+        return outs[0].download(np.uint32, len(sizes))
 
     cfg = {"workload": "SSTable file, block sizes 256 B-64 KiB zipf(1.1) (BASELINE configs[2])",
            "blocks": int(len(sizes)), "file_bytes": int(total), "mean_block": float(sizes.mean())}
-    return step_on, int((sizes.astype(np.uint64) + 1).sum()), cfg, None, None
+    return Workload(run, int(lens.sum()), cfg, None, ("ranges", data, offs, lens), crcs)
 
 
-def workload_wal(m, synth, engs, rank, device):
+def workload_wal(m, synth, engs, rank, device, args):
     w = m.LogWriter()
     payload = synth.splitmix_bytes(synth.SEED_WAL + 1000 + rank, 1 << 20)
     for n in synth.wal_lengths(256 << 20, seed=synth.SEED_WAL + rank):
@@ -243,22 +331,41 @@ def workload_wal(m, synth, engs, rank, device):
     for e in engs:
         e.reserve(len(data))
     first = engs[0].wal_scan(dev, len(data), maxr, recs[0])
+    if engs[0].mode != m.MODE_REF:
+        # the writer's headers hold crc32fast values (log.rs:61-64); for a CRC-32C log re-seal every header in
+        # place with this mode's raw CRC (lcrc_batch_seal, {h + 6, 1 + len, -6}) so the scan verifies clean
+        d = np.zeros(len(first), m.DESC_DTYPE)
+        d["offset"], d["length"], d["expect_rel"] = first["header"] + 6, first["length"] + 1, -6
+        dd = m.DeviceBuffer.from_host(d.view(np.uint8), device)
+        seal = m.Engine(device, engs[0].mode, 0)
+        seal.batch_seal(dev, len(data), dd, len(first))
+        seal.sync()
+        seal.close()
+        data = dev.download(np.uint8, len(data))
+        first = engs[0].wal_scan(dev, len(data), maxr, recs[0])
     covered = int((first["length"].astype(np.uint64) + 1).sum())
+    # structure: every record lies inside its 32 KiB block, in file order, none overlapping
+    h = first["header"].astype(np.uint64)
+    ends = h + 7 + first["length"].astype(np.uint64)
+    if len(first) and (np.any(h[1:] < ends[:-1]) or np.any((h // 32768) != ((ends - 1) // 32768))):
+        raise RuntimeError("wal bench: the device scan's records overlap or straddle a block")
+    if (first["status"] != 0).any():
+        raise RuntimeError("wal bench: a freshly written log has a record flagged as corrupt")
 
-    def step_on(i, eng):  # enqueued like the other workloads; records and their count stay on the device
-        k = engs.index(eng)
-        eng.wal_scan_async(dev, len(data), recs[k], maxr, counts[k])
-
-    step_on.graphable = True
+    def run(first_, count):  # records and their count stay on the device
+        for i in range(first_, first_ + count):
+            k = i % len(engs)
+            engs[k].wal_scan_async(dev, len(data), recs[k], maxr, counts[k])
 
     cfg = {"workload": "WAL: 32 KiB log blocks, records n~U[1,2^k), k~U[1,16] (BASELINE configs[3])",
            "file_bytes": int(len(data)), "records": int(len(first)), "bytes_counted": "sum(1+len)"}
-    return step_on, covered, cfg, None, None
+    sample = ("ranges_raw", data, h + 6, first["length"].astype(np.uint64) + 1)
+    return Workload(run, covered, cfg, None, sample, lambda: first["crc"].copy())
 
 
-def workload_table(m, synth, engs, rank, device):
+def workload_table(m, synth, engs, rank, device, args):
     """Whole-table verify scan of a 64K x 4 KiB-block SSTable: footer, index parse on
-    the host, one device verify of every trailer. The trailers are sealed once by the device writer path."""
+    the device, one device verify of every trailer. The trailers are sealed once by the device writer path."""
     nblk, blen = 65536, 4096
     f, blocks = synth.table_layout(nblk, blen, seed=synth.SEED_TABLE + rank)
     dev = m.DeviceBuffer.from_host(f, device)
@@ -281,17 +388,17 @@ def workload_table(m, synth, engs, rank, device):
     if got != len(blocks) or (out["status"][:got] != 0).any():
         raise RuntimeError("table bench: the sealed table does not scan clean")
 
-    def step_on(i, eng):  # synchronous: host footer/index parse, device verify, results back on the host
-        scanners[engs.index(eng)].table_scan_into(dev, len(f), out)
+    def run(first, count):  # synchronous: footer, device index walk and verify, results back on the host
+        for i in range(first, first + count):
+            scanners[i % len(engs)].table_scan_into(dev, len(f), out)
 
-    step_on.keep = pinned  # the pinned buffer lives as long as the step
-
+    run.keep = (pinned, scanners)
     cfg = {"workload": "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)",
            "blocks": len(blocks), "file_bytes": int(len(f))}
-    return step_on, int(sum(b[1] + 1 for b in blocks)), cfg, None, None
+    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None, per_step_sync=True)
 
 
-def workload_seal(m, synth, engs, rank, device):
+def workload_seal(m, synth, engs, rank, device, args):
     """Writer-side trailers in batch: the trailer of every block of a 64K x 4 KiB-block
     SSTable computed over content||type and stored in place (write_raw_block, table.rs:507-529, for a whole
     flush/compaction output at once); --mode ref gives the reference's crc32fast trailers."""
@@ -311,16 +418,16 @@ def workload_seal(m, synth, engs, rank, device):
     if engs[0].table_scan_into(dev, len(f), out) != len(blocks) or (out["status"][:len(blocks)] != 0).any():
         raise RuntimeError("seal bench: the sealed table does not scan clean")
 
-    def step_on(i, eng):  # enqueued: CRCs of every block, stored little-endian in the trailers
-        eng.batch_seal(dev, len(f), dd, len(blocks))
+    def run(first, count):  # enqueued: CRCs of every block, stored little-endian in the trailers
+        for i in range(first, first + count):
+            engs[i % len(engs)].batch_seal(dev, len(f), dd, len(blocks))
 
-    step_on.graphable = True
     cfg = {"workload": "writer-side trailers: 64K x 4 KiB blocks of one SSTable sealed in place",
            "blocks": len(blocks), "file_bytes": int(len(f))}
-    return step_on, int(sum(b[1] + 1 for b in blocks)), cfg, None, None
+    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg)
 
 
-def workload_snappy(m, synth, engs, rank, device):
+def workload_snappy(m, synth, engs, rank, device, args):
     """Snappy-framed blocks: 64K frames of one compressed 4 KiB chunk each, decoded and
     every chunk's masked CRC-32C checked on the device. Bytes counted: decoded bytes."""
     nfr = 65536
@@ -341,15 +448,19 @@ def workload_snappy(m, synth, engs, rank, device):
     if total != cap or outs[0][2].download(np.uint8, nfr).any():
         raise RuntimeError("snappy bench: the synthetic frames do not verify")
 
-    def step_on(i, eng):  # synchronous: sizes back to the host once, then decode + CRC on the device
-        o, off, st = outs[engs.index(eng)]
-        eng.snappy_frames_into(base, dd, nfr, o, cap, off, st)
+    def run(first, count):  # synchronous: sizes back to the host once, then decode + CRC on the device
+        for i in range(first, first + count):
+            o, off, st = outs[i % len(engs)]
+            engs[i % len(engs)].snappy_frames_into(base, dd, nfr, o, cap, off, st)
 
     cfg = {"workload": "Snappy frames: 64K x (1 compressed chunk -> 4 KiB), decode + masked CRC-32C per chunk",
            "frames": nfr, "frame_bytes": len(frame)}
-    return step_on, cap, cfg, None, None
+    return Workload(run, cap, cfg, None, None, None, per_step_sync=True)
 
 
+# ---------------------------------------------------------------------------------------------------
+# evidence: committed profiles, CPU baseline
+# ---------------------------------------------------------------------------------------------------
 def load_traffic(config, mode):
     path = os.path.join(ROOT, "profiles", f"traffic_{config}_{mode}.json")
     if not os.path.exists(path):
@@ -358,26 +469,67 @@ def load_traffic(config, mode):
         return json.load(f).get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(orc, sample, mode, seconds, device_crcs):
+def load_profile(config, mode):
+    """The newest committed rocprofv3 summary of this config (tools/profile_round.sh): the dominant
+    kernel's average duration and the roofline fraction it implies for the bytes per launch of that run."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_{mode}_summary.json")))
+    for path in reversed(cands):
+        with open(path) as f:
+            s = json.load(f)
+        if "frac" in s and "kernel" in s:
+            return {"file": os.path.relpath(path, ROOT), "kernel": s["kernel"], "avg_us": s["avg_us"],
+                    "bytes_per_launch": s["bytes_per_launch"], "frac": s["frac"]}
+    return None
+
+
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota when one is set (a GPU
+    box's share of a large host is a quota, not an affinity mask)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_baseline(orc, m, sample, mode, seconds, device_crcs):
     """The reference's CPU CRC restated in oracle/ (snap's SSE4.2 CRC-32C path for mode c, crc32fast's
-    PCLMULQDQ path for mode ref), all usable host cores, repeated passes over the same 256 MiB batch."""
-    data, nblk, blen = sample
-    threads = min(16, os.cpu_count() or 1)
+    PCLMULQDQ path for mode ref) on every usable host core, repeated passes over the same sample, and the
+    device's CRCs of that sample checked against it."""
+    kind, data = sample[0], sample[1]
+    threads, affinity, quota = usable_cpus()
     algo = orc.ALGO_SSE42_C if mode == "c" else orc.ALGO_PCLMUL_REF
-    crcs, secs = orc.crc_uniform_mt(data, nblk, blen, blen, threads, algo)  # warm + cross-check
+    raw = kind == "ranges_raw"  # WAL records carry the raw (unmasked) crc
+
+    if kind == "uniform":
+        nblk, blen = sample[2], sample[3]
+        fn = lambda t: orc.crc_uniform_mt(data, nblk, blen, blen, t, algo)  # noqa: E731
+        nbytes = nblk * blen
+        what = f"one {nblk // 1024}K x 4 KiB batch"
+    else:
+        offs, lens = sample[2], sample[3]
+        fn = lambda t: orc.crc_ranges_mt(data, offs, lens, t, algo)  # noqa: E731
+        nbytes = int(np.asarray(lens, np.uint64).sum())
+        what = f"{len(offs)} ranges, {nbytes / 2 ** 20:.0f} MiB covered"
+    crcs, _ = fn(threads)  # warm + cross-check
     match = None
     if device_crcs is not None:
-        want = crcs if mode == "ref" else np.fromiter((orc.mask(int(c)) for c in crcs), np.uint32, len(crcs))
+        want = orc.mask_array(crcs) if (mode == "c" and not raw) else crcs
         match = bool(np.array_equal(device_crcs(), want))
     passes, total = 0, 0.0
     while total < seconds or passes < 2:
-        _, s = orc.crc_uniform_mt(data, nblk, blen, blen, threads, algo)
+        _, s = fn(threads)
         total += s
         passes += 1
-    gib = passes * nblk * blen / 2 ** 30
+    gib = passes * nbytes / 2 ** 30
     one, one_s = 0, 0.0  # the same restatement on one core (SURVEY 8(d): single thread and all cores)
     while one_s < min(seconds, 1.0) or one < 1:
-        _, s1 = orc.crc_uniform_mt(data, nblk, blen, blen, 1, algo)
+        _, s1 = fn(1)
         one_s += s1
         one += 1
     model = ""
@@ -387,16 +539,20 @@ def cpu_baseline(orc, sample, mode, seconds, device_crcs):
     except OSError:
         pass
     return {"value": round(gib / total, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "single_thread": round(one * nblk * blen / 2 ** 30 / one_s, 2), "cpu_model": model,
-            "host_cpus": os.cpu_count(),
-            "sample": f"{passes} passes over one 64K x 4 KiB batch ({gib:.1f} GiB), "
+            "single_thread": round(one * nbytes / 2 ** 30 / one_s, 2), "cpu_model": model,
+            "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "sample": f"{passes} passes over {what} ({gib:.1f} GiB), "
                       f"{'snap SSE4.2 crc32c' if mode == 'c' else 'crc32fast PCLMULQDQ'} restated in oracle/, "
-                      f"{threads} threads",
+                      f"{threads} threads (every usable CPU: affinity {affinity}, cgroup quota {quota})",
             "cpu_seconds": round(total * threads, 1), "matches_device": match}
 
 
+# ---------------------------------------------------------------------------------------------------
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus, argv)
     dist = Dist()
     rank, world = dist.rank, dist.world
     device = dist.local_rank
@@ -404,25 +560,30 @@ def main(argv=None):
     synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
     mode = m.MODE_C if args.mode == "c" else m.MODE_REF
     flags = m.FLAG_MASK if mode == m.MODE_C else 0
-    engs = [m.Engine(device, mode, flags) for _ in range(max(1, args.streams))]
-    if args.host_resident:
-        step_on, nbytes, cfg, sample, crcs = workload_host(m, synth, engs, rank, device, args.chunk_mib)
+    queued = args.config == "fixed" and not args.host_resident and args.queue != 1
+    nstreams = args.streams or (1 if queued else 2)
+    if args.engine == "host":
+        engs = []
+        w = workload_fixed_host(m, synth, rank, args)
     else:
-        step_on, nbytes, cfg, sample, crcs = {"fixed": workload_fixed, "mixed": workload_mixed, "wal": workload_wal,
-                                              "table": workload_table, "seal": workload_seal,
-                                              "snappy": workload_snappy}[args.config](m, synth, engs, rank, device)
+        engs = [m.Engine(device, mode, flags) for _ in range(max(1, nstreams))]
+        if args.host_resident:
+            w = workload_host(m, synth, engs, rank, device, args)
+        else:
+            w = {"fixed": workload_fixed, "mixed": workload_mixed, "wal": workload_wal, "table": workload_table,
+                 "seal": workload_seal, "snappy": workload_snappy}[args.config](m, synth, engs, rank, device, args)
 
-    def step(i):
-        step_on(i, engs[i % len(engs)])
+    prepare = w.run if getattr(w.run, "prepares", False) else (lambda f, c: (lambda: w.run(f, c)))
+    elapsed_max, elapsed, gpu_ms = timed_run(dist, prepare, args.steps, args.warmup, engs)
+    value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
+    # this rank's fingerprint and rate, gathered over gloo (no RCCL)
+    fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
+    rows = dist.gather([rank, device, elapsed, fp])
+    per_gpu = [{"rank": int(r[0]), "device": int(r[1]),
+                "gib_s": round(w.nbytes * args.steps / r[2] / 2 ** 30, 2),
+                "pct_hbm": round(100.0 * w.nbytes * args.steps / r[2] / (PEAK_GBS * 1e9), 2),
+                "crc_xor": f"{int(r[3]):08x}"} for r in rows]
 
-    elapsed_max, _ = timed_run(dist, step, args.steps, args.warmup, engs)
-    total_bytes = nbytes * args.steps * world
-    value = aggregate_gibs(nbytes, args.steps, world, elapsed_max)
-    per_launch_s = launch_ms(step_on, engs[0], args.steps) / 1e3
-    graph_ms = launch_ms_graph(step_on, engs[0], args.steps) if getattr(step_on, "graphable", False) else None
-    kernel_s = graph_ms / 1e3 if graph_ms else per_launch_s
-    achieved = nbytes / kernel_s / 1e9
-    traffic = load_traffic(args.config, args.mode)
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -436,20 +597,34 @@ def main(argv=None):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 bytes, seeds in leveldb-rust_amd/synth.py)",
-        "config": dict(cfg, crc="crc32c, LevelDB-masked" if mode == m.MODE_C else "crc-32/iso-hdlc (crc32fast)",
-                       parallelism=f"{world} independent shard(s), no collective",
-                       streams=len(engs)),
-        "pct_hbm_peak": round(100.0 * (total_bytes / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_GBS, 4),
-                     "traffic": traffic, "launch_us": round(kernel_s * 1e6, 2),
-                     "stream_launch_us": round(per_launch_s * 1e6, 2),
-                     "timing": ("steps launches captured in one HIP graph, replayed on the engine stream, HIP events "
-                                "on that stream, median of 3 replays" if graph_ms else
-                                "one stream, launches back to back, HIP events on that stream, median of 3 windows")},
+        "config": dict(w.cfg, crc="crc32c, LevelDB-masked" if mode == m.MODE_C else "crc-32/iso-hdlc (crc32fast)",
+                       parallelism=f"{world} independent shard(s), no collective", streams=len(engs)),
+        "pct_hbm_peak": round(100.0 * (w.nbytes * args.steps * world / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
+        "per_gpu": per_gpu,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and sample is not None:
-        result["cpu_baseline"] = cpu_baseline(entry.load_oracle(), sample, args.mode, args.cpu_seconds, crcs)
+    if engs:
+        nl = w.launches(args.steps)
+        launch_s = gpu_ms / 1e3 / nl
+        bytes_per_launch = w.nbytes * args.steps / nl
+        achieved = bytes_per_launch / launch_s / 1e9
+        one_stream = len(engs) == 1 and not w.per_step_sync
+        result["roofline"] = {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(args.config, args.mode),
+            "bytes_per_launch": int(bytes_per_launch), "launches": nl, "launch_us": round(launch_s * 1e6, 2),
+            "timing": ("HIP events on the engine stream around the timed region, / launches" if one_stream else
+                       "HIP events on the first engine's stream around the timed region, / its steps; with "
+                       f"{len(engs)} streams the other engines' launches overlap it, so this is wall per step, "
+                       "not a single launch's duration"),
+            "profile": load_profile(args.config, args.mode),
+        }
+        if not one_stream:  # the first stream carried every len(engs)-th step
+            result["roofline"]["launch_us"] = round(gpu_ms / 1e3 / args.steps * 1e6, 2)
+    else:
+        result["roofline"] = None
+    if (rank == 0 and world == 1 and not args.no_cpu_baseline and w.sample is not None
+            and args.engine == "device"):
+        result["cpu_baseline"] = cpu_baseline(entry.load_oracle(), m, w.sample, args.mode, args.cpu_seconds, w.crcs)
     else:
         result["cpu_baseline"] = None
     if rank == 0:
@@ -460,7 +635,8 @@ def main(argv=None):
     for e in engs:
         e.close()
     dist.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

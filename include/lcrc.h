@@ -20,6 +20,8 @@
  *   lcrc_combine                        <- crc32fast::Hasher::combine (zlib crc32_combine)
  *   lcrc_batch / lcrc_batch_uniform     <- N independent calls of (3)/(4): one launch checksums and
  *                                          optionally verifies thousands of device-resident blocks
+ *   lcrc_batch_uniform_queue            <- the same for a queue of independent batches (e.g. every table of
+ *                                          a compaction's output), submitted as one launch per 32 batches
  *   lcrc_batch_host_uniform             <- the same starting and ending in host memory (pinned H2D,
  *                                          kernel, D2H, double-buffered)
  *   lcrc_wal_scan / lcrc_wal_scan_async <- the header parse + CRC verify of (2) for every physical record
@@ -138,6 +140,23 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
  * per-block expected CRCs. The 4 KiB / stride 4 KiB case is the single-pass fast path. */
 int lcrc_batch_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
                        const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch, void* stream);
+
+/* One batch of a queue (lcrc_batch_uniform_queue): n blocks of the queue's length at base + i*stride. */
+typedef struct lcrc_ujob {
+  const uint8_t* base;      /* device */
+  uint64_t n;               /* blocks */
+  const uint32_t* expected; /* device, nullable */
+  uint32_t* out_crc;        /* device, n words */
+  uint32_t* out_mismatch;   /* device, nullable, ceil(n/32) words, zeroed by the call */
+} lcrc_ujob;
+
+/* A queue of independent uniform batches (jobs: HOST array of njobs), each exactly as one
+ * lcrc_batch_uniform(ctx, jobs[k].base, jobs[k].n, length, stride, ...) call, in one submission. For the
+ * 4 KiB / stride 4 KiB layout the batches are streamed by ONE launch of the fast-path kernel per 32 jobs
+ * (the LDS table image and the end-of-launch spread paid once per launch, not once per batch); other
+ * layouts run batch by batch. Enqueued on `stream`, graph-capturable, nothing synchronized. */
+int lcrc_batch_uniform_queue(lcrc_ctx* ctx, const lcrc_ujob* jobs, size_t njobs, uint32_t length, uint64_t stride,
+                             void* stream);
 
 /* Same as lcrc_batch_uniform but base / expected / out_crc / out_mismatch are HOST pointers. Data is
  * staged through pinned buffers in chunks of chunk_bytes (0 = default) with H2D copies overlapping

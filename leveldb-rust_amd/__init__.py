@@ -70,6 +70,11 @@ class _WalRec(ctypes.Structure):
                 ("stop", ctypes.c_uint32)]
 
 
+class _UJob(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("n", ctypes.c_uint64), ("expected", ctypes.c_void_p),
+                ("out_crc", ctypes.c_void_p), ("out_mismatch", ctypes.c_void_p)]
+
+
 class _Hasher(ctypes.Structure):
     _fields_ = [("state", ctypes.c_uint32), ("mode", ctypes.c_int32), ("amount", ctypes.c_uint64)]
 
@@ -81,7 +86,7 @@ ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
-    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
+    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
     "lcrc_table_scan", "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
@@ -125,6 +130,7 @@ def lib():
     sig("lcrc_ctx_sync", i32, vp)
     sig("lcrc_batch", i32, vp, vp, u64, vp, sz, vp, vp, vp)
     sig("lcrc_batch_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, vp)
+    sig("lcrc_batch_uniform_queue", i32, vp, ctypes.POINTER(_UJob), sz, u32, u64, vp)
     sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
     sig("lcrc_wal_scan", i32, vp, vp, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp)
     sig("lcrc_wal_scan_async", i32, vp, vp, u64, vp, sz, vp, vp)
@@ -381,6 +387,14 @@ class Engine:
         _check(lib().lcrc_batch_uniform(self.ctx, _ptr(base), int(n), int(length), int(stride), _ptr(expected),
                                         _ptr(out_crc), _ptr(out_mismatch), stream), "lcrc_batch_uniform")
 
+    def batch_uniform_queue(self, jobs, length, stride, stream=None):
+        """lcrc_batch_uniform_queue: jobs = [(base, n, out_crc[, expected[, out_mismatch]])] (or the array
+        ujobs() made of them), each one lcrc_batch_uniform batch; the 4 KiB layout streams up to 32 of them per
+        launch."""
+        arr = jobs if isinstance(jobs, UJobs) else ujobs(jobs)
+        _check(lib().lcrc_batch_uniform_queue(self.ctx, arr.arr, arr.n, int(length), int(stride), stream),
+               "lcrc_batch_uniform_queue")
+
     def batch_host_uniform(self, base, n, length, stride, expected=None, chunk_bytes=0):
         """Host-resident input (numpy / PinnedBuffer). Returns (crc array, mismatch bitmap)."""
         bp, _nb, keep = (base.ptr, base.nbytes, base) if isinstance(base, PinnedBuffer) else _buf(base)
@@ -531,6 +545,23 @@ class Engine:
         crcs = out.download(np.uint32, n)
         bits = mm.download(np.uint32, (n + 31) // 32)
         return crcs, unpack_bits(bits, n)
+
+
+class UJobs:
+    """A prepared lcrc_ujob array (the queue's jobs, built once, submitted any number of times)."""
+
+    def __init__(self, jobs):
+        self.n = len(jobs)
+        self.arr = (_UJob * max(1, self.n))()
+        self.keep = list(jobs)
+        for k, j in enumerate(jobs):
+            exp = j[3] if len(j) > 3 else None
+            mm = j[4] if len(j) > 4 else None
+            self.arr[k] = _UJob(_ptr(j[0]), int(j[1]), _ptr(exp), _ptr(j[2]), _ptr(mm))
+
+
+def ujobs(jobs):
+    return UJobs(jobs)
 
 
 def unpack_bits(words, n):

@@ -1,6 +1,7 @@
 """Build the in-tree shared library `_build/liblcrc.so` (HIP kernels for gfx950 + C ABI + C++ host
 restatement) with hipcc. No JIT cache, no site-packages install: the .so lives next to this file so it
 travels to the GPU box with the repository snapshot."""
+import hashlib
 import os
 import subprocess
 import sys
@@ -21,12 +22,25 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
+def source_hash():
+    """sha256 (16 hex digits) of every source and header the library is built from, and of this recipe. It is
+    compiled into lcrc_version(), so a library can be matched to the tree it claims to come from (smoke()
+    checks the loaded library against the tree it runs in)."""
+    h = hashlib.sha256()
+    for name in sorted(SOURCES + HEADERS) + [os.path.basename(__file__)]:
+        path = __file__ if name == os.path.basename(__file__) else os.path.join(CSRC, name)
+        h.update(name.encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _stale():
+    """Rebuild unless the library carries this tree's source hash (mtimes do not survive a copy)."""
     if not os.path.exists(LIB):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    with open(LIB, "rb") as f:
+        return ("src " + source_hash()).encode() not in f.read()
 
 
 def build(force=False, verbose=False, extra_flags=()):
@@ -38,7 +52,7 @@ def build(force=False, verbose=False, extra_flags=()):
     # stalling on every load issued before it; k_windows reads it one walk later instead
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-           "-Wall", "-Wno-unused-result", "-o", tmp] + list(extra_flags) + [os.path.join(CSRC, s) for s in SOURCES]
+           "-Wall", "-Wno-unused-result", f'-DLCRC_SRC_HASH="{source_hash()}"', "-o", tmp] + list(extra_flags) + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -28,6 +28,8 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
                               const uint32_t* uexp, const uint32_t* gtab, uint32_t x4096, uint32_t poly,
                               uint32_t init, uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
                               const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st);
+hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
+                                     uint32_t fin, uint32_t flags, hipStream_t st);
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
@@ -193,7 +195,12 @@ hipStream_t pick_stream(lcrc_ctx* ctx, void* stream) { return stream ? (hipStrea
 extern "C" {
 
 const char* lcrc_last_error(void) { return g_last_error.c_str(); }
-const char* lcrc_version(void) { return "lcrc 0.1 (gfx950: k_windows slice4x32-LDS + DPP16 transpose, k_blocks row16)"; }
+#ifndef LCRC_SRC_HASH
+#define LCRC_SRC_HASH "unknown"
+#endif
+const char* lcrc_version(void) {
+  return "lcrc 0.2 src " LCRC_SRC_HASH " (gfx950: k_windows slice4x32-LDS + DPP16 transpose, queued batches, k_blocks row16)";
+}
 
 int lcrc_device_count(int* n) {
   if (!n) return LCRC_EINVAL;
@@ -399,6 +406,41 @@ int lcrc_batch_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t le
   if (rc) return rc;
   return batch_uniform_impl(ctx, base, n, length, stride, expected, out_crc, out_mismatch, pick_stream(ctx, stream),
                             true);
+}
+
+int lcrc_batch_uniform_queue(lcrc_ctx* ctx, const lcrc_ujob* jobs, size_t njobs, uint32_t length, uint64_t stride,
+                             void* stream) {
+  if (!ctx || (njobs && !jobs)) return LCRC_EINVAL;
+  for (size_t k = 0; k < njobs; ++k)
+    if ((jobs[k].n && (!jobs[k].base || !jobs[k].out_crc)) || (jobs[k].n > 1 && stride < length)) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  if (!(length == 4096 && stride == 4096)) {
+    for (size_t k = 0; k < njobs; ++k)
+      if ((rc = batch_uniform_impl(ctx, jobs[k].base, jobs[k].n, length, stride, jobs[k].expected, jobs[k].out_crc,
+                                   jobs[k].out_mismatch, st, true)))
+        return rc;
+    return LCRC_OK;
+  }
+  lcrc_qjob_host q[32];
+  size_t k = 0;
+  while (k < njobs) {
+    uint32_t m = 0;
+    for (; k < njobs && m < 32; ++k) {
+      const lcrc_ujob& j = jobs[k];
+      if (j.out_mismatch && j.n) HIPCHK(hipMemsetAsync(j.out_mismatch, 0, ((j.n + 31) / 32) * sizeof(uint32_t), st));
+      if (j.n == 0) continue;
+      q[m].base = j.base;
+      q[m].out = j.out_crc;
+      q[m].expected = j.expected;
+      q[m].mismatch = j.out_mismatch;
+      q[m].nblk = j.n;
+      ++m;
+    }
+    if (m) HIPCHK(lcrc_launch_windows_queue(ctx->grid_a, q, m, ctx->d_tab, ctx->fin4096, ctx->flags & LCRC_FLAG_MASK, st));
+  }
+  return LCRC_OK;
 }
 
 int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,

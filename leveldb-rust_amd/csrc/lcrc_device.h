@@ -49,3 +49,12 @@ struct lcrc_wal_rec_dev {  // == lcrc_wal_rec
 #define LCRC_WAL_STOP_TRAILER_DEV 0
 #define LCRC_WAL_STOP_BAD_LENGTH_DEV 1
 #define LCRC_WAL_STOP_ZERO_DEV 2
+
+// One batch of a queued uniform launch as the launcher receives it (lcrc_ujob minus the layout fields).
+struct lcrc_qjob_host {
+  const uint8_t* base;
+  uint32_t* out;
+  const uint32_t* expected;
+  uint32_t* mismatch;
+  uint64_t nblk;
+};

@@ -21,6 +21,7 @@
 //     record descriptors for k_blocks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "lcrc_device.h"
 
@@ -272,25 +273,25 @@ __device__ __forceinline__ uint32_t tree_level(const void* L, const Rot& R, uint
 
 // FINAL = false: out[t*64 + l] = walk(0, 256 B window l of region t) (raw partials for k_blocks)
 // FINAL = true : span = nblk * 4096; out[b] = crc of 4 KiB block b (xor fin, optional mask, verify)
-template <bool FINAL>
+template <bool FINAL, class Src>
 __device__ __forceinline__ void finish_region(const void* L, const Rot& R, uint32_t p, uint64_t t, uint32_t lane,
-                                              uint32_t* __restrict__ out, uint64_t nblk, uint32_t fin,
-                                              uint32_t flags, const uint32_t* __restrict__ expected, uint32_t ev,
-                                              uint32_t* __restrict__ mismatch) {
+                                              const Src& src, uint32_t fin, uint32_t flags, uint32_t ev) {
   if (!FINAL) {
-    out[t * 64 + lane] = p;
+    src.out_cur()[t * 64 + lane] = p;
     return;
   }
   p = tree_level<0>(L, R, p, lane);
   p = tree_level<1>(L, R, p, lane);
   p = tree_level<2>(L, R, p, lane);
   p = tree_level<3>(L, R, p, lane);
-  const uint64_t blk = t * 4 + (lane >> 4);
-  if ((lane & 15) == 0 && blk < nblk) {
+  bool ok;
+  const uint64_t blk = src.block_cur(t, lane >> 4, ok);
+  if ((lane & 15) == 0 && ok) {
     uint32_t crc = p ^ fin;
     if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
-    out[blk] = crc;
-    if (expected && mismatch && ev != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
+    src.out_cur()[blk] = crc;
+    uint32_t* mismatch = src.mismatch_cur();
+    if (src.expected_cur() && mismatch && ev != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
   }
 }
 
@@ -379,16 +380,103 @@ __device__ unsigned long long lcrc_dbg_stamp[4096 * 8];  // k_windows per wave: 
 __device__ unsigned long long lcrc_dbg_bstamp[8192 * 4];  // k_blocks per wave: entry, tables, first range, end
 #endif
 
-template <bool FINAL>
-__global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict__ base, uint64_t span,
-                                                      uint64_t nreg, const uint32_t* __restrict__ gtab,
-                                                      uint32_t* __restrict__ out, uint64_t nblk, uint32_t fin,
-                                                      uint32_t flags, const uint32_t* __restrict__ expected,
-                                                      uint32_t* __restrict__ mismatch) {
-  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
-  __shared__ uint32_t wg_ticket;
+// Where k_windows' regions come from. WinOne: one contiguous span (a batch, a file). WinQueue: a queue of
+// independent uniform 4 KiB batches (lcrc_batch_uniform_queue) numbered into one region space, so that one
+// launch streams them all: the LDS image is built and the per-CU end spread paid once per queue, not once
+// per batch. Both answer, for a region t: its buffer descriptor, and where its blocks' CRCs go. A wave's
+// regions increase monotonically (tickets), so the queue keeps a job cursor per region in flight: `cur` for
+// the region being walked and finished, `nxt` for the one being loaded.
+struct WinOne {
+  const uint8_t* base;
+  uint64_t span, nreg;
+  uint32_t* out;
+  uint64_t nblk;
+  const uint32_t* expected;
+  uint32_t* mismatch;
+  __device__ __forceinline__ uint64_t regions() const { return nreg; }
+  __device__ __forceinline__ void start_cur(uint64_t) {}
+  __device__ __forceinline__ void set_next(uint64_t) {}
+  __device__ __forceinline__ void rotate(uint64_t) {}
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_next(uint64_t t) const {
+    return region_rsrc(base, span, t, nreg);
+  }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_cur(uint64_t t) const {
+    return region_rsrc(base, span, t, nreg);
+  }
+  // block b of region t: (output slot, valid)
+  __device__ __forceinline__ uint64_t block_cur(uint64_t t, uint32_t q, bool& ok) const {
+    const uint64_t b = t * 4 + q;
+    ok = b < nblk;
+    return b;
+  }
+  __device__ __forceinline__ uint32_t* out_cur() const { return out; }
+  __device__ __forceinline__ const uint32_t* expected_cur() const { return expected; }
+  __device__ __forceinline__ uint32_t* mismatch_cur() const { return mismatch; }
+};
+
+constexpr int MAX_QJOBS = 32;  // batches per queued launch (kernel-argument space: 32 x 48 B)
+struct QJobDev {
+  const uint8_t* base;
+  uint32_t* out;
+  const uint32_t* expected;
+  uint32_t* mismatch;
+  uint64_t nblk;
+  uint64_t reg0;  // the job's first region in the launch's region space
+};
+struct QJobsArg {
+  QJobDev j[MAX_QJOBS];
+  uint64_t nreg;
+  uint32_t n;
+};
+
+struct WinQueue {
+  const QJobDev* J;
+  uint32_t nj;
+  uint64_t nreg;
+  uint32_t cur, nxt;
+  __device__ __forceinline__ uint64_t regions() const { return nreg; }
+  __device__ __forceinline__ uint32_t locate(uint64_t t, uint32_t from) const {
+    uint32_t j = from;
+    if (t >= nreg) return j;
+    while (j + 1 < nj && t >= J[j + 1].reg0) ++j;
+    return j;
+  }
+  __device__ __forceinline__ void start_cur(uint64_t t) { cur = nxt = locate(t, 0); }
+  __device__ __forceinline__ void set_next(uint64_t tn) { nxt = locate(tn, cur); }
+  __device__ __forceinline__ void rotate(uint64_t tnn) {  // region tn becomes current, tnn next
+    cur = nxt;
+    nxt = locate(tnn, nxt);
+  }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_job(uint64_t t, uint32_t j) const {
+    uint32_t nrec = 0;
+    const uint8_t* b = J[j].base;
+    if (t < nreg) {
+      const uint64_t local = t - J[j].reg0;
+      b += local * (uint64_t)REGION;
+      const uint64_t rem = J[j].nblk * 4096 - local * (uint64_t)REGION;
+      nrec = rem < (uint64_t)REGION ? (uint32_t)rem : (uint32_t)REGION;
+    }
+    return __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, (int)nrec, 0x00020000);
+  }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_next(uint64_t t) const { return rsrc_job(t, nxt); }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_cur(uint64_t t) const { return rsrc_job(t, cur); }
+  __device__ __forceinline__ uint64_t block_cur(uint64_t t, uint32_t q, bool& ok) const {
+    const uint64_t b = (t - J[cur].reg0) * 4 + q;
+    ok = b < J[cur].nblk;
+    return b;
+  }
+  __device__ __forceinline__ uint32_t* out_cur() const { return J[cur].out; }
+  __device__ __forceinline__ const uint32_t* expected_cur() const { return J[cur].expected; }
+  __device__ __forceinline__ uint32_t* mismatch_cur() const { return J[cur].mismatch; }
+};
+
+template <bool FINAL, class Src>
+__device__ __forceinline__ void windows_body(Src& src, const uint32_t* __restrict__ gtab, uint32_t fin,
+                                             uint32_t flags, uint32_t* L, uint32_t* wg_ticket_p) {
+  uint32_t& wg_ticket = *wg_ticket_p;
   const uint32_t lane = __lane_id();
   const uint32_t tid = threadIdx.x;
+  const uint64_t nreg = src.regions();
   const Share share = make_share(nreg);  // this workgroup's regions
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_entry = __builtin_amdgcn_s_memrealtime();
@@ -414,7 +502,8 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
   u32x4 va[8], vb[8];
   {
-    const __amdgpu_buffer_rsrc_t rs0 = region_rsrc(base, span, t, nreg);
+    src.start_cur(t);
+    const __amdgpu_buffer_rsrc_t rs0 = src.rsrc_cur(t);
     __builtin_amdgcn_sched_barrier(0);
     load_half(va, rs0, voff_a);
     __builtin_amdgcn_sched_barrier(0);  // issue order va, vb: the loop's vmcnt bookkeeping assumes it
@@ -433,6 +522,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   if (tid == 0) wg_ticket = A_THREADS / 64;  // tickets 0 .. waves-1 were the static first regions
   lds_barrier();
   uint64_t tn = take_region(&wg_ticket, share, lane);
+  src.set_next(tn);
 
   const Rot R = make_rot(lane);
 #ifdef LCRC_PROBE_CLOCK
@@ -445,13 +535,14 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   // Chain a of the second half continues from the first half's register value, so one Z64 join per
   // half is the only recombination inside a window.
   while (t != NO_REGION) {
-    const __amdgpu_buffer_rsrc_t rsn = region_rsrc(base, span, tn, nreg);
+    const __amdgpu_buffer_rsrc_t rsn = src.rsrc_next(tn);
     // expected values of this region's blocks, loaded ahead of the refills so that the verify at the
     // end of the iteration does not wait for them (vmcnt retires in issue order)
     uint32_t ev = 0;
-    if (FINAL && expected) {
-      const uint64_t blk = t * 4 + (lane >> 4);
-      if ((lane & 15) == 0 && blk < nblk) ev = expected[blk];
+    if (FINAL && src.expected_cur()) {
+      bool ok;
+      const uint64_t blk = src.block_cur(t, lane >> 4, ok);
+      if ((lane & 15) == 0 && ok) ev = src.expected_cur()[blk];
     }
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t x = walk_half(L, R, va, 0u, rsn, voff_a);
@@ -461,9 +552,10 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     __builtin_amdgcn_sched_barrier(0);
     const uint64_t tnn = take_region(&wg_ticket, share, lane);
     const uint32_t p = walk_half(L, R, vb, x, rsn, voff_b);
-    finish_region<FINAL>(L, R, p, t, lane, out, nblk, fin, flags, expected, ev, mismatch);
+    finish_region<FINAL>(L, R, p, t, lane, src, fin, flags, ev);
     t = tn;
     tn = tnn;
+    src.rotate(tnn);
   }
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -484,6 +576,27 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
     lcrc_dbg_stamp[gw * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 #endif
+}
+
+template <bool FINAL>
+__global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict__ base, uint64_t span,
+                                                      uint64_t nreg, const uint32_t* __restrict__ gtab,
+                                                      uint32_t* __restrict__ out, uint64_t nblk, uint32_t fin,
+                                                      uint32_t flags, const uint32_t* __restrict__ expected,
+                                                      uint32_t* __restrict__ mismatch) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
+  __shared__ uint32_t wg_ticket;
+  WinOne src{base, span, nreg, out, nblk, expected, mismatch};
+  windows_body<FINAL>(src, gtab, fin, flags, L, &wg_ticket);
+}
+
+// a queue of uniform 4 KiB batches in one launch (final CRCs only)
+__global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, const uint32_t* __restrict__ gtab,
+                                                        uint32_t fin, uint32_t flags) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
+  __shared__ uint32_t wg_ticket;
+  WinQueue src{jobs.j, jobs.n, jobs.nreg, 0, 0};
+  windows_body<true>(src, gtab, fin, flags, L, &wg_ticket);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2012,6 +2125,37 @@ hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, u
   else
     hipLaunchKernelGGL(lcrc_dev::k_windows<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg,
                        gtab, out, nblk, fin, flags, expected, mismatch);
+  return hipGetLastError();
+}
+
+// A queue of uniform 4 KiB batches (lcrc_batch_uniform_queue), at most MAX_QJOBS per launch: jobs[k] =
+// {base, out, expected, mismatch, nblk} (host array, copied into the kernel arguments).
+hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
+                                     uint32_t fin, uint32_t flags, hipStream_t st) {
+  using lcrc_dev::QJobsArg;
+  if (njobs == 0 || njobs > (uint32_t)lcrc_dev::MAX_QJOBS) return njobs ? hipErrorInvalidValue : hipSuccess;
+  QJobsArg a;
+  memset(&a, 0, sizeof(a));
+  uint64_t reg = 0;
+  uint32_t n = 0;
+  for (uint32_t k = 0; k < njobs; ++k) {
+    if (jobs[k].nblk == 0) continue;
+    a.j[n].base = jobs[k].base;
+    a.j[n].out = jobs[k].out;
+    a.j[n].expected = jobs[k].expected;
+    a.j[n].mismatch = jobs[k].mismatch;
+    a.j[n].nblk = jobs[k].nblk;
+    a.j[n].reg0 = reg;
+    reg += (jobs[k].nblk * 4096 + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
+    ++n;
+  }
+  if (n == 0) return hipSuccess;
+  a.n = n;
+  a.nreg = reg;
+  grid *= lcrc_dev::A_WG_PER_CU;
+  const uint64_t need = (reg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
+  const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
+  hipLaunchKernelGGL(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, a, gtab, fin, flags);
   return hipGetLastError();
 }
 

@@ -54,6 +54,8 @@ def lib():
     L.orc_crc_ranges.argtypes = [ctypes.c_int, vp, vp, vp, sz, vp]
     L.orc_crc_uniform_mt.restype = ctypes.c_double
     L.orc_crc_uniform_mt.argtypes = [ctypes.c_int, vp, sz, sz, sz, ctypes.c_int, vp]
+    L.orc_crc_ranges_mt.restype = ctypes.c_double
+    L.orc_crc_ranges_mt.argtypes = [ctypes.c_int, vp, vp, vp, sz, ctypes.c_int, vp]
     L.orc_splitmix_fill.restype = None
     L.orc_splitmix_fill.argtypes = [ctypes.c_uint64, vp, sz]
     _L = L
@@ -116,6 +118,22 @@ def crc_uniform_mt(data, nblocks, blen, stride, threads, algo):
     out = np.empty(nblocks, np.uint32)
     secs = lib().orc_crc_uniform_mt(algo, _p(a), nblocks, blen, stride, threads, _p(out))
     return out, secs
+
+
+def crc_ranges_mt(data, offsets, lengths, threads, algo):
+    """CRC of every range on `threads` threads (contiguous shares of about equal bytes); (crcs, seconds)."""
+    a = _arr(data)
+    offs = np.ascontiguousarray(offsets, np.uint64)
+    lens = np.ascontiguousarray(lengths, np.uint32)
+    out = np.empty(len(offs), np.uint32)
+    secs = lib().orc_crc_ranges_mt(algo, _p(a), _p(offs), _p(lens), len(offs), threads, _p(out))
+    return out, secs
+
+
+def mask_array(crcs):
+    """LevelDB mask of a u32 array (vectorised orc_mask): ((c >> 15) | (c << 17)) + 0xa282ead8."""
+    c = np.asarray(crcs, np.uint32).astype(np.uint64)
+    return ((((c >> 15) | (c << 17)) + 0xA282EAD8) & 0xFFFFFFFF).astype(np.uint32)
 
 
 def splitmix_bytes(seed, n):

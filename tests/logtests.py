@@ -98,7 +98,7 @@ def t_read_write(t):
     t.assert_read_eof()
 
 
-def t_many_blocks(t, n=100000):  # reference uses 1,000,000; scaled for test time
+def t_many_blocks(t, n=1000000):  # log.rs:535-545: 1,000,000 records
     for i in range(n):
         t.write(str(i))
     for i in range(n):

@@ -96,3 +96,10 @@ def test_scalar_extend_every_length_and_register(lcrc, orc):
         assert lcrc.extend(init, d, lcrc.MODE_REF) == zlib.crc32(d, init)
         if n < 5000:
             assert lcrc.extend(init, d, lcrc.MODE_C) == orc.crc(d, 1, init)
+
+
+def test_library_built_from_this_tree(lcrc):
+    """Build provenance: lcrc_version() carries the hash of the sources and recipe the library was built from,
+    and it is this tree's (smoke() makes the same check on the GPU box)."""
+    import __graft_entry__ as entry
+    assert f"src {entry.source_hash()}" in lcrc.lib().lcrc_version().decode()

@@ -431,3 +431,124 @@ def test_out_of_bounds_descriptors(lcrc, orc, path, monkeypatch):
     assert after[:64] == data[:64] and after[68:] == data[68:]
     assert int.from_bytes(after[64:68], "little") == orc.crc(data[:64], 1)
     eng.close()
+
+
+# ---- round 2: BASELINE configs[2] at full size, the queue API, unaligned bases, large logs ------------------
+@pytest.mark.parametrize("path", ["blocks", "ranges"])
+def test_config3_mixed_sstable_full_size(lcrc, orc, synth, path, monkeypatch):
+    """BASELINE configs[2] exactly as bench.py's mixed leg builds it: synth.mixed_sizes(256 MiB) (zipf 1.1 over
+    256 B-64 KiB) laid out by synth.sstable_layout, every block's trailer sealed with the oracle's CRC (REF:
+    the reference's crc32fast bytes; C: masked CRC-32C), a few blocks corrupted, then ONE lcrc_batch with
+    {off, n + 1, expect n + 1} (format.rs:162-171): every CRC equals the oracle's and exactly the corrupted
+    blocks are flagged. Both general paths (k_windows + k_blocks, k_ranges)."""
+    monkeypatch.setenv("LCRC_GENERAL", path)
+    sizes = synth.mixed_sizes(256 << 20)
+    offs, total = synth.sstable_layout(sizes)
+    lens = sizes.astype(np.uint64) + 1
+    base = synth.splitmix_bytes(synth.SEED_MIXED + 1000, total)
+    bad = [0, 1, 777, len(sizes) // 2, len(sizes) - 1]
+    for mode, flags, algo in ((0, 0, orc.ALGO_PCLMUL_REF), (1, lcrc.FLAG_MASK, orc.ALGO_SSE42_C)):
+        want, _ = orc.crc_ranges_mt(base, offs, lens, 8, algo)
+        if mode:
+            want = orc.mask_array(want)
+        f = base.copy()
+        slot = (offs + lens).astype(np.int64)
+        for k in range(4):
+            f[slot + k] = ((want >> np.uint32(8 * k)) & 0xFF).astype(np.uint8)
+        for i in bad:
+            f[int(offs[i] + lens[i] // 2)] ^= 0x40
+        eng = lcrc.Engine(0, mode, flags)
+        crcs, mm = eng.crc_ranges(f, offs, lens, expect_rel=lens.astype(np.int64))
+        eng.close()
+        got_want, _ = orc.crc_ranges_mt(f, offs, lens, 8, algo)
+        if mode:
+            got_want = orc.mask_array(got_want)
+        assert np.array_equal(crcs, got_want), (mode, np.nonzero(crcs != got_want)[0][:10])
+        assert np.nonzero(mm)[0].tolist() == bad
+        assert int(np.bitwise_xor.reduce(crcs)) == int(np.bitwise_xor.reduce(got_want))
+
+
+def test_uniform_queue_matches_batches(lcrc, orc):
+    """lcrc_batch_uniform_queue: 37 independent 4 KiB batches (ragged counts, an empty one, expected values
+    with injected mismatches, one at an unaligned address) in one call -- two launches of the queued kernel --
+    give exactly the CRCs and mismatch bits of 37 separate batches; a 4,000/4,100 B queue runs batch by batch."""
+    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
+    counts = [4096, 1, 3, 0, 5, 4097, 1000, 2] + [64] * 29
+    jobs, want, bad = [], [], []
+    keep = []
+    for k, n in enumerate(counts):
+        shift = 3 if k == 6 else 0
+        data = orc.splitmix_bytes(0x9000 + k, n * 4096)
+        w = orc.mask_array(orc.crc_ranges(data, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096), 1))
+        exp = w.copy()
+        flip = [i for i in (0, 2, n - 1) if 0 <= i < n][: 1 + k % 2]
+        exp[flip] ^= 0x10
+        buf = lcrc.DeviceBuffer.from_host(np.concatenate([np.full(shift, 0x5A, np.uint8), data]), pad=16)
+        out = lcrc.DeviceBuffer(max(4, 4 * n))
+        ed = lcrc.DeviceBuffer.from_host(exp) if n else lcrc.DeviceBuffer(4)
+        mm = lcrc.DeviceBuffer(max(4, 4 * ((n + 31) // 32)))
+        keep += [buf, out, ed, mm]
+        jobs.append((buf.ptr + shift, n, out, ed, mm))
+        want.append(w)
+        bad.append(sorted(set(flip)))
+    eng.batch_uniform_queue(jobs, 4096, 4096)
+    eng.sync()
+    for k, n in enumerate(counts):
+        assert np.array_equal(jobs[k][2].download(np.uint32, n), want[k]), k
+        bits = lcrc.unpack_bits(jobs[k][4].download(np.uint32, (n + 31) // 32), n) if n else np.zeros(0, bool)
+        assert np.nonzero(bits)[0].tolist() == bad[k], k
+    # another layout: the queue runs its batches one by one through lcrc_batch_uniform
+    data = orc.splitmix_bytes(0x9999, 300 * 4100)
+    w = orc.mask_array(orc.crc_ranges(data, np.arange(300, dtype=np.uint64) * 4100, np.full(300, 4000), 1))
+    buf = lcrc.DeviceBuffer.from_host(data)
+    outs = [lcrc.DeviceBuffer(4 * 300) for _ in range(3)]
+    eng.batch_uniform_queue([(buf, 300, o) for o in outs], 4000, 4100)
+    eng.sync()
+    for o in outs:
+        assert np.array_equal(o.download(np.uint32, 300), w)
+    eng.close()
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3, 5, 13])
+def test_fast_path_unaligned_base(lcrc, orc, engines, shift):
+    """The 4 KiB fast path (k_windows<true>) over a batch that starts at an arbitrary device address (an
+    mmap'd .ldb file's blocks need not be aligned): the same CRCs as the oracle, tail blocks included."""
+    n = 1003
+    data = orc.splitmix_bytes(0x7700 + shift, n * 4096)
+    dev = lcrc.DeviceBuffer.from_host(np.concatenate([np.full(shift, 0xA5, np.uint8), data]), pad=64)
+    for mode in MODES:
+        out = lcrc.DeviceBuffer(4 * n)
+        engines[mode].batch_uniform(dev.ptr + shift, n, 4096, 4096, out)
+        engines[mode].sync()
+        want = orc.crc_ranges(data, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096), mode)
+        assert np.array_equal(out.download(np.uint32, n), want), mode
+
+
+def test_wal_scan_hundreds_of_blocks(lcrc, orc, synth, engines):
+    """A log of ~275 32 KiB blocks (not a multiple of the parse's 64 blocks per workgroup): the per-workgroup
+    record counts, their prefix and the workgroup-0 total of k_wal_parse / k_wal_emit are all exercised. Every
+    (header, length, type) equals the reference reader's header walk (log.rs:204-279) and every crc the
+    oracle's, in both modes (REF: the stored crc32fast values verify; C: every record is flagged)."""
+    w = lcrc.LogWriter()
+    payload = synth.splitmix_bytes(0x4444, 1 << 17)
+    for n in synth.wal_lengths(9_000_000, seed=0x4445):
+        w.add_record(payload[:n] if n <= len(payload) else np.resize(payload, n))
+    data = w.contents()
+    nblocks = (len(data) + 32767) // 32768
+    assert nblocks > 200 and nblocks % 64 != 0
+    dev = lcrc.DeviceBuffer.from_host(np.frombuffer(data, np.uint8))
+    want = _wal_expect(orc, data)
+    h = np.array([x[0] for x in want], np.uint64)
+    ln = np.array([x[1] for x in want], np.uint64)
+    for mode in MODES:
+        got = engines[mode].wal_scan(dev, len(data))
+        assert [(int(r["header"]), int(r["length"]), int(r["type"])) for r in got] == want
+        crc = orc.crc_ranges(data, h + 6, ln + 1, mode)
+        assert np.array_equal(got["crc"], crc)
+        assert (got["status"] == (0 if mode == 0 else 1)).all()
+
+
+def test_wal_many_blocks_reference_size_on_device(lcrc, engines):
+    """The reference's test_many_blocks at its own size (log.rs:535-545): 1,000,000 records written, every
+    one read back through the device-verified BatchLogReader."""
+    logtests.t_many_blocks(logtests.Tester(lcrc, _batch_reader(lcrc, engines)), 1000000)

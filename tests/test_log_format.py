@@ -17,7 +17,7 @@ def test_reference_scenario(tester, scenario):
 
 
 def test_many_blocks(tester):
-    logtests.t_many_blocks(tester, 20000)
+    logtests.t_many_blocks(tester)  # the reference's 1,000,000 records (log.rs:535-545)
 
 
 def test_random_read(tester):

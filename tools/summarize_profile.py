@@ -56,6 +56,22 @@ def main(outdir, rnd, config, mode):
         traffic[k] = {"hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                       "fetch_size_kib_raw": sum(vals) / len(vals), "launches_sampled": len(vals)}
     summary["traffic"] = traffic
+    # the roofline fraction this profile implies: the bench line of the SAME command (--extra-out) gives the
+    # algorithmic bytes per launch; the dominant kernel's average duration comes from the kernel trace
+    bj = os.path.join(outdir, "bench.json")
+    if summary["kernels"] and os.path.exists(bj):
+        with open(bj) as f:
+            line = json.load(f)
+        dom = max(summary["kernels"].items(), key=lambda kv: kv[1]["total_ns"])
+        bpl = (line.get("roofline") or {}).get("bytes_per_launch")
+        if bpl:
+            summary["kernel"] = dom[0]
+            summary["avg_us"] = round(dom[1]["avg_ns"] / 1e3, 3)
+            summary["bytes_per_launch"] = bpl
+            summary["frac"] = round(bpl / dom[1]["avg_ns"] / 8000.0, 4)
+            summary["bench_line"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
+                                     "frac": line["roofline"]["frac"], "launch_us": line["roofline"]["launch_us"],
+                                     "launches": line["roofline"].get("launches")}
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     # the dominant kernel's traffic for bench.py
