@@ -168,6 +168,13 @@ int upload_tables(int mode, uint32_t** d_tab) {
                                  : TAB_ZWIN + (t - 8) * 256;              // Z256, Z512, Z1024
     for (int i = 0; i < 8; ++i) tab[TAB_COLS + t * 8 + i] = tab[src + (1u << i)];
   }
+  // the queued fast path's per-window shifts to the block end: Z_{256 k} of byte q, by columns
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t xp = lcrc::x8n(256ull * k, poly);
+    for (int q = 0; q < 4; ++q)
+      for (int i = 0; i < 8; ++i)
+        tab[TAB_SCOLS + (4 * k + q) * 8 + i] = lcrc::multmodp(xp, 1u << (8 * q + i), poly);
+  }
   // inverses of the zero-byte shifts for k_ranges: x^-1 = (P - 1) / x, i.e. (poly << 1) | 1 reflected
   const uint32_t xinv = (poly << 1) | 1u;
   if (lcrc::multmodp(xinv, 1u << 30, poly) != (1u << 31)) return LCRC_EINVAL;  // x * x^-1 == 1

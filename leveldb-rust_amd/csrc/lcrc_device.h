@@ -20,7 +20,9 @@ enum : int {
                       // S0 T_p (p = 0..3), S1 Z64[3 - p], then Z256, Z512, Z1024 in TAB_ZWIN word order
   TAB_INV = 10400,    // x^(-8k) mod P for k = 0..4096 (k_ranges: undo the zero padding of a last chunk)
   TAB_XCH = 14497,    // x^(8 * 4096 * k) mod P for k = 0..4095 (k_ranges: place a shared range's chunk)
-  TAB_TOTAL = 18600,
+  TAB_SCOLS = 18600,  // the queued fast path's block shifts as columns: Z_{256 k}, k = 0..15, byte position q =
+                      // 0..3 (table index 4 k + q, entry b = Z_{256 k}(b << 8 q)), 8 columns each
+  TAB_TOTAL = 19112,
 };
 
 struct lcrc_desc_dev {  // == lcrc_desc

@@ -139,9 +139,8 @@ __device__ __forceinline__ uint32_t zlook(const void* L, uint32_t tab_byte_off, 
 //          move is also the select (one instruction per register)
 //   bit 4: v_permlane16_swap (odd rows of a <-> even rows of b), bit 5: v_permlane32_swap (one
 //          instruction per register pair)
-template <int LB>
+template <int LB, int D = 1 << (LB - 3)>  // D: the register-index bit paired with lane bit LB
 __device__ __forceinline__ void transpose_stage(u32x4 (&v)[8]) {
-  constexpr int D = 1 << (LB - 3);  // register-index bit paired with lane bit LB
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (j & D) continue;
@@ -197,28 +196,50 @@ __shared__ u32x4 lcrc_probe_tile[256];
 #define LCRC_REFILL(rs, off) __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LCRC_LOAD_AUX)
 #endif
 
+// Two load layouts of a 16 KiB region (half h = bytes [128 h, 128 h + 128) of every 256 B window):
+//  L8 (k_ranges): instruction j, lane l = 8c + k reads region byte 2048 j + 256 k + 128 h + 16 c -- eight
+//      whole 128 B lines per instruction; an 8x8 transpose (lane bits 3..5 x register bits 0..2) follows.
+//  L4 (k_windows): instruction j, lane l = 16b + a reads byte 256 (a + 16 (j & 3)) + 128 h + 16 ((j & 4) | b)
+//      -- the four lanes a, a+16, a+32, a+48 read one 64 B half-line, sixteen half-lines per instruction (the
+//      same sixteen 64 B units as L8's eight lines); a 4x4 transpose (lane bits 4, 5 x register bits 0, 1: two
+//      permlane swaps per register pair, no DPP stage) leaves lane l with half h of window l, as L8 does.
+template <bool L4>
+__device__ __forceinline__ uint32_t lane_voff(uint32_t lane, uint32_t h) {
+  return L4 ? 256u * (lane & 15) + 16u * ((lane >> 4) & 3) + 128u * h : 256u * (lane & 7) + 16u * (lane >> 3) + 128u * h;
+}
+template <bool L4>
+__device__ __forceinline__ constexpr uint32_t j_off(int j) {
+  return L4 ? 4096u * (j & 3) + 16u * (j & 4) : 2048u * j;
+}
+
+template <bool L4 = false>
 __device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j * 2048);
+  for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j_off<L4>(j));
 }
 
 // Transpose + walk one half-tile already in registers, starting chain a from register value `init`:
 // returns walk(init, 128 B half of window l). As each register pair is consumed it is refilled from `rs`
 // (the same half of the next region), so every wave keeps between one and two half-tiles in flight.
-template <bool REFILL = true>
+template <bool REFILL = true, bool L4 = false>
 __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4 (&v)[8], uint32_t init,
                                               __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
 #ifndef LCRC_PROBE_NOTRANSPOSE  // ablation build: walk the pieces as loaded (wrong CRCs, timing only)
-  transpose_stage<3>(v);
-  transpose_stage<4>(v);
-  transpose_stage<5>(v);
+  if constexpr (L4) {
+    transpose_stage<4, 1>(v);
+    transpose_stage<5, 2>(v);
+  } else {
+    transpose_stage<3>(v);
+    transpose_stage<4>(v);
+    transpose_stage<5>(v);
+  }
 #endif
 #ifdef LCRC_PROBE_NOWALK  // ablation build: fold the data with xor only
   uint32_t p = init;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     p ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-    v[j] = LCRC_REFILL(rs, voff + j * 2048);
+    v[j] = LCRC_REFILL(rs, voff + j_off<L4>(j));
   }
   return p;
 #else
@@ -241,8 +262,8 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     xa = step4x(L, R, xa, j < 3 ? v[j + 1].x : 0u);
     xb = step4x(L, R, xb, j < 3 ? v[5 + j].x : 0u);
     if (REFILL && j - D >= 0) {
-      v[j - D] = LCRC_REFILL(rs, voff + (j - D) * 2048);
-      v[4 + j - D] = LCRC_REFILL(rs, voff + (4 + j - D) * 2048);
+      v[j - D] = LCRC_REFILL(rs, voff + j_off<L4>(j - D));
+      v[4 + j - D] = LCRC_REFILL(rs, voff + j_off<L4>(4 + j - D));
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the refill here: hipcc would otherwise sink it past the walk
   }
@@ -250,8 +271,8 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
 #pragma unroll
   for (int j = 4 - D; j < 4; ++j) {
     if (!REFILL) break;
-    v[j] = LCRC_REFILL(rs, voff + j * 2048);
-    v[4 + j] = LCRC_REFILL(rs, voff + (4 + j) * 2048);
+    v[j] = LCRC_REFILL(rs, voff + j_off<L4>(j));
+    v[4 + j] = LCRC_REFILL(rs, voff + j_off<L4>(4 + j));
   }
   return res;
 #endif
@@ -273,25 +294,39 @@ __device__ __forceinline__ uint32_t tree_level(const void* L, const Rot& R, uint
 
 // FINAL = false: out[t*64 + l] = walk(0, 256 B window l of region t) (raw partials for k_blocks)
 // FINAL = true : span = nblk * 4096; out[b] = crc of 4 KiB block b (xor fin, optional mask, verify)
-template <bool FINAL, class Src>
-__device__ __forceinline__ void finish_region(const void* L, const Rot& R, uint32_t p, uint64_t t, uint32_t lane,
-                                              const Src& src, uint32_t fin, uint32_t flags, uint32_t ev) {
+template <bool FINAL, bool SHIFT, class Src>
+__device__ __forceinline__ void finish_region(const void* L, const Rot& R, const Rot& SR, uint32_t p, uint64_t t,
+                                              uint32_t h, uint32_t lane, const Src& src, uint32_t fin,
+                                              uint32_t flags, uint32_t ev) {
   if (!FINAL) {
-    src.out_cur()[t * 64 + lane] = p;
+    src.out_of(h)[t * 64 + lane] = p;
     return;
   }
-  p = tree_level<0>(L, R, p, lane);
-  p = tree_level<1>(L, R, p, lane);
-  p = tree_level<2>(L, R, p, lane);
-  p = tree_level<3>(L, R, p, lane);
+  if constexpr (SHIFT) {
+    // window g's register moved to the block end (Z_{256 (15 - g)}), then the 16 windows xored into lane 0
+    const uint32_t a0 = lds_u32(L, __builtin_amdgcn_perm(SR.b[0], p, SR.s[0]));
+    const uint32_t a1 = lds_u32(L, __builtin_amdgcn_perm(SR.b[1], p, SR.s[1]));
+    const uint32_t a2 = lds_u32(L, __builtin_amdgcn_perm(SR.b[2], p, SR.s[2]));
+    const uint32_t a3 = lds_u32(L, __builtin_amdgcn_perm(SR.b[3], p, SR.s[3]));
+    p = xor3(a0, a1, a2 ^ a3);
+    p ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x101, 0xF, 0xF, false);  // row_shl:1
+    p ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x102, 0xF, 0xF, false);  // row_shl:2
+    p ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x104, 0xF, 0xF, false);  // row_shl:4
+    p ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x108, 0xF, 0xF, false);  // row_shl:8
+  } else {
+    p = tree_level<0>(L, R, p, lane);
+    p = tree_level<1>(L, R, p, lane);
+    p = tree_level<2>(L, R, p, lane);
+    p = tree_level<3>(L, R, p, lane);
+  }
   bool ok;
-  const uint64_t blk = src.block_cur(t, lane >> 4, ok);
+  const uint64_t blk = src.block(t, h, lane >> 4, ok);
   if ((lane & 15) == 0 && ok) {
     uint32_t crc = p ^ fin;
     if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
-    src.out_cur()[blk] = crc;
-    uint32_t* mismatch = src.mismatch_cur();
-    if (src.expected_cur() && mismatch && ev != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
+    src.out_of(h)[blk] = crc;
+    uint32_t* mismatch = src.mismatch_of(h);
+    if (src.expected_of(h) && mismatch && ev != crc) atomicOr(&mismatch[blk >> 5], 1u << (blk & 31));
   }
 }
 
@@ -348,15 +383,70 @@ __device__ __forceinline__ uint32_t lin8(const uint32_t* __restrict__ col, uint3
   return v;
 }
 
+// The queued kernel's LDS image instead keeps, from 64 KiB on, the per-window block shifts: row e (256 B)
+// holds in dword c = 4 k + p the entry Z_{256 k}(e << 8 (3 - p)) (k = 0..15, p = 0..3): 64 byte tables, 288
+// wave passes in all. Window g of a block row is shifted by Z_{256 (15 - g)} to the block end, and the
+// rotated lookup order (the slice sets' q = (lane >> 3) & 3) keeps the 32 lanes of an LDS read group on
+// distinct banks: lanes g and g + 8 share 4 k mod 32 but differ in q, as do the two rows of the group.
+constexpr int A_SHIFT = 65536;       // LDS offset of the block shifts (queued kernel)
+constexpr int AQ_LDS_BYTES = 131072;
+
+// Lane c of every wave owns column c (table 4 k + p); wave w writes rows e = gray(32 w + i), i = 0..31, so one
+// store instruction fills one 256 B row (conflict-free) and consecutive rows differ in one index bit: each
+// entry after the first is ONE xor with a column (the table is linear in e). `cols` = the lane's 8 columns,
+// loaded before the first region's HBM loads are issued (they return first).
+struct ShiftCols {
+  u32x4 lo, hi;
+};
+__device__ __forceinline__ ShiftCols load_shift_cols(const uint32_t* __restrict__ gtab, uint32_t lane) {
+  const uint32_t c = lane;
+  const uint32_t src = (c & ~3u) + (3 - (c & 3));  // TAB_SCOLS table 4 k + byte position (3 - p)
+  const u32x4* q = (const u32x4*)(gtab + TAB_SCOLS + src * 8);
+  return ShiftCols{q[0], q[1]};
+}
+__device__ __forceinline__ void build_shift_tables(uint32_t* L, const ShiftCols& sc, uint32_t wv, uint32_t lane) {
+  constexpr int WAVES = A_THREADS / 64;
+  constexpr int PER = 256 / WAVES;
+  static_assert(PER == 32, "rows per wave");
+  const uint32_t col[8] = {sc.lo.x, sc.lo.y, sc.lo.z, sc.lo.w, sc.hi.x, sc.hi.y, sc.hi.z, sc.hi.w};
+  const uint32_t n0 = wv * PER;  // uniform; gray(n0) = its bits 4..7
+  const uint32_t g0 = n0 ^ (n0 >> 1);
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 4; i < 8; ++i)
+    if ((g0 >> i) & 1) v ^= col[i];
+  L[A_SHIFT / 4 + g0 * 64 + lane] = v;
+#pragma unroll
+  for (int i = 1; i < PER; ++i) {
+    v ^= col[__builtin_ctz(i)];  // gray(n) = gray(n - 1) ^ (1 << ctz(n)); ctz(n0 + i) = ctz(i)
+    const uint32_t n = n0 + i;
+    L[A_SHIFT / 4 + (n ^ (n >> 1)) * 64 + lane] = v;
+  }
+}
+
+// lane-dependent lookup parameters of the block shifts: table 4 k + p, k = 15 - (lane & 15)
+__device__ __forceinline__ Rot make_shift_rot(uint32_t lane) {
+  Rot R;
+  const uint32_t k = 15 - (lane & 15), q = (lane >> 3) & 3;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t p = (i + q) & 3;
+    R.b[i] = (1u << 16) | ((4 * k + p) << 2);
+    R.s[i] = 0x0C060004u | ((3 - p) << 8);
+  }
+  return R;
+}
+
 // k_windows' LDS image built from the column block TAB_COLS. 80 wave passes of 64 entries each, one
 // byte table per pass (uniform columns -> scalar loads): passes 0..31 the replicated sets (set s,
 // position p), passes 32..79 the tree's Z256/Z512/Z1024 (same word order as the global TAB_ZWIN).
+template <bool TREE = true>
 __device__ __forceinline__ void build_tables(uint32_t* L, const uint32_t* __restrict__ gtab, uint32_t wv,
                                              uint32_t lane) {
   constexpr int WAVES = A_THREADS / 64;
   static_assert(80 % WAVES == 0, "passes per wave");
 #pragma unroll
-  for (int k = 0; k < 80 / WAVES; ++k) {
+  for (int k = 0; k < (TREE ? 80 : 32) / WAVES; ++k) {
     const uint32_t P = wv + WAVES * k;  // uniform
     const uint32_t e = ((P & 3) << 6) | lane;
     if (P < 32) {
@@ -382,10 +472,10 @@ __device__ unsigned long long lcrc_dbg_bstamp[8192 * 4];  // k_blocks per wave: 
 
 // Where k_windows' regions come from. WinOne: one contiguous span (a batch, a file). WinQueue: a queue of
 // independent uniform 4 KiB batches (lcrc_batch_uniform_queue) numbered into one region space, so that one
-// launch streams them all: the LDS image is built and the per-CU end spread paid once per queue, not once
-// per batch. Both answer, for a region t: its buffer descriptor, and where its blocks' CRCs go. A wave's
-// regions increase monotonically (tickets), so the queue keeps a job cursor per region in flight: `cur` for
-// the region being walked and finished, `nxt` for the one being loaded.
+// launch streams them all: the LDS image is built and the per-CU end spread paid once per launch, not once
+// per batch. Both answer, for a region t: its buffer descriptor, and where its blocks' CRCs go. A region's
+// job is found from a wave-uniform handle `find(t, hint)`; a wave's regions increase monotonically
+// (tickets), so the previous region's handle is always a valid hint.
 struct WinOne {
   const uint8_t* base;
   uint64_t span, nreg;
@@ -394,24 +484,19 @@ struct WinOne {
   const uint32_t* expected;
   uint32_t* mismatch;
   __device__ __forceinline__ uint64_t regions() const { return nreg; }
-  __device__ __forceinline__ void start_cur(uint64_t) {}
-  __device__ __forceinline__ void set_next(uint64_t) {}
-  __device__ __forceinline__ void rotate(uint64_t) {}
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_next(uint64_t t) const {
+  __device__ __forceinline__ uint32_t find(uint64_t, uint32_t) const { return 0; }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(uint64_t t, uint32_t) const {
     return region_rsrc(base, span, t, nreg);
   }
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_cur(uint64_t t) const {
-    return region_rsrc(base, span, t, nreg);
-  }
-  // block b of region t: (output slot, valid)
-  __device__ __forceinline__ uint64_t block_cur(uint64_t t, uint32_t q, bool& ok) const {
+  // block q of region t: (output slot, valid)
+  __device__ __forceinline__ uint64_t block(uint64_t t, uint32_t, uint32_t q, bool& ok) const {
     const uint64_t b = t * 4 + q;
     ok = b < nblk;
     return b;
   }
-  __device__ __forceinline__ uint32_t* out_cur() const { return out; }
-  __device__ __forceinline__ const uint32_t* expected_cur() const { return expected; }
-  __device__ __forceinline__ uint32_t* mismatch_cur() const { return mismatch; }
+  __device__ __forceinline__ uint32_t* out_of(uint32_t) const { return out; }
+  __device__ __forceinline__ const uint32_t* expected_of(uint32_t) const { return expected; }
+  __device__ __forceinline__ uint32_t* mismatch_of(uint32_t) const { return mismatch; }
 };
 
 constexpr int MAX_QJOBS = 32;  // batches per queued launch (kernel-argument space: 32 x 48 B)
@@ -433,21 +518,14 @@ struct WinQueue {
   const QJobDev* J;
   uint32_t nj;
   uint64_t nreg;
-  uint32_t cur, nxt;
   __device__ __forceinline__ uint64_t regions() const { return nreg; }
-  __device__ __forceinline__ uint32_t locate(uint64_t t, uint32_t from) const {
+  __device__ __forceinline__ uint32_t find(uint64_t t, uint32_t from) const {
     uint32_t j = from;
     if (t >= nreg) return j;
     while (j + 1 < nj && t >= J[j + 1].reg0) ++j;
     return j;
   }
-  __device__ __forceinline__ void start_cur(uint64_t t) { cur = nxt = locate(t, 0); }
-  __device__ __forceinline__ void set_next(uint64_t tn) { nxt = locate(tn, cur); }
-  __device__ __forceinline__ void rotate(uint64_t tnn) {  // region tn becomes current, tnn next
-    cur = nxt;
-    nxt = locate(tnn, nxt);
-  }
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_job(uint64_t t, uint32_t j) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(uint64_t t, uint32_t j) const {
     uint32_t nrec = 0;
     const uint8_t* b = J[j].base;
     if (t < nreg) {
@@ -458,20 +536,36 @@ struct WinQueue {
     }
     return __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, (int)nrec, 0x00020000);
   }
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_next(uint64_t t) const { return rsrc_job(t, nxt); }
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_cur(uint64_t t) const { return rsrc_job(t, cur); }
-  __device__ __forceinline__ uint64_t block_cur(uint64_t t, uint32_t q, bool& ok) const {
-    const uint64_t b = (t - J[cur].reg0) * 4 + q;
-    ok = b < J[cur].nblk;
+  __device__ __forceinline__ uint64_t block(uint64_t t, uint32_t j, uint32_t q, bool& ok) const {
+    const uint64_t b = (t - J[j].reg0) * 4 + q;
+    ok = b < J[j].nblk;
     return b;
   }
-  __device__ __forceinline__ uint32_t* out_cur() const { return J[cur].out; }
-  __device__ __forceinline__ const uint32_t* expected_cur() const { return J[cur].expected; }
-  __device__ __forceinline__ uint32_t* mismatch_cur() const { return J[cur].mismatch; }
+  __device__ __forceinline__ uint32_t* out_of(uint32_t j) const { return J[j].out; }
+  __device__ __forceinline__ const uint32_t* expected_of(uint32_t j) const { return J[j].expected; }
+  __device__ __forceinline__ uint32_t* mismatch_of(uint32_t j) const { return J[j].mismatch; }
 };
 
+// expected values of region t's blocks (verify), loaded ahead of the refills that follow so the compare at
+// the end of the region does not wait for them (vmcnt retires in issue order)
 template <bool FINAL, class Src>
-__device__ __forceinline__ void windows_body(Src& src, const uint32_t* __restrict__ gtab, uint32_t fin,
+__device__ __forceinline__ uint32_t expect_of(const Src& src, uint64_t t, uint32_t h, uint32_t lane) {
+  uint32_t ev = 0;
+  if (FINAL && src.expected_of(h)) {
+    bool ok;
+    const uint64_t blk = src.block(t, h, lane >> 4, ok);
+    if ((lane & 15) == 0 && ok) ev = src.expected_of(h)[blk];
+  }
+  return ev;
+}
+
+#ifndef LCRC_KW_L4
+#define LCRC_KW_L4 0
+#endif
+constexpr bool KW_L4 = LCRC_KW_L4;  // k_windows' load layout (see lane_voff)
+
+template <bool FINAL, bool SHIFT, class Src>
+__device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __restrict__ gtab, uint32_t fin,
                                              uint32_t flags, uint32_t* L, uint32_t* wg_ticket_p) {
   uint32_t& wg_ticket = *wg_ticket_p;
   const uint32_t lane = __lane_id();
@@ -497,66 +591,123 @@ __device__ __forceinline__ void windows_body(Src& src, const uint32_t* __restric
   // 1, 2, 4, .., 128 of the global image), read with SCALAR loads -- vector-memory returns reach a CU in
   // issue order, and a table read through the vector path would wait for every HBM load issued before it.
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t voff_a = lane_voff<KW_L4>(lane, 0), voff_b = lane_voff<KW_L4>(lane, 1);
+  ShiftCols scols{};
+  if (SHIFT) scols = load_shift_cols(gtab, lane);  // issued before the region loads: returns first
+#ifndef LCRC_DEEP
   uint64_t t = share.region(wv);
-  // lane (k, c) = (lane & 7, lane >> 3) reads piece 16*k + 8*h + c of every 2 KiB of the region
-  const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
+  uint32_t ht = src.find(t, 0);
   u32x4 va[8], vb[8];
   {
-    src.start_cur(t);
-    const __amdgpu_buffer_rsrc_t rs0 = src.rsrc_cur(t);
+    const __amdgpu_buffer_rsrc_t rs0 = src.rsrc(t, ht);
     __builtin_amdgcn_sched_barrier(0);
-    load_half(va, rs0, voff_a);
+    load_half<KW_L4>(va, rs0, voff_a);
     __builtin_amdgcn_sched_barrier(0);  // issue order va, vb: the loop's vmcnt bookkeeping assumes it
-    load_half(vb, rs0, voff_b);
+    load_half<KW_L4>(vb, rs0, voff_b);
     __builtin_amdgcn_sched_barrier(0);
   }
+#else
+  // deep pipeline: two regions (four half-tiles, 128 VGPRs) in flight per wave; the first two regions of
+  // wave w are static (w and w + waves), tickets start after them
+  constexpr uint32_t NW = A_THREADS / 64;
+  uint64_t t = share.region(wv), t1 = share.region(wv + NW);
+  uint32_t ht = src.find(t, 0), h1 = src.find(t1, ht);
+  u32x4 va[8], vb[8], vc[8], vd[8];
+  {
+    const __amdgpu_buffer_rsrc_t rs0 = src.rsrc(t, ht);
+    const __amdgpu_buffer_rsrc_t rs1 = src.rsrc(t1, h1);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half<KW_L4>(va, rs0, voff_a);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half<KW_L4>(vb, rs0, voff_b);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half<KW_L4>(vc, rs1, voff_a);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half<KW_L4>(vd, rs1, voff_b);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
 #endif
 #ifndef LCRC_PROBE_NOTABLES  // ablation build: no LDS image (wrong CRCs, timing only)
-  build_tables(L, gtab, wv, lane);
+  build_tables<!SHIFT>(L, gtab, wv, lane);
+  if (SHIFT) build_shift_tables(L, scols, wv, lane);
 #endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifndef LCRC_DEEP
   if (tid == 0) wg_ticket = A_THREADS / 64;  // tickets 0 .. waves-1 were the static first regions
+#else
+  if (tid == 0) wg_ticket = 2 * NW;
+#endif
   lds_barrier();
-  uint64_t tn = take_region(&wg_ticket, share, lane);
-  src.set_next(tn);
-
   const Rot R = make_rot(lane);
+  const Rot SR = SHIFT ? make_shift_rot(lane) : R;
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
+#ifndef LCRC_DEEP
+  uint64_t tn = take_region(&wg_ticket, share, lane);
+  uint32_t hn = src.find(tn, ht);
   // tn = the region the refills load (ticket taken after the prologue or in the previous iteration);
   // the ticket for the one after is taken between the two walks.
   // va/vb hold the two halves of region t; walking a half refills it with the same half of region tn.
   // Chain a of the second half continues from the first half's register value, so one Z64 join per
   // half is the only recombination inside a window.
   while (t != NO_REGION) {
-    const __amdgpu_buffer_rsrc_t rsn = src.rsrc_next(tn);
-    // expected values of this region's blocks, loaded ahead of the refills so that the verify at the
-    // end of the iteration does not wait for them (vmcnt retires in issue order)
-    uint32_t ev = 0;
-    if (FINAL && src.expected_cur()) {
-      bool ok;
-      const uint64_t blk = src.block_cur(t, lane >> 4, ok);
-      if ((lane & 15) == 0 && ok) ev = src.expected_cur()[blk];
-    }
+    const __amdgpu_buffer_rsrc_t rsn = src.rsrc(tn, hn);
+    const uint32_t ev = expect_of<FINAL>(src, t, ht, lane);
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t x = walk_half(L, R, va, 0u, rsn, voff_a);
+    const uint32_t x = walk_half<true, KW_L4>(L, R, va, 0u, rsn, voff_a);
 #ifdef LCRC_PROBE_CLOCK
     if (!s_first) s_first = __builtin_amdgcn_s_memrealtime();
 #endif
     __builtin_amdgcn_sched_barrier(0);
     const uint64_t tnn = take_region(&wg_ticket, share, lane);
-    const uint32_t p = walk_half(L, R, vb, x, rsn, voff_b);
-    finish_region<FINAL>(L, R, p, t, lane, src, fin, flags, ev);
+    const uint32_t p = walk_half<true, KW_L4>(L, R, vb, x, rsn, voff_b);
+    finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
     t = tn;
+    ht = hn;
     tn = tnn;
-    src.rotate(tnn);
+    hn = src.find(tnn, hn);
   }
+#else
+  // va/vb: region t, vc/vd: region t1; walking a half refills it with the same half of the region two
+  // ahead (t2 for va/vb, t3 for vc/vd): a refill has three half-walks to arrive instead of one
+  uint64_t t2 = take_region(&wg_ticket, share, lane);
+  uint32_t h2 = src.find(t2, h1);
+  while (t != NO_REGION) {
+    {
+      const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t2, h2);
+      const uint32_t ev = expect_of<FINAL>(src, t, ht, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t x = walk_half<true, KW_L4>(L, R, va, 0u, rsn, voff_a);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t p = walk_half<true, KW_L4>(L, R, vb, x, rsn, voff_b);
+      finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
+    }
+    const uint64_t t3 = take_region(&wg_ticket, share, lane);
+    const uint32_t h3 = src.find(t3, h2);
+    if (t1 != NO_REGION) {
+      const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t3, h3);
+      const uint32_t ev = expect_of<FINAL>(src, t1, h1, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t x = walk_half<true, KW_L4>(L, R, vc, 0u, rsn, voff_a);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t p = walk_half<true, KW_L4>(L, R, vd, x, rsn, voff_b);
+      finish_region<FINAL, SHIFT>(L, R, SR, p, t1, h1, lane, src, fin, flags, ev);
+    }
+    t = t2;
+    ht = h2;
+    t1 = t3;
+    h1 = h3;
+    t2 = take_region(&wg_ticket, share, lane);
+    h2 = src.find(t2, h3);
+  }
+#endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0 && blockIdx.x < 1024) {
@@ -587,16 +738,23 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
   WinOne src{base, span, nreg, out, nblk, expected, mismatch};
-  windows_body<FINAL>(src, gtab, fin, flags, L, &wg_ticket);
+  windows_body<FINAL, false>(src, gtab, fin, flags, L, &wg_ticket);
 }
 
 // a queue of uniform 4 KiB batches in one launch (final CRCs only)
 __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, const uint32_t* __restrict__ gtab,
                                                         uint32_t fin, uint32_t flags) {
+#ifndef LCRC_Q_TREE
+  __shared__ __attribute__((aligned(16))) uint32_t L[AQ_LDS_BYTES / 4];
+  __shared__ uint32_t wg_ticket;
+  WinQueue src{jobs.j, jobs.n, jobs.nreg};
+  windows_body<true, true>(src, gtab, fin, flags, L, &wg_ticket);
+#else  // ablation: the block tree of the single-batch kernel
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
-  WinQueue src{jobs.j, jobs.n, jobs.nreg, 0, 0};
-  windows_body<true>(src, gtab, fin, flags, L, &wg_ticket);
+  WinQueue src{jobs.j, jobs.n, jobs.nreg};
+  windows_body<true, false>(src, gtab, fin, flags, L, &wg_ticket);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------

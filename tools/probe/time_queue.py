@@ -25,8 +25,15 @@ for rep in range(5):
     res.append(eng.timer_stop() / Q)
     eng.sync()
 ms = sorted(res)[len(res) // 2]
+clk = ""
+if hasattr(m.lib(), "lcrc_probe_clock_mhz"):  # LCRC_PROBE_CLOCK builds: median workgroup shader clock
+    import ctypes
+    f = m.lib().lcrc_probe_clock_mhz
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_int]
+    clk = f"  clock {f(256):.0f} MHz"
 print(f"{os.path.basename(os.environ['LCRC_LIB_PATH']):18s} {ms*1000:7.2f} us/batch  {NB*4096/ms/1e6:7.1f} GB/s  "
-      f"frac {NB*4096/ms/1e6/8000:.4f}  (min {min(res)*1000:.2f}, max {max(res)*1000:.2f})", flush=True)
+      f"frac {NB*4096/ms/1e6/8000:.4f}  (min {min(res)*1000:.2f}, max {max(res)*1000:.2f}){clk}", flush=True)
 '''.replace("ROOT", repr(ROOT))
 vdir = os.path.join(ROOT, "tools", "probe", "variants")
 names = sys.argv[1:] or sorted(f for f in os.listdir(vdir) if f.startswith("q_"))
