@@ -20,6 +20,8 @@
  *   lcrc_combine                        <- crc32fast::Hasher::combine (zlib crc32_combine)
  *   lcrc_batch / lcrc_batch_uniform     <- N independent calls of (3)/(4): one launch checksums and
  *                                          optionally verifies thousands of device-resident blocks
+ *   lcrc_batch_covered                  <- the same for a sparse set (Table::block_iter_from_index reading a
+ *                                          few blocks of a file, table.rs:114-146): cost ~ the blocks read
  *   lcrc_batch_uniform_queue            <- the same for a queue of independent batches (e.g. every table of
  *                                          a compaction's output), submitted as one launch per 32 batches
  *   lcrc_batch_host_uniform             <- the same starting and ending in host memory (pinned H2D,
@@ -135,6 +137,13 @@ int lcrc_ctx_sync(lcrc_ctx* ctx);
  * does not lie inside [0, base_len) is never read: its CRC is 0 and its mismatch bit is set. */
 int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
                uint32_t* out_crc, uint32_t* out_mismatch, void* stream);
+
+/* lcrc_batch with a hint: covered_bytes = the sum of the descriptors' lengths, or an upper bound (0 = not
+ * known). A sparse batch -- a few blocks verified inside a large file, covered_bytes < base_len / 4 -- runs
+ * the one-pass range kernel, which reads only the covered bytes (its cost follows the blocks, not the
+ * file); otherwise exactly lcrc_batch. The results are the same either way. */
+int lcrc_batch_covered(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
+                       uint64_t covered_bytes, uint32_t* out_crc, uint32_t* out_mismatch, void* stream);
 
 /* n blocks of `length` bytes, block i at base + i*stride (device). expected (device, nullable):
  * per-block expected CRCs. The 4 KiB / stride 4 KiB case is the single-pass fast path. */

@@ -86,7 +86,7 @@ ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
-    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
+    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
     "lcrc_table_scan", "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
@@ -129,6 +129,7 @@ def lib():
     sig("lcrc_ctx_stream", vp, vp)
     sig("lcrc_ctx_sync", i32, vp)
     sig("lcrc_batch", i32, vp, vp, u64, vp, sz, vp, vp, vp)
+    sig("lcrc_batch_covered", i32, vp, vp, u64, vp, sz, u64, vp, vp, vp)
     sig("lcrc_batch_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, vp)
     sig("lcrc_batch_uniform_queue", i32, vp, ctypes.POINTER(_UJob), sz, u32, u64, vp)
     sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
@@ -177,6 +178,16 @@ def lib():
     sig("lcrc_tbl_data", vp, vp)
     sig("lcrc_tbl_append", None, vp, vp, sz)
     sig("lcrc_tbl_read_block", cp, vp, sz, u64, u64, i32, ctypes.POINTER(ctypes.c_uint8))
+    # C++ restatement of the reference's TableBuilder (lcrc_tbuild.cpp)
+    sig("lcrc_tb_create", vp, u32, i32, ctypes.c_uint8, i32, u32, i32)
+    sig("lcrc_tb_destroy", None, vp)
+    sig("lcrc_tb_add", i32, vp, vp, sz, vp, sz)
+    sig("lcrc_tb_flush", None, vp)
+    sig("lcrc_tb_finish", i32, vp, cp, vp, sz)
+    sig("lcrc_tb_size", sz, vp)
+    sig("lcrc_tb_data", vp, vp)
+    sig("lcrc_tb_blocks", sz, vp, vp, sz)
+    sig("lcrc_tb_seal_descs", sz, vp, vp, sz)
     _lib = L
     return L
 
@@ -379,9 +390,15 @@ class Engine:
     def reserve(self, max_span):
         _check(lib().lcrc_ctx_reserve(self.ctx, int(max_span)), "lcrc_ctx_reserve")
 
-    def batch(self, base, base_len, descs, n, out_crc, out_mismatch=None, stream=None):
-        _check(lib().lcrc_batch(self.ctx, _ptr(base), int(base_len), _ptr(descs), int(n), _ptr(out_crc),
-                                _ptr(out_mismatch), stream), "lcrc_batch")
+    def batch(self, base, base_len, descs, n, out_crc, out_mismatch=None, stream=None, covered=None):
+        """lcrc_batch; with covered (sum of the lengths, or a bound) lcrc_batch_covered, which verifies a
+        sparse set reading only its own bytes."""
+        if covered is None:
+            _check(lib().lcrc_batch(self.ctx, _ptr(base), int(base_len), _ptr(descs), int(n), _ptr(out_crc),
+                                    _ptr(out_mismatch), stream), "lcrc_batch")
+        else:
+            _check(lib().lcrc_batch_covered(self.ctx, _ptr(base), int(base_len), _ptr(descs), int(n), int(covered),
+                                            _ptr(out_crc), _ptr(out_mismatch), stream), "lcrc_batch_covered")
 
     def batch_uniform(self, base, n, length, stride, out_crc, expected=None, out_mismatch=None, stream=None):
         _check(lib().lcrc_batch_uniform(self.ctx, _ptr(base), int(n), int(length), int(stride), _ptr(expected),
@@ -529,7 +546,7 @@ class Engine:
         return ms.value
 
     # convenience: host numpy in, host numpy out (copies; for tests)
-    def crc_ranges(self, data, offsets, lengths, expect_rel=None):
+    def crc_ranges(self, data, offsets, lengths, expect_rel=None, covered_hint=False):
         data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data)
         n = len(offsets)
         d = np.zeros(n, DESC_DTYPE)
@@ -540,7 +557,8 @@ class Engine:
         dd = DeviceBuffer.from_host(d.view(np.uint8), self.device)
         out = DeviceBuffer(max(4 * n, 4), self.device)
         mm = DeviceBuffer(max(4 * ((n + 31) // 32), 4), self.device)
-        self.batch(base, data.nbytes, dd, n, out, mm)
+        self.batch(base, data.nbytes, dd, n, out, mm,
+                   covered=int(np.asarray(lengths, np.uint64).sum()) if covered_hint else None)
         self.sync()
         crcs = out.download(np.uint32, n)
         bits = mm.download(np.uint32, (n + 31) // 32)
@@ -700,6 +718,51 @@ class TableFile:
     def __del__(self):
         try:
             lib().lcrc_tbl_destroy(self._t)
+        except Exception:
+            pass
+
+
+class TableBuilder:
+    """src/sstable/table.rs TableBuilder (C++ restatement, lcrc_tbuild.cpp): add(key, value) in key order,
+    finish(filter_name, filter_block) -> the table file's bytes. host_seal=True computes every trailer CRC
+    on the host as the reference does; host_seal=False leaves them zero and seal_descs() gives one
+    {offset, n + 1, n + 1} descriptor per block (data, filter, metaindex, index) for Engine.batch_seal."""
+
+    def __init__(self, block_size=4096, restart_interval=16, compression=0, mode=MODE_REF, flags=0, host_seal=True):
+        self._t = lib().lcrc_tb_create(block_size, restart_interval, compression, mode, flags, 1 if host_seal else 0)
+        if not self._t:
+            raise LcrcError("lcrc_tb_create: bad arguments")
+
+    def add(self, key, value):
+        kp, kn, _k1 = _buf(key)
+        vp, vn, _k2 = _buf(value)
+        _check(lib().lcrc_tb_add(self._t, kp, kn, vp, vn), "TableBuilder.add (keys must increase)")
+
+    def flush(self):
+        lib().lcrc_tb_flush(self._t)
+
+    def finish(self, filter_name=None, filter_block=b""):
+        fp, fn, _k = _buf(filter_block) if filter_block else (None, 0, None)
+        name = filter_name.encode() if isinstance(filter_name, str) else filter_name
+        _check(lib().lcrc_tb_finish(self._t, name, fp, fn), "TableBuilder.finish")
+        n = lib().lcrc_tb_size(self._t)
+        return ctypes.string_at(lib().lcrc_tb_data(self._t), n) if n else b""
+
+    def blocks(self):
+        n = lib().lcrc_tb_blocks(self._t, None, 0)
+        out = np.zeros(n, TBLK_DTYPE)
+        lib().lcrc_tb_blocks(self._t, out.ctypes.data_as(ctypes.c_void_p), n)
+        return out
+
+    def seal_descs(self):
+        n = lib().lcrc_tb_seal_descs(self._t, None, 0)
+        out = np.zeros(n, DESC_DTYPE)
+        lib().lcrc_tb_seal_descs(self._t, out.ctypes.data_as(ctypes.c_void_p), n)
+        return out
+
+    def __del__(self):
+        try:
+            lib().lcrc_tb_destroy(self._t)
         except Exception:
             pass
 

@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "liblcrc.so")
-SOURCES = ["lcrc_kernels.hip", "lcrc_api.cpp", "lcrc_scalar.cpp", "lcrc_leveldb.cpp", "lcrc_table.cpp"]
+SOURCES = ["lcrc_kernels.hip", "lcrc_api.cpp", "lcrc_scalar.cpp", "lcrc_leveldb.cpp", "lcrc_table.cpp", "lcrc_tbuild.cpp"]
 HEADERS = ["lcrc_device.h", "lcrc_math.h", "lcrc_table.h", os.path.join("..", "..", "include", "lcrc.h")]
 ARCH = os.environ.get("LCRC_OFFLOAD_ARCH", "gfx950")
 

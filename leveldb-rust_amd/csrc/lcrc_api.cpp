@@ -367,6 +367,23 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
   return LCRC_OK;
 }
 
+int lcrc_batch_covered(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
+                       uint64_t covered_bytes, uint32_t* out_crc, uint32_t* out_mismatch, void* stream) {
+  if (!ctx || (n && (!descs || !out_crc || !base))) return LCRC_EINVAL;
+  // sparse: the window pass would stream all of base_len for a small fraction of it
+  if (covered_bytes == 0 || covered_bytes >= base_len / 4 || (ctx->flags & LCRC_FLAG_DIRECT))
+    return lcrc_batch(ctx, base, base_len, descs, n, out_crc, out_mismatch, stream);
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  if (out_mismatch && n) HIPCHK(hipMemsetAsync(out_mismatch, 0, ((n + 31) / 32) * sizeof(uint32_t), st));
+  if (n == 0) return LCRC_OK;
+  HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr,
+                            ctx->d_tab, ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
+                            out_crc, out_mismatch, nullptr, nullptr, st));
+  return LCRC_OK;
+}
+
 static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
                               const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch, hipStream_t st,
                               bool clear_mismatch) {

@@ -552,3 +552,41 @@ def test_wal_many_blocks_reference_size_on_device(lcrc, engines):
     """The reference's test_many_blocks at its own size (log.rs:535-545): 1,000,000 records written, every
     one read back through the device-verified BatchLogReader."""
     logtests.t_many_blocks(logtests.Tester(lcrc, _batch_reader(lcrc, engines)), 1000000)
+
+
+def test_sparse_verify_in_a_large_file(lcrc, orc):
+    """A few blocks verified inside a 1 GiB device buffer (Table::block_iter_from_index reading single data
+    blocks, table.rs:114-146 -> format.rs:162-171): lcrc_batch_covered takes the one-pass range kernel, whose
+    cost follows the 100 blocks read, not the buffer. Every CRC and mismatch bit equals the oracle's and the
+    dense path's; the launch stays far below one pass over the buffer (~150 us)."""
+    size = 1 << 30
+    rng = np.random.default_rng(1234)
+    base = lcrc.DeviceBuffer(size)
+    offs = np.sort(rng.choice(size // 8192 - 1, 100, replace=False)).astype(np.uint64) * 8192 + \
+        rng.integers(0, 4000, 100).astype(np.uint64)
+    lens = np.full(100, 4097, np.uint32)
+    host = {}
+    for i, o in enumerate(offs):
+        blk = bytearray(orc.splitmix_bytes(0x5A00 + i, 4097))
+        c = orc.crc(bytes(blk), 0)
+        if i in (7, 50):
+            c ^= 1  # stored trailer wrong -> mismatch
+        host[int(o)] = bytes(blk) + c.to_bytes(4, "little")
+        base.upload(np.frombuffer(host[int(o)], np.uint8), int(o))
+    d = np.zeros(100, lcrc.DESC_DTYPE)
+    d["offset"], d["length"], d["expect_rel"] = offs, lens, lens
+    dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8))
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    out, mm = lcrc.DeviceBuffer(400), lcrc.DeviceBuffer(16)
+    eng.batch(base, size, dd, 100, out, mm, covered=int(lens.sum()))
+    eng.sync()
+    want = np.array([orc.crc(host[int(o)][:4097], 0) for o in offs], np.uint32)
+    assert np.array_equal(out.download(np.uint32, 100), want)
+    assert np.nonzero(lcrc.unpack_bits(mm.download(np.uint32, 4), 100))[0].tolist() == [7, 50]
+    eng.timer_start()
+    for _ in range(20):
+        eng.batch(base, size, dd, 100, out, mm, covered=int(lens.sum()))
+    us = eng.timer_stop() / 20 * 1e3
+    print(f"sparse verify: 100 x 4,097 B in a 1 GiB buffer: {us:.1f} us per call")
+    assert us < 60.0
+    eng.close()

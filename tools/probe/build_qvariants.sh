@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/../.."
 mkdir -p tools/probe/variants
-SRC="leveldb-rust_amd/csrc/lcrc_kernels.hip leveldb-rust_amd/csrc/lcrc_api.cpp leveldb-rust_amd/csrc/lcrc_scalar.cpp leveldb-rust_amd/csrc/lcrc_leveldb.cpp leveldb-rust_amd/csrc/lcrc_table.cpp"
+SRC="leveldb-rust_amd/csrc/lcrc_kernels.hip leveldb-rust_amd/csrc/lcrc_api.cpp leveldb-rust_amd/csrc/lcrc_scalar.cpp leveldb-rust_amd/csrc/lcrc_leveldb.cpp leveldb-rust_amd/csrc/lcrc_table.cpp leveldb-rust_amd/csrc/lcrc_tbuild.cpp"
 build() { out=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -mllvm -amdgpu-atomic-optimizer-strategy=None -std=c++17 -fPIC -shared -Wno-unused-result "$@" $SRC -o tools/probe/variants/q_$out.so; }
 if [ $# -eq 0 ]; then
   set -- "base:" "nowalk:-DLCRC_PROBE_NOWALK" "noload:-DLCRC_PROBE_NOLOAD" "wg2:-DLCRC_A_WGCU=2" "t1024:-DLCRC_A_THREADS=1024" "aux0:-DLCRC_LOAD_AUX=0"
