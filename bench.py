@@ -145,25 +145,34 @@ class Dist:
 
 def timed_run(dist, prepare, steps, warmup, engines=()):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
-    `prepare(first, count)` returns a callable that submits steps first .. first+count-1 (argument
-    marshalling done before the clock starts). Returns the max-over-ranks wall seconds, this rank's wall
-    seconds and its GPU milliseconds of the timed region from HIP events on the first engine's stream."""
+    `prepare(first, count)` returns the submissions for steps first .. first+count-1 as (submit, launches,
+    steps) triples (argument marshalling done before the clock starts). The wall clock covers all K steps.
+    The GPU clock -- HIP events on the first engine's stream -- starts when the FIRST submission's work has
+    finished (an event enqueued behind it) and stops at the end: it measures the launches of submissions
+    2..n back to back, without the host latency before the first kernel. Returns (max-over-ranks wall
+    seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock covers)."""
     if warmup:
-        prepare(0, warmup)()
-    go = prepare(warmup, steps)
+        for sub, _, _ in prepare(0, warmup):
+            sub()
+    subs = prepare(warmup, steps)
     for e in engines:
         e.sync()
     dist.barrier()
-    if engines:
-        engines[0].timer_start()
     t0 = time.perf_counter()
-    go()
+    subs[0][0]()
+    timed = engines and len(subs) > 1
+    if timed:
+        engines[0].timer_start()
+    for sub, _, _ in subs[1:]:
+        sub()
     for e in engines:
         e.sync()
     elapsed = time.perf_counter() - t0
-    gpu_ms = engines[0].timer_stop() if engines else None
+    gpu_ms = engines[0].timer_stop() if timed else None
     dist.barrier()
-    return dist.max(elapsed), elapsed, gpu_ms
+    cov_launches = sum(n for _, n, _ in subs[1:])
+    cov_steps = sum(k for _, _, k in subs[1:])
+    return dist.max(elapsed), elapsed, gpu_ms, cov_launches, cov_steps
 
 
 def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
@@ -232,12 +241,10 @@ def workload_fixed(m, synth, engs, rank, device, args):
             for g, (i0, n) in enumerate(groups(first, count, q)):
                 k = g % len(engs)
                 jobs = [(bufs[i % NBUF], nblk, outs[k][i % NBUF]) for i in range(i0, i0 + n)]
-                subs += [(engs[k], m.ujobs(part)) for part in balanced_jobs(jobs)]
-
-            def go():
-                for e, arr in subs:
-                    e.batch_uniform_queue(arr, blen, blen)
-            return go
+                for part in balanced_jobs(jobs):
+                    arr = m.ujobs(part)
+                    subs.append((lambda e=engs[k], a=arr: e.batch_uniform_queue(a, blen, blen), 1, len(part)))
+            return subs
         run.prepares = True
 
         launches = lambda count: sum(launches_of(n) for _, n in groups(0, count, q))  # noqa: E731
@@ -573,8 +580,12 @@ def main(argv=None):
             w = {"fixed": workload_fixed, "mixed": workload_mixed, "wal": workload_wal, "table": workload_table,
                  "seal": workload_seal, "snappy": workload_snappy}[args.config](m, synth, engs, rank, device, args)
 
-    prepare = w.run if getattr(w.run, "prepares", False) else (lambda f, c: (lambda: w.run(f, c)))
-    elapsed_max, elapsed, gpu_ms = timed_run(dist, prepare, args.steps, args.warmup, engs)
+    if getattr(w.run, "prepares", False):
+        prepare = w.run
+    else:  # one submission per step
+        per = w.launches(1)
+        prepare = lambda f, c: [(lambda i=i: w.run(i, 1), per, 1) for i in range(f, f + c)]  # noqa: E731
+    elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, engs)
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
     # this rank's fingerprint and rate, gathered over gloo (no RCCL)
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
@@ -602,24 +613,23 @@ def main(argv=None):
         "pct_hbm_peak": round(100.0 * (w.nbytes * args.steps * world / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
         "per_gpu": per_gpu,
     }
-    if engs:
-        nl = w.launches(args.steps)
-        launch_s = gpu_ms / 1e3 / nl
-        bytes_per_launch = w.nbytes * args.steps / nl
-        achieved = bytes_per_launch / launch_s / 1e9
+    if engs and gpu_ms:
         one_stream = len(engs) == 1 and not w.per_step_sync
+        launch_s = gpu_ms / 1e3 / cov_launches
+        bytes_per_launch = w.nbytes * cov_steps / cov_launches
+        achieved = bytes_per_launch / launch_s / 1e9
         result["roofline"] = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(args.config, args.mode),
-            "bytes_per_launch": int(bytes_per_launch), "launches": nl, "launch_us": round(launch_s * 1e6, 2),
-            "timing": ("HIP events on the engine stream around the timed region, / launches" if one_stream else
-                       "HIP events on the first engine's stream around the timed region, / its steps; with "
-                       f"{len(engs)} streams the other engines' launches overlap it, so this is wall per step, "
-                       "not a single launch's duration"),
+            "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
+            "launch_us": round(launch_s * 1e6, 2),
+            "timing": ("HIP events on the engine stream: from the end of the timed region's first submission to "
+                       "its end, / the launches in between (back to back, dispatch gaps included)" if one_stream else
+                       "HIP events on the first engine's stream from the end of the first step to the end of the "
+                       f"timed region, / steps; with {len(engs)} streams the steps overlap, so this is wall per "
+                       "step of the whole pipeline, not one kernel's duration"),
             "profile": load_profile(args.config, args.mode),
         }
-        if not one_stream:  # the first stream carried every len(engs)-th step
-            result["roofline"]["launch_us"] = round(gpu_ms / 1e3 / args.steps * 1e6, 2)
     else:
         result["roofline"] = None
     if (rank == 0 and world == 1 and not args.no_cpu_baseline and w.sample is not None

@@ -53,9 +53,9 @@ hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uin
                                  uint64_t* count, uint64_t* flag, const uint64_t* pos, lcrc_tblk_dev* out,
                                  lcrc_desc_dev* descs, hipStream_t st);
 hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
-                                  const uint8_t* file, lcrc_desc_dev* frames, uint32_t* unsorted, uint32_t gen,
-                                  hipStream_t st);
-hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, hipStream_t st);
+                                  const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st);
+hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, uint32_t* unsorted,
+                                   uint32_t gen, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
 hipError_t lcrc_launch_store_crc(uint8_t* base, uint64_t base_len, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
@@ -832,12 +832,11 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     HIPCHK(hipMemsetAsync(ctx->tbl_flag.p, 0, sizeof(uint32_t), st));
   }
   if (++ctx->tbl_gen == 0) ctx->tbl_gen = 1;
-  HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p,
-                                ctx->tbl_flag.p, ctx->tbl_gen, st));
+  HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, st));
   // the Snappy frames' framing pass (a malformed frame is already status 3 here), then the results and the
   // frame totals come back in ONE round trip; only a table with compressed blocks goes on to decode them
   if ((rc = snappy_plan(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out_off.p, ctx->sn_status.p, st))) return rc;
-  HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, st));
+  HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, ctx->tbl_flag.p, ctx->tbl_gen, st));
   HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
   uint32_t* h_unsorted = (uint32_t*)(ctx->h_count + 7);  // pinned
   HIPCHK(hipMemcpyAsync(h_unsorted, ctx->tbl_flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -849,7 +848,7 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     if ((rc = snappy_run(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
                          ctx->sn_status.p, &total, st)))
       return rc;
-    HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, st));
+    HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, nullptr, 0, st));
     HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }

@@ -2167,18 +2167,15 @@ __global__ void __launch_bounds__(256) k_idx_parse(const uint8_t* __restrict__ d
 }
 
 // per block: computed crc, stored type, status (mismatch / bad type), and the Snappy frame to check when
-// the checksum holds and the type is 1 (length 0 otherwise); *unsorted = gen when a block starts before
-// its predecessor (the host then sorts the result: a well-formed table never needs it)
+// the checksum holds and the type is 1 (length 0 otherwise)
 __global__ void __launch_bounds__(256) k_tbl_finish(lcrc_tblk_dev* blk, uint64_t n,
                                                     const uint32_t* __restrict__ crc,
                                                     const uint32_t* __restrict__ mismatch,
                                                     const uint8_t* __restrict__ file,
-                                                    lcrc_desc_dev* __restrict__ frames,
-                                                    uint32_t* __restrict__ unsorted, uint32_t gen) {
+                                                    lcrc_desc_dev* __restrict__ frames) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   lcrc_tblk_dev b = blk[i];
-  if (i > 0 && blk[i - 1].offset > b.offset) *unsorted = gen;  // offsets are never rewritten here
   lcrc_desc_dev f;
   f.offset = 0;
   f.length = 0;
@@ -2197,10 +2194,16 @@ __global__ void __launch_bounds__(256) k_tbl_finish(lcrc_tblk_dev* blk, uint64_t
   frames[i] = f;
 }
 
+// the Snappy frames' verdicts into the blocks' status; *unsorted = gen when a block starts before its
+// predecessor (the host then sorts the result: a well-formed table never needs it). Only the status byte
+// is written here, so the offsets every thread compares are read-only in this kernel.
 __global__ void __launch_bounds__(256) k_tbl_content(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
-                                                     const uint8_t* __restrict__ fstatus) {
+                                                     const uint8_t* __restrict__ fstatus,
+                                                     uint32_t* __restrict__ unsorted, uint32_t gen) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && fstatus[i]) blk[i].status = 3;  // LCRC_TBLK_BAD_CONTENT
+  if (i >= n) return;
+  if (unsorted && i > 0 && blk[i - 1].offset > blk[i].offset) *unsorted = gen;
+  if (fstatus[i]) blk[i].status = 3;  // LCRC_TBLK_BAD_CONTENT
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2431,17 +2434,18 @@ hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uin
 }
 
 hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
-                                  const uint8_t* file, lcrc_desc_dev* frames, uint32_t* unsorted, uint32_t gen,
-                                  hipStream_t st) {
+                                  const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(lcrc_dev::k_tbl_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, crc, mismatch,
-                     file, frames, unsorted, gen);
+                     file, frames);
   return hipGetLastError();
 }
 
-hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, hipStream_t st) {
+hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, uint32_t* unsorted,
+                                   uint32_t gen, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_tbl_content, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, fstatus);
+  hipLaunchKernelGGL(lcrc_dev::k_tbl_content, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, fstatus,
+                     unsorted, gen);
   return hipGetLastError();
 }
 

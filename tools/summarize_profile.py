@@ -69,9 +69,15 @@ def main(outdir, rnd, config, mode):
             summary["avg_us"] = round(dom[1]["avg_ns"] / 1e3, 3)
             summary["bytes_per_launch"] = bpl
             summary["frac"] = round(bpl / dom[1]["avg_ns"] / 8000.0, 4)
+            # every kernel of the pipeline per dominant-kernel call (general path: k_windows + k_blocks, WAL:
+            # parse + emit + windows + blocks), for configs whose step is more than one kernel
+            summary["pipeline_us_per_call"] = round(
+                sum(k["total_ns"] for k in summary["kernels"].values()) / dom[1]["calls"] / 1e3, 3)
             summary["bench_line"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
                                      "frac": line["roofline"]["frac"], "launch_us": line["roofline"]["launch_us"],
-                                     "launches": line["roofline"].get("launches")}
+                                     "launches": line["roofline"].get("launches"),
+                                     "streams": line["config"].get("streams")}
+            summary["agreement"] = round(summary["frac"] / line["roofline"]["frac"], 4)
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     # the dominant kernel's traffic for bench.py
