@@ -55,6 +55,8 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", choices=["fixed", "mixed", "wal", "table", "snappy", "seal"], default="fixed")
+    p.add_argument("--table-sync", action="store_true",
+                   help="table config: time the synchronous lcrc_table_scan (results to pinned host memory)")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
     p.add_argument("--queue", type=int, default=5,
                    help="fixed config: steps per lcrc_batch_uniform_queue submission (default 5 = the driver's warmup, so "
@@ -210,11 +212,12 @@ class Workload:
     launches the dominant kernel makes for `count` steps; sample / crcs: the CPU baseline's sample and the
     device's CRCs of that sample; xor(): xor of the device CRCs of step 0 (per-rank shard fingerprint)."""
 
-    def __init__(self, run, nbytes, cfg, launches=None, sample=None, crcs=None, per_step_sync=False):
+    def __init__(self, run, nbytes, cfg, launches=None, sample=None, crcs=None, per_step_sync=False, engines=None):
         self.run, self.nbytes, self.cfg = run, nbytes, cfg
         self.launches = launches or (lambda count: count)
         self.sample, self.crcs = sample, crcs
         self.per_step_sync = per_step_sync
+        self.engines = engines  # the engines the steps run on, when not the bench's own
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -385,8 +388,8 @@ def workload_table(m, synth, engs, rank, device, args):
     seal.batch_seal(dev, len(f), dd, len(blocks))
     seal.sync()
     seal.close()
-    # the results land in pinned host memory (lcrc_host_alloc_pinned), as a caller that scans often would
-    # keep them: the 1.5 MB copy then runs at the PCIe rate instead of through a pageable staging copy
+    # the synchronous form's results land in pinned host memory (lcrc_host_alloc_pinned), as a caller that scans
+    # often would keep them: the 1.5 MB copy then runs at the PCIe rate instead of through a pageable staging copy
     pinned = m.PinnedBuffer((len(blocks) + 8) * m.TBLK_DTYPE.itemsize)
     out = pinned.array.view(m.TBLK_DTYPE)
     out[:] = 0
@@ -394,15 +397,35 @@ def workload_table(m, synth, engs, rank, device, args):
     got = scanners[0].table_scan_into(dev, len(f), out)
     if got != len(blocks) or (out["status"][:got] != 0).any():
         raise RuntimeError("table bench: the sealed table does not scan clean")
+    cap = len(blocks) + 8
+    res = [(m.DeviceBuffer(cap * m.TBLK_DTYPE.itemsize, device), m.DeviceBuffer(8, device), m.DeviceBuffer(8, device))
+           for _ in scanners]
+    for e in scanners:
+        e.table_scan_reserve(len(f), cap)
+    # the async form (lcrc_table_scan_async) must agree with the synchronous one before it is timed
+    scanners[0].table_scan_async(dev, len(f), res[0][0], cap, res[0][1], res[0][2])
+    scanners[0].sync()
+    st = res[0][2].download(np.uint32, 2)
+    n = int(res[0][1].download(np.uint64, 1)[0])
+    if st[0] != 0 or n != got or res[0][0].download(m.TBLK_DTYPE, n).tobytes() != out[:got].tobytes():
+        raise RuntimeError("table bench: the device-only scan disagrees with the synchronous scan")
 
-    def run(first, count):  # synchronous: footer, device index walk and verify, results back on the host
-        for i in range(first, first + count):
-            scanners[i % len(engs)].table_scan_into(dev, len(f), out)
+    if args.table_sync:
+        def run(first, count):  # synchronous: one device scan, results back on the host
+            for i in range(first, first + count):
+                scanners[i % len(engs)].table_scan_into(dev, len(f), out)
+    else:
+        def run(first, count):  # device-only: enqueued, results, count and verdict stay on the device
+            for i in range(first, first + count):
+                k = i % len(engs)
+                scanners[k].table_scan_async(dev, len(f), res[k][0], cap, res[k][1], res[k][2])
 
-    run.keep = (pinned, scanners)
+    run.keep = (pinned, scanners, res)
     cfg = {"workload": "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)",
-           "blocks": len(blocks), "file_bytes": int(len(f))}
-    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None, per_step_sync=True)
+           "blocks": len(blocks), "file_bytes": int(len(f)),
+           "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else "lcrc_table_scan_async"}
+    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None,
+                    per_step_sync=bool(args.table_sync), engines=scanners)
 
 
 def workload_seal(m, synth, engs, rank, device, args):
@@ -585,7 +608,8 @@ def main(argv=None):
     else:  # one submission per step
         per = w.launches(1)
         prepare = lambda f, c: [(lambda i=i: w.run(i, 1), per, 1) for i in range(f, f + c)]  # noqa: E731
-    elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, engs)
+    timers = w.engines if w.engines else engs
+    elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, timers)
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
     # this rank's fingerprint and rate, gathered over gloo (no RCCL)
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
@@ -613,8 +637,8 @@ def main(argv=None):
         "pct_hbm_peak": round(100.0 * (w.nbytes * args.steps * world / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
         "per_gpu": per_gpu,
     }
-    if engs and gpu_ms:
-        one_stream = len(engs) == 1 and not w.per_step_sync
+    if timers and gpu_ms:
+        one_stream = len(timers) == 1 and not w.per_step_sync
         launch_s = gpu_ms / 1e3 / cov_launches
         bytes_per_launch = w.nbytes * cov_steps / cov_launches
         achieved = bytes_per_launch / launch_s / 1e9
@@ -626,7 +650,7 @@ def main(argv=None):
             "timing": ("HIP events on the engine stream: from the end of the timed region's first submission to "
                        "its end, / the launches in between (back to back, dispatch gaps included)" if one_stream else
                        "HIP events on the first engine's stream from the end of the first step to the end of the "
-                       f"timed region, / steps; with {len(engs)} streams the steps overlap, so this is wall per "
+                       f"timed region, / steps; with {len(timers)} streams the steps overlap, so this is wall per "
                        "step of the whole pipeline, not one kernel's duration"),
             "profile": load_profile(args.config, args.mode),
         }

@@ -28,7 +28,7 @@
  *                                          kernel, D2H, double-buffered)
  *   lcrc_wal_scan / lcrc_wal_scan_async <- the header parse + CRC verify of (2) for every physical record
  *                                          of a device-resident log file, 32 KiB block by block
- *   lcrc_table_scan                     <- Table::open with paranoid_checks (table.rs:39-103) followed by
+ *   lcrc_table_scan[_async]             <- Table::open with paranoid_checks (table.rs:39-103) followed by
  *                                          read_block_from_file(verify_checksum) (format.rs:146-171) of
  *                                          every data, filter, metaindex and index block: one batched verify
  *   lcrc_snappy_frames                  <- snap::read::FrameDecoder at format.rs:194-206 (decode + the masked
@@ -218,6 +218,28 @@ typedef struct lcrc_tblk {
  * err (capacity err_cap, may be NULL). Synchronous. */
 int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
                     lcrc_tblk* blocks, size_t max_blocks, size_t* n_blocks, char* err, size_t err_cap);
+
+/* The same scan with no host round trip: every step -- footer, index walk (one thread per restart
+ * segment), read_meta's filter entry, ONE batched verify of every block, the type dispatch, Snappy frames
+ * decoded and their chunks checked -- is enqueued on `stream` and runs on the device; graph-capturable after
+ * lcrc_table_scan_reserve. The index and metaindex are walked before their own checksums are known and
+ * verified in the same batch; the outcome is then ordered as the reference's (index checksum first, a filter
+ * named by a metaindex that does not verify dropped). blocks (DEVICE, capacity max_blocks) receives the
+ * blocks in index order (by offset for a well-formed table); *n_blocks (device or pinned) their count;
+ * status[0..1] (device or pinned u32) the verdict: LCRC_TSCAN_OK, LCRC_TSCAN_CORRUPT with status[1] the
+ * message (lcrc_table_scan_message), LCRC_TSCAN_HOST when the table needs the synchronous scan's host
+ * walk (a Snappy-framed index or metaindex, a handle past the file, restart segments over 4 KiB, decoded
+ * frames over the reserved workspace), or LCRC_TSCAN_CAPACITY with *n_blocks the capacity needed. */
+#define LCRC_TSCAN_OK 0
+#define LCRC_TSCAN_CORRUPT 1
+#define LCRC_TSCAN_HOST 2
+#define LCRC_TSCAN_CAPACITY 3
+int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
+                          lcrc_tblk* blocks, size_t max_blocks, uint64_t* n_blocks, uint32_t* status, void* stream);
+/* Workspace for lcrc_table_scan_async up to these sizes (decoded_cap: the Snappy frames' decoded bytes). */
+int lcrc_table_scan_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap);
+/* The reference's message for a LCRC_TSCAN_CORRUPT code ("" for none). */
+const char* lcrc_table_scan_message(uint32_t code);
 
 /* Writer side, for a batch: CRC of every descriptor (masked if LCRC_FLAG_MASK) stored little-endian at
  * base[offset + expect_rel] in place (device). SSTable block: {off, n + 1, n + 1} writes the trailer crc;

@@ -87,7 +87,8 @@ ABI_SYMBOLS = [
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
-    "lcrc_table_scan", "lcrc_batch_seal", "lcrc_snappy_frames",
+    "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
+    "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_stop",
     "lcrc_graph_begin", "lcrc_graph_end", "lcrc_graph_launch", "lcrc_graph_destroy",
@@ -137,6 +138,9 @@ def lib():
     sig("lcrc_wal_scan_async", i32, vp, vp, u64, vp, sz, vp, vp)
     sig("lcrc_table_scan", i32, vp, vp, u64, cp, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp, sz)
     sig("lcrc_batch_seal", i32, vp, vp, u64, vp, sz, vp, vp)
+    sig("lcrc_table_scan_async", i32, vp, vp, u64, cp, vp, sz, vp, vp, vp)
+    sig("lcrc_table_scan_reserve", i32, vp, u64, sz, u64)
+    sig("lcrc_table_scan_message", cp, u32)
     sig("lcrc_snappy_frames", i32, vp, vp, vp, sz, vp, u64, vp, vp, ctypes.POINTER(ctypes.c_uint64))
     sig("lcrc_snappy_frame_decode", ctypes.c_int64, vp, sz, vp, sz)
     sig("lcrc_dev_alloc", i32, i32, sz, ctypes.POINTER(vp))
@@ -482,6 +486,19 @@ class Engine:
             raise TableCorruption(err.value.decode())
         _check(rc, "lcrc_table_scan")
         return n.value
+
+    def table_scan_reserve(self, max_file_len, max_blocks, decoded_cap=0):
+        _check(lib().lcrc_table_scan_reserve(self.ctx, int(max_file_len), int(max_blocks), int(decoded_cap)),
+               "lcrc_table_scan_reserve")
+
+    def table_scan_async(self, file_dev, file_len, blocks_dev, max_blocks, count_dev, status_dev, filter_name=None,
+                         stream=None):
+        """lcrc_table_scan_async: enqueued, device-only; results, count (u64) and status (2 x u32) stay where
+        the caller points them (device or pinned memory)."""
+        fname = filter_name.encode() if isinstance(filter_name, str) else filter_name
+        _check(lib().lcrc_table_scan_async(self.ctx, _ptr(file_dev), int(file_len), fname, _ptr(blocks_dev),
+                                           int(max_blocks), _ptr(count_dev), _ptr(status_dev), stream),
+               "lcrc_table_scan_async")
 
     def snappy_frames_into(self, base, frames_dev, n, out, out_cap, out_off, status):
         """lcrc_snappy_frames with caller-owned device buffers; returns the decoded size."""

@@ -30,6 +30,16 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
                               const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st);
 hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
                                      uint32_t fin, uint32_t flags, hipStream_t st);
+hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
+                               lcrc_tscan_dev* st, hipStream_t s);
+hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
+                                uint64_t* flag, uint64_t bound, hipStream_t s);
+hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
+                               const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
+                               uint64_t bound, hipStream_t s);
+hipError_t lcrc_launch_ts_gate(lcrc_tscan_dev* st, const uint64_t* out_off, const uint64_t* chunk_off, uint64_t out_cap,
+                               uint64_t chunk_cap, hipStream_t s);
+hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, hipStream_t s);
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
@@ -40,22 +50,23 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
-                                   uint64_t* nchunks, uint8_t* status, uint32_t* maxes, hipStream_t st);
+                                   uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
+                                   hipStream_t st);
 hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
-                             uint64_t* part, hipStream_t st);
+                             uint64_t* part, const uint64_t* n_dev, hipStream_t st);
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
-                                     uint32_t max_out, hipStream_t st);
+                                     uint32_t max_out, const uint64_t* n_dev, const uint32_t* gate, hipStream_t st);
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
 hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
                                  uint64_t* count, uint64_t* flag, const uint64_t* pos, lcrc_tblk_dev* out,
                                  lcrc_desc_dev* descs, hipStream_t st);
 hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
-                                  const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st);
+                                  const uint8_t* file, lcrc_desc_dev* frames, const uint64_t* n_dev, hipStream_t st);
 hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, uint32_t* unsorted,
-                                   uint32_t gen, hipStream_t st);
+                                   uint32_t gen, const uint64_t* n_dev, hipStream_t st);
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st);
 hipError_t lcrc_launch_store_crc(uint8_t* base, uint64_t base_len, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st);
@@ -149,6 +160,13 @@ struct lcrc_ctx {
   DevBuf<uint32_t> tbl_crcs, tbl_mm;
   DevBuf<uint64_t> tbl_pos;
   DevBuf<uint8_t> tbl_types;
+  // asynchronous table scan: its device state, the result staging of the synchronous wrapper, capacities
+  DevBuf<lcrc_tscan_dev> ts_state;
+  DevBuf<lcrc_tblk_dev> ts_blocks;
+  DevBuf<uint64_t> ts_count;
+  uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
+  void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
+  uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
 };
 
 namespace {
@@ -262,6 +280,9 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
       return bail(fail_hip(e, "hipEventCreate"));
   if ((e = hipHostMalloc(&ctx->h_count, 8 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
     return bail(fail_hip(e, "hipHostMalloc"));
+  if ((e = hipHostMalloc(&ctx->ts_host, sizeof(lcrc_tscan_dev), hipHostMallocDefault)) != hipSuccess)
+    return bail(fail_hip(e, "hipHostMalloc"));
+  if ((e = hipMalloc(&ctx->ts_count_status, 4 * sizeof(uint32_t))) != hipSuccess) return bail(fail_hip(e, "hipMalloc"));
 
   // constant tables for this mode
   const uint32_t poly = lcrc::poly_of(mode);
@@ -309,6 +330,11 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->tbl_mm.release();
   ctx->tbl_pos.release();
   ctx->tbl_types.release();
+  ctx->ts_state.release();
+  ctx->ts_blocks.release();
+  ctx->ts_count.release();
+  if (ctx->ts_host) (void)hipHostFree(ctx->ts_host);
+  if (ctx->ts_count_status) (void)hipFree(ctx->ts_count_status);
   if (ctx->d_tab) (void)hipFree(ctx->d_tab);
   if (ctx->t0) (void)hipEventDestroy(ctx->t0);
   if (ctx->t1) (void)hipEventDestroy(ctx->t1);
@@ -615,8 +641,8 @@ static int snappy_plan(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* 
       (rc = ctx->sn_part.ensure(2 * nparts)) || (rc = ctx->sn_max.ensure(2)))
     return rc;
   HIPCHK(hipMemsetAsync(ctx->sn_max.p, 0, 8, st));
-  HIPCHK(lcrc_launch_snappy_size(base, frames, n, ctx->sn_size.p, ctx->sn_nch.p, status, ctx->sn_max.p, st));
-  HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, n, out_off, ctx->sn_choff.p, ctx->sn_part.p, st));
+  HIPCHK(lcrc_launch_snappy_size(base, frames, n, ctx->sn_size.p, ctx->sn_nch.p, status, ctx->sn_max.p, nullptr, st));
+  HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, n, out_off, ctx->sn_choff.p, ctx->sn_part.p, nullptr, st));
   uint64_t* tot = ctx->h_count + 4;  // pinned staging: decoded total, chunk total, then the two maxima
   HIPCHK(hipMemcpyAsync(&tot[0], out_off + n, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], ctx->sn_choff.p + n, 8, hipMemcpyDeviceToHost, st));
@@ -639,7 +665,7 @@ static int snappy_run(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* f
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
-                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], st));
+                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, st));
   // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
   if (ctx->general == 1) {
     static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
@@ -765,7 +791,7 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
   HIPCHK(lcrc_launch_idx_parse(false, contents, len, nres, file_len, ctx->idx_count.p, ctx->idx_flag.p, nullptr, nullptr,
                                nullptr, st));
   HIPCHK(lcrc_launch_scan2(ctx->idx_count.p, ctx->idx_flag.p, nres, ctx->idx_pos.p, ctx->idx_fpos.p, ctx->sn_part.p,
-                           st));
+                           nullptr, st));
   uint64_t* tot = ctx->h_count + 2;  // pinned
   HIPCHK(hipMemcpyAsync(&tot[0], ctx->idx_pos.p + nres, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], ctx->idx_fpos.p + nres, 8, hipMemcpyDeviceToHost, st));
@@ -832,11 +858,12 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     HIPCHK(hipMemsetAsync(ctx->tbl_flag.p, 0, sizeof(uint32_t), st));
   }
   if (++ctx->tbl_gen == 0) ctx->tbl_gen = 1;
-  HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, st));
+  HIPCHK(lcrc_launch_tbl_finish(ctx->tbl_blk.p, n, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, nullptr,
+                                st));
   // the Snappy frames' framing pass (a malformed frame is already status 3 here), then the results and the
   // frame totals come back in ONE round trip; only a table with compressed blocks goes on to decode them
   if ((rc = snappy_plan(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out_off.p, ctx->sn_status.p, st))) return rc;
-  HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, ctx->tbl_flag.p, ctx->tbl_gen, st));
+  HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, ctx->tbl_flag.p, ctx->tbl_gen, nullptr, st));
   HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
   uint32_t* h_unsorted = (uint32_t*)(ctx->h_count + 7);  // pinned
   HIPCHK(hipMemcpyAsync(h_unsorted, ctx->tbl_flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -848,13 +875,118 @@ static int table_scan_device(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     if ((rc = snappy_run(ctx, file, ctx->tbl_frames.p, n, ctx->sn_out.p, ctx->sn_out.cap, ctx->sn_out_off.p,
                          ctx->sn_status.p, &total, st)))
       return rc;
-    HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, nullptr, 0, st));
+    HIPCHK(lcrc_launch_tbl_content(ctx->tbl_blk.p, n, ctx->sn_status.p, nullptr, 0, nullptr, st));
     HIPCHK(hipMemcpyAsync(blocks, ctx->tbl_blk.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
   // sorted by offset (a well-formed table already is; the order was checked by k_tbl_finish)
   if (!sorted)
     std::stable_sort(blocks, blocks + n, [](const lcrc_tblk& a, const lcrc_tblk& b) { return a.offset < b.offset; });
+  return LCRC_OK;
+}
+
+// ---- asynchronous whole-table scan: every step on the device, nothing synchronized ----
+static const char* const kTscanMsg[] = {"",
+                                        "file is too short to be an sstable",
+                                        "not an sstable (bad magic number)",
+                                        "Error when decoding varint64",
+                                        "block checksum mismatch",
+                                        "bad block type",
+                                        "bad block contents, size smaller than u32",
+                                        "bad block contents"};
+
+const char* lcrc_table_scan_message(uint32_t code) {
+  return code < sizeof(kTscanMsg) / sizeof(kTscanMsg[0]) ? kTscanMsg[code] : "";
+}
+
+static uint64_t ts_chunk_cap(size_t max_blocks, uint64_t decoded_cap) {
+  return 2ull * max_blocks + decoded_cap / 1024 + 64;
+}
+
+static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap, uint64_t chunks) {
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  const uint64_t nb = max_blocks + 1;
+  const uint64_t cc = std::max<uint64_t>(std::max(ts_chunk_cap(max_blocks, decoded_cap), chunks), ctx->ts_chunk_cap);
+  decoded_cap = std::max<uint64_t>(decoded_cap, ctx->ts_decoded_cap);
+  if ((rc = ctx->ts_state.ensure(1)) || (rc = ctx->idx_count.ensure(nb)) || (rc = ctx->idx_flag.ensure(nb)) ||
+      (rc = ctx->idx_pos.ensure(nb)) || (rc = ctx->idx_fpos.ensure(nb)) || (rc = ctx->sn_part.ensure(2 * (nb / 256 + 2))) ||
+      (rc = ctx->tbl_descs.ensure(nb)) || (rc = ctx->tbl_crcs.ensure(nb)) || (rc = ctx->tbl_mm.ensure(nb / 32 + 1)) ||
+      (rc = ctx->tbl_frames.ensure(nb)) || (rc = ctx->sn_size.ensure(nb)) || (rc = ctx->sn_nch.ensure(nb)) ||
+      (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) || (rc = ctx->sn_status.ensure(nb)) ||
+      (rc = ctx->sn_max.ensure(2)) || (rc = ctx->sn_cdesc.ensure(cc)) || (rc = ctx->sn_cexp.ensure(cc)) ||
+      (rc = ctx->sn_cframe.ensure(cc)) || (rc = ctx->sn_ccrc.ensure(cc)) || (rc = ctx->sn_out.ensure(decoded_cap + 16)) ||
+      (rc = ctx->win.ensure(window_words(max_file_len))))
+    return rc;
+  if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
+  ctx->ts_decoded_cap = decoded_cap;
+  ctx->ts_chunk_cap = cc;
+  return LCRC_OK;
+}
+
+int lcrc_table_scan_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap) {
+  if (!ctx) return LCRC_EINVAL;
+  return ts_reserve(ctx, max_file_len, max_blocks, decoded_cap, 0);
+}
+
+int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
+                          lcrc_tblk* blocks, size_t max_blocks, uint64_t* n_blocks, uint32_t* status, void* stream) {
+  if (!ctx || !n_blocks || !status || (file_len && !file) || (max_blocks && !blocks)) return LCRC_EINVAL;
+  lcrc_tscan_key key;
+  memset(&key, 0, sizeof(key));
+  if (filter_name) {
+    const size_t nl = strlen(filter_name);
+    if (nl + 6 > sizeof(key.key)) return LCRC_EINVAL;
+    memcpy(key.key, "filter", 6);
+    memcpy(key.key + 6, filter_name, nl);
+    key.len = (uint32_t)(nl + 6);
+  }
+  // workspace for this size (reserved beforehand, this allocates nothing: graph-capturable)
+  int rc = ts_reserve(ctx, file_len, max_blocks, 0, 0);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  lcrc_tscan_dev* S = ctx->ts_state.p;
+  lcrc_tblk_dev* blk = (lcrc_tblk_dev*)blocks;
+  const uint64_t cap = max_blocks;
+  const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
+  static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
+  // footer, index block header, the metaindex filter entry (optimistic: checksums come with the batch)
+  HIPCHK(lcrc_launch_ts_open(file, file_len, &key, cap, S, st));
+  // the index block's restart segments: entry counts, their scan, the handles and the verify descriptors
+  const uint64_t* nres_dev = &S->nres;
+  HIPCHK(lcrc_launch_ts_count(file, file_len, S, ctx->idx_count.p, ctx->idx_flag.p, cap, st));
+  HIPCHK(lcrc_launch_scan2(ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->idx_pos.p, ctx->idx_fpos.p, ctx->sn_part.p,
+                           nres_dev, st));
+  HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_pos.p, ctx->idx_fpos.p, blk, ctx->tbl_descs.p, cap, cap, st));
+  // ONE batched verify of every block (data, filter, metaindex, index) over the file
+  const uint64_t* ntot = &S->n_total;
+  if (cap) {
+    HIPCHK(hipMemsetAsync(ctx->tbl_mm.p, 0, (cap / 32 + 1) * sizeof(uint32_t), st));
+    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
+    HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_BATCH_GRID_DIV, file, file_len, ctx->tbl_descs.p, cap, 0, 0,
+                              nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
+                              ctx->tbl_crcs.p, ctx->tbl_mm.p, ntot, nullptr, st));
+    // read_block_from_file's type dispatch; Snappy frames decoded and their chunks' masked CRC-32C checked
+    HIPCHK(lcrc_launch_tbl_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ntot, st));
+    HIPCHK(hipMemsetAsync(ctx->sn_max.p, 0, 8, st));
+    HIPCHK(lcrc_launch_snappy_size(file, ctx->tbl_frames.p, cap, ctx->sn_size.p, ctx->sn_nch.p, ctx->sn_status.p,
+                                   ctx->sn_max.p, ntot, st));
+    HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_part.p,
+                             ntot, st));
+    HIPCHK(lcrc_launch_ts_gate(S, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->ts_decoded_cap, ctx->ts_chunk_cap, st));
+    HIPCHK(lcrc_launch_snappy_decode(file, ctx->tbl_frames.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_out.p,
+                                     ctx->sn_status.p, ctx->sn_cdesc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, 1u << 30,
+                                     1u << 30, ntot, &S->gate, st));
+    HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, ctx->sn_out.p, ctx->ts_decoded_cap, ctx->sn_cdesc.p, ctx->ts_chunk_cap,
+                              0, 0, nullptr, tab_c, x4096_c, lcrc::POLY_C, lcrc::CRC_INIT, lcrc::CRC_XOROUT,
+                              LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr, &S->n_chunks, nullptr, st));
+    HIPCHK(lcrc_launch_snappy_check(ctx->sn_ccrc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, &S->n_chunks, ctx->ts_chunk_cap,
+                                    ctx->sn_status.p, st));
+    HIPCHK(lcrc_launch_tbl_content(blk, cap, ctx->sn_status.p, &S->unsorted, 1, ntot, st));
+  }
+  // the reference's order of outcomes; the count and status for the caller
+  HIPCHK(lcrc_launch_ts_final(S, blk, n_blocks, st));
+  HIPCHK(hipMemcpyAsync(status, S, 2 * sizeof(uint32_t), hipMemcpyDefault, st));
   return LCRC_OK;
 }
 
@@ -883,6 +1015,40 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
     return nullptr;
   };
   if (file_len < FOOTER_ENCODED_LENGTH) return corrupt("file is too short to be an sstable");
+  // the device-only scan first (one synchronisation); it grows its own result capacity as needed
+  {
+    uint64_t cap = std::max<uint64_t>(std::max<uint64_t>(max_blocks, ctx->ts_blocks.cap), 1024);
+    lcrc_tscan_dev* hs = (lcrc_tscan_dev*)ctx->ts_host;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      if ((rc = ctx->ts_blocks.ensure(cap)) || (rc = ctx->ts_count.ensure(1))) return rc;
+      if ((rc = lcrc_table_scan_async(ctx, file, file_len, filter_name, (lcrc_tblk*)ctx->ts_blocks.p, cap,
+                                      ctx->ts_count.p, ctx->ts_count_status, nullptr)))
+        return rc;
+      HIPCHK(hipMemcpyAsync(hs, ctx->ts_state.p, sizeof(lcrc_tscan_dev), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (hs->status == 3) {  // capacity: grow to what the table needs and scan again
+        cap = std::max<uint64_t>(hs->n_data + 16, cap * 2);
+      } else if (hs->status == 2 && hs->gate) {  // decoded frames over the workspace: grow it, scan again
+        if ((rc = ts_reserve(ctx, file_len, cap, hs->need_out + hs->need_out / 4 + 4096, hs->need_chunks + 64)))
+          return rc;
+      } else {
+        break;
+      }
+    }
+    if (hs->status == 1) return corrupt(lcrc_table_scan_message(hs->code));
+    if (hs->status == 0) {
+      const size_t n = hs->n_total;
+      *n_blocks = n;
+      if (!blocks || max_blocks < n) return LCRC_ERANGE;
+      HIPCHK(hipMemcpyAsync(blocks, ctx->ts_blocks.p, n * sizeof(lcrc_tblk), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (hs->unsorted)
+        std::stable_sort(blocks, blocks + n, [](const lcrc_tblk& a, const lcrc_tblk& b) { return a.offset < b.offset; });
+      return LCRC_OK;
+    }
+    // status 2: what the device walk cannot vouch for (a Snappy-framed index or metaindex, long restart
+    // segments, a handle past the file, decoded frames over the workspace) -- the paths below
+  }
   uint8_t footer[FOOTER_ENCODED_LENGTH];
   HIPCHK(hipMemcpy(footer, file + file_len - FOOTER_ENCODED_LENGTH, FOOTER_ENCODED_LENGTH, hipMemcpyDeviceToHost));
   Handle meta_h, index_h;

@@ -60,3 +60,22 @@ struct lcrc_qjob_host {
   uint32_t* mismatch;
   uint64_t nblk;
 };
+
+// State of an asynchronous whole-table scan (lcrc_table_scan_async), in device memory.
+struct lcrc_tscan_dev {
+  uint32_t status;  // LCRC_TSCAN_* of include/lcrc.h: 0 ok, 1 corrupt (`code`), 2 host walk needed, 3 capacity
+  uint32_t code;    // LCRC_TSCAN_MSG_* when corrupt
+  uint32_t pcode;   // an index-contents error, reported only if the index checksum holds
+  uint32_t has_filter;
+  uint64_t meta_off, meta_size, idx_off, idx_size, filt_off, filt_size;
+  uint64_t nres;     // restart segments of the index block (0: nothing to walk)
+  uint64_t n_data;   // data blocks named by the index
+  uint64_t n_total;  // blocks in the result (data, filter, metaindex, index)
+  uint64_t n_chunks;  // Snappy data chunks of the compressed blocks (0 when over the capacity)
+  uint32_t unsorted, gate;
+  uint64_t need_out, need_chunks;  // the decoded bytes and chunks the Snappy frames need (set by the gate)
+};
+struct lcrc_tscan_key {  // the metaindex key read_meta looks for: "filter" + the policy name
+  uint32_t len;          // 0: no filter policy
+  uint8_t key[124];
+};

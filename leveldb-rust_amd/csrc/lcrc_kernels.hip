@@ -1121,7 +1121,8 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
   const uint32_t tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t* __restrict__ xch = inv + 4097;  // x^(8 * 4096 * k) mod P, k < R_KMAX
-  if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
+  if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan, async table scan)
+  if (blockIdx.x >= n) return;  // a grid sized by a bound: no range is dealt to this workgroup
   build_tables(L, gtab, wv, lane);
   if (tid < R_SLOTS) sl_gen[tid] = 0;
   if (tid == 0) {
@@ -1625,7 +1626,9 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
 __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__ base,
                                                      const lcrc_desc_dev* __restrict__ frames, uint64_t n,
                                                      uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
-                                                     uint8_t* __restrict__ status, uint32_t* __restrict__ maxes) {
+                                                     uint8_t* __restrict__ status, uint32_t* __restrict__ maxes,
+                                                     const uint64_t* __restrict__ n_dev) {
+  if (n_dev) n = *n_dev < n ? *n_dev : n;  // the count produced on the device (async table scan)
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint8_t* p = f < n ? base + frames[f].offset : base;
   const uint32_t len = f < n ? frames[f].length : 0u;
@@ -1686,8 +1689,11 @@ __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__
 // of the workgroups before it; out_a[n], out_b[n] = the totals
 __global__ void __launch_bounds__(256) k_scan2_local(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
                                                      uint64_t n, uint64_t* __restrict__ out_a,
-                                                     uint64_t* __restrict__ out_b, uint64_t* __restrict__ part) {
+                                                     uint64_t* __restrict__ out_b, uint64_t* __restrict__ part,
+                                                     const uint64_t* __restrict__ n_dev) {
   __shared__ uint64_t sa[256], sb[256];
+  if (n_dev) n = *n_dev < n ? *n_dev : n;
+  if ((uint64_t)blockIdx.x * 256 > n) return;  // past the device count (the grid is sized by a bound)
   const uint32_t t = threadIdx.x;
   const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
   const uint64_t va = i < n ? a[i] : 0, vb = i < n ? b[i] : 0;
@@ -1712,11 +1718,15 @@ __global__ void __launch_bounds__(256) k_scan2_local(const uint64_t* __restrict_
 }
 
 __global__ void __launch_bounds__(256) k_scan2_add(uint64_t n, uint64_t* __restrict__ out_a,
-                                                   uint64_t* __restrict__ out_b, const uint64_t* __restrict__ part) {
+                                                   uint64_t* __restrict__ out_b, const uint64_t* __restrict__ part,
+                                                   const uint64_t* __restrict__ n_dev) {
   __shared__ uint64_t ra[256], rb[256];
   const uint32_t t = threadIdx.x;
+  if (n_dev) n = *n_dev < n ? *n_dev : n;
   const uint64_t nparts = (n + 255) / 256;
-  const uint64_t upto = blockIdx.x == gridDim.x - 1 ? nparts : blockIdx.x;  // the last also sums for the totals
+  const uint64_t last = nparts ? nparts - 1 : 0;  // the workgroup that also writes the totals
+  if (blockIdx.x > last) return;
+  const uint64_t upto = blockIdx.x == last ? nparts : blockIdx.x;
   uint64_t xa = 0, xb = 0, ma = 0, mb = 0;
   for (uint64_t w = t; w < upto; w += 256) {
     xa += part[2 * w];
@@ -1743,7 +1753,7 @@ __global__ void __launch_bounds__(256) k_scan2_add(uint64_t n, uint64_t* __restr
     out_a[i] += ba;
     out_b[i] += bb;
   }
-  if (blockIdx.x == gridDim.x - 1) {
+  if (blockIdx.x == last) {
     ra[t] = xa;
     rb[t] = xb;
     __syncthreads();
@@ -1922,8 +1932,12 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
                                                            uint8_t* __restrict__ out, uint8_t* __restrict__ status,
                                                            lcrc_desc_dev* __restrict__ cdesc,
                                                            uint32_t* __restrict__ cexp, uint32_t* __restrict__ cframe,
-                                                           uint32_t in_lim, uint32_t out_cap) {
+                                                           uint32_t in_lim, uint32_t out_cap,
+                                                           const uint64_t* __restrict__ n_dev,
+                                                           const uint32_t* __restrict__ gate) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sn_lds[];
+  if (gate && *gate) return;  // the decoded total does not fit the output (async table scan: host fallback)
+  if (n_dev) n = *n_dev < n ? *n_dev : n;
   uint8_t* const lin = sn_lds;
   uint8_t* const lout = sn_lds + in_lim + SN_SLACK;
   const uint32_t lane = __lane_id();
@@ -2100,12 +2114,27 @@ __device__ __forceinline__ uint32_t dev_varint(const uint8_t* __restrict__ d, ui
 // (tblk offset/size, kind DATA) at pos[i] .. and their verify descriptors; a handle past the end of the file
 // gets an empty descriptor and status TRUNCATED.
 template <bool PASS2>
+__device__ __forceinline__ void idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
+                                            uint64_t file_len, uint64_t* __restrict__ count,
+                                            uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos,
+                                            lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs,
+                                            uint64_t i);
+
+template <bool PASS2>
 __global__ void __launch_bounds__(256) k_idx_parse(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
                                                    uint64_t file_len, uint64_t* __restrict__ count,
                                                    uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos,
                                                    lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nres) return;
+  if (i < nres) idx_segment<PASS2>(d, len, nres, file_len, count, flag, pos, out, descs, i);
+}
+
+template <bool PASS2>
+__device__ __forceinline__ void idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
+                                            uint64_t file_len, uint64_t* __restrict__ count,
+                                            uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos,
+                                            lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs,
+                                            uint64_t i) {
   const uint32_t restarts = len - (1 + nres) * 4;
   auto rst = [&](uint32_t k) { return load_le32(d + restarts + 4 * k); };
   const uint32_t start = rst((uint32_t)i);
@@ -2172,7 +2201,9 @@ __global__ void __launch_bounds__(256) k_tbl_finish(lcrc_tblk_dev* blk, uint64_t
                                                     const uint32_t* __restrict__ crc,
                                                     const uint32_t* __restrict__ mismatch,
                                                     const uint8_t* __restrict__ file,
-                                                    lcrc_desc_dev* __restrict__ frames) {
+                                                    lcrc_desc_dev* __restrict__ frames,
+                                                    const uint64_t* __restrict__ n_dev) {
+  if (n_dev) n = *n_dev < n ? *n_dev : n;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   lcrc_tblk_dev b = blk[i];
@@ -2199,11 +2230,257 @@ __global__ void __launch_bounds__(256) k_tbl_finish(lcrc_tblk_dev* blk, uint64_t
 // is written here, so the offsets every thread compares are read-only in this kernel.
 __global__ void __launch_bounds__(256) k_tbl_content(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
                                                      const uint8_t* __restrict__ fstatus,
-                                                     uint32_t* __restrict__ unsorted, uint32_t gen) {
+                                                     uint32_t* __restrict__ unsorted, uint32_t gen,
+                                                     const uint64_t* __restrict__ n_dev) {
+  if (n_dev) n = *n_dev < n ? *n_dev : n;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (unsorted && i > 0 && blk[i - 1].offset > blk[i].offset) *unsorted = gen;
   if (fstatus[i]) blk[i].status = 3;  // LCRC_TBLK_BAD_CONTENT
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Asynchronous whole-table scan (lcrc_table_scan_async): Table::open + read_meta + one verify of every block
+// (table.rs:39-146, format.rs:146-213) with no host round trip. The index and metaindex are walked
+// OPTIMISTICALLY, before their own checksums are known: both are verified in the same batch as the data
+// blocks, and k_ts_final applies the reference's order afterwards (index checksum before any index-contents
+// error; the filter block named by a metaindex that does not verify is dropped, as read_meta swallows it).
+// Whatever the device walk cannot vouch for sets status 2 and the synchronous wrapper walks on the host.
+// ---------------------------------------------------------------------------------------------------
+enum { TS_OK = 0, TS_CORRUPT = 1, TS_HOST = 2, TS_CAPACITY = 3 };
+enum { TSM_SHORT = 1, TSM_MAGIC = 2, TSM_VARINT = 3, TSM_CHECKSUM = 4, TSM_TYPE = 5, TSM_SMALL = 6, TSM_CONTENTS = 7 };
+
+// footer, index block header, metaindex filter entry: one thread
+__global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                const lcrc_tscan_key fkey, uint64_t seg_cap,
+                                                lcrc_tscan_dev* __restrict__ st) {
+  __shared__ uint8_t key[256];
+  if (threadIdx.x != 0) return;
+  lcrc_tscan_dev s = {};
+  auto done = [&]() { *st = s; };
+  if (file_len < 48) {
+    s.status = TS_CORRUPT;
+    s.code = TSM_SHORT;
+    return done();
+  }
+  const uint8_t* f = file + file_len - 48;
+  const uint64_t magic = (uint64_t)load_le32(f + 40) | ((uint64_t)load_le32(f + 44) << 32);
+  if (magic != 0xdb4775248b80fb57ull) {
+    s.status = TS_CORRUPT;
+    s.code = TSM_MAGIC;
+    return done();
+  }
+  uint32_t p = dev_varint<64>(f, 0, 48, &s.meta_off);
+  if (p != ~0u) p = dev_varint<64>(f, p, 48, &s.meta_size);
+  if (p != ~0u) p = dev_varint<64>(f, p, 48, &s.idx_off);
+  if (p != ~0u) p = dev_varint<64>(f, p, 48, &s.idx_size);
+  if (p == ~0u) {
+    s.status = TS_CORRUPT;
+    s.code = TSM_VARINT;
+    return done();
+  }
+  // Table::open reads the index block (verified: paranoid_checks); its checksum comes with the batch
+  if (s.idx_off > file_len || s.idx_size + 5 > file_len - s.idx_off || s.idx_size + 1 > 0x7FFFFFFFull) {
+    s.status = TS_HOST;  // "truncated block read" and its kin: the host walk
+    return done();
+  }
+  const uint8_t itype = file[s.idx_off + s.idx_size];
+  const uint64_t clen = s.idx_size;
+  if (itype == 1) {
+    s.status = TS_HOST;  // a Snappy-framed index block: decoded on the host path
+    return done();
+  }
+  if (itype > 1) {
+    s.pcode = TSM_TYPE;
+  } else if (clen < 4) {
+    s.pcode = TSM_SMALL;
+  } else {
+    const uint32_t nres = load_le32(file + s.idx_off + clen - 4);
+    if ((uint64_t)nres > (clen - 4) / 4) {
+      s.pcode = TSM_CONTENTS;
+    } else if (nres == 0 || (clen - 4) / nres > 4096) {
+      s.status = TS_HOST;  // no restart points / long segments: the sequential host walk
+      return done();
+    } else if (nres + 2 > seg_cap) {
+      s.status = TS_CAPACITY;  // at least one block per segment: more than the result can hold
+      s.n_data = nres + 2;
+      return done();
+    } else {
+      s.nres = nres;
+    }
+  }
+  // read_meta (only with a filter policy): the first metaindex key >= "filter" + name; a malformed
+  // metaindex yields no filter, as the reference swallows read_meta's errors
+  if (fkey.len && s.meta_off <= file_len && s.meta_size + 5 <= file_len - s.meta_off && s.meta_size <= 0xFFFFFFFFull) {
+    const uint8_t* d = file + s.meta_off;
+    const uint64_t n = s.meta_size;
+    const uint8_t mtype = d[n];
+    if (mtype == 1) {
+      s.status = TS_HOST;  // compressed metaindex: the host path decodes it
+      return done();
+    }
+    if (mtype == 0 && n >= 4) {
+      const uint32_t nr = load_le32(d + n - 4);
+      if ((uint64_t)nr <= (n - 4) / 4) {
+        const uint32_t restarts = (uint32_t)(n - (1 + (uint64_t)nr) * 4);
+        uint32_t off = 0, klen = 0;
+        while (off < restarts) {
+          if (restarts - off < 3) break;
+          uint64_t shared, non_shared, vlen;
+          uint32_t q = dev_varint<32>(d, off, restarts, &shared);
+          if (q != ~0u) q = dev_varint<32>(d, q, restarts, &non_shared);
+          if (q != ~0u) q = dev_varint<32>(d, q, restarts, &vlen);
+          if (q == ~0u || (uint64_t)restarts - q < non_shared + vlen || klen < shared) break;
+          if (shared + non_shared > sizeof(key)) {
+            s.status = TS_HOST;  // a key longer than the walk's buffer
+            return done();
+          }
+          for (uint32_t i = 0; i < non_shared; ++i) key[shared + i] = d[q + i];
+          klen = (uint32_t)(shared + non_shared);
+          int c = 0;  // compare key with the wanted key (bytewise, then length)
+          const uint32_t m = klen < fkey.len ? klen : fkey.len;
+          for (uint32_t i = 0; i < m && !c; ++i) c = (int)key[i] - (int)fkey.key[i];
+          if (!c) c = klen < fkey.len ? -1 : klen > fkey.len ? 1 : 0;
+          if (c >= 0) {
+            if (c == 0) {
+              const uint32_t ve = (uint32_t)(q + non_shared + vlen);
+              uint64_t fo, fs;
+              uint32_t r = dev_varint<64>(d, (uint32_t)(q + non_shared), ve, &fo);
+              if (r != ~0u) r = dev_varint<64>(d, r, ve, &fs);
+              if (r != ~0u) {
+                s.has_filter = 1;
+                s.filt_off = fo;
+                s.filt_size = fs;
+              }
+            }
+            break;
+          }
+          off = (uint32_t)(q + non_shared + vlen);
+        }
+      }
+    }
+  }
+  done();
+}
+
+// pass 1 over the restart segments, the count taken from the device state (grid-stride)
+__global__ void __launch_bounds__(256) k_ts_count(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                  const lcrc_tscan_dev* __restrict__ st, uint64_t* __restrict__ count,
+                                                  uint64_t* __restrict__ flag) {
+  if (st->status != TS_OK) return;
+  const uint64_t nres = st->nres;
+  const uint8_t* d = file + st->idx_off;
+  const uint32_t len = (uint32_t)st->idx_size;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nres; i += (uint64_t)gridDim.x * blockDim.x)
+    idx_segment<false>(d, len, (uint32_t)nres, file_len, count, flag, nullptr, nullptr, nullptr, i);
+}
+
+// after the scan of the counts: the data-block total, the capacity check, the fallback flags; then pass 2
+// writes the handles and thread 0 appends the filter, metaindex and index blocks with their descriptors
+__global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                 lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ pos,
+                                                 const uint64_t* __restrict__ fpos, lcrc_tblk_dev* __restrict__ out,
+                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap) {
+  if (st->status != TS_OK) return;
+  const uint64_t nres = st->nres;
+  const uint64_t nd = nres ? pos[nres] : 0;
+  if (nres && fpos[nres]) return;  // a segment the device walk cannot vouch for: k_ts_final reports it
+  const uint64_t ntot = nd + (st->has_filter ? 3 : 2);
+  if (ntot > cap) return;
+  const uint8_t* d = file + st->idx_off;
+  const uint32_t len = (uint32_t)st->idx_size;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nres; i += (uint64_t)gridDim.x * blockDim.x)
+    idx_segment<true>(d, len, (uint32_t)nres, file_len, nullptr, nullptr, pos, out, descs, i);
+  if (blockIdx.x == 0 && threadIdx.x < 3) {
+    const uint32_t k = threadIdx.x;  // 0 filter (if any), then metaindex, index
+    const bool hf = st->has_filter;
+    if (k == 0 && !hf) return;
+    const uint64_t at = nd + (hf ? k : k - 1);
+    const uint64_t off = k == 0 ? st->filt_off : k == 1 ? st->meta_off : st->idx_off;
+    const uint64_t size = k == 0 ? st->filt_size : k == 1 ? st->meta_size : st->idx_size;
+    lcrc_tblk_dev b;
+    b.offset = off;
+    b.size = size;
+    b.crc = 0;
+    b.kind = (uint8_t)(k + 1);  // LCRC_TBLK_FILTER, _METAINDEX, _INDEX
+    b.type = 0;
+    b.status = 0;
+    b.reserved = 0;
+    lcrc_desc_dev dd;
+    const bool in = off <= file_len && size + 5 <= file_len - off && size + 1 <= 0x7FFFFFFFull;
+    dd.offset = in ? off : 0;
+    dd.length = in ? (uint32_t)(size + 1) : 0;
+    dd.expect_rel = in ? (int32_t)(size + 1) : LCRC_NO_EXPECT_DEV;
+    if (!in) {
+      b.status = 2;  // LCRC_TBLK_TRUNCATED
+      b.type = 0xFF;
+    }
+    out[at] = b;
+    descs[at] = dd;
+  }
+}
+
+// the result count for the batch kernels (status, capacity and fallback resolved first)
+__global__ void __launch_bounds__(64) k_ts_count_total(lcrc_tscan_dev* __restrict__ st,
+                                                       const uint64_t* __restrict__ pos,
+                                                       const uint64_t* __restrict__ fpos, uint64_t cap) {
+  if (threadIdx.x != 0) return;
+  st->n_total = 0;
+  if (st->status != TS_OK) return;
+  const uint64_t nres = st->nres;
+  if (nres && fpos[nres]) {
+    st->status = TS_HOST;
+    return;
+  }
+  const uint64_t nd = nres ? pos[nres] : 0;
+  const uint64_t ntot = nd + (st->has_filter ? 3 : 2);
+  st->n_data = nd;
+  if (ntot > cap) {
+    st->status = TS_CAPACITY;
+    st->n_data = ntot;  // the capacity needed (reported); n_total stays 0: nothing is verified
+    return;
+  }
+  st->n_total = ntot;
+}
+
+// the Snappy frames' decoded total against the output capacity: gate the decode (host fallback when over)
+__global__ void __launch_bounds__(64) k_ts_gate(lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ out_off,
+                                                const uint64_t* __restrict__ chunk_off, uint64_t out_cap,
+                                                uint64_t chunk_cap) {
+  if (threadIdx.x != 0) return;
+  const uint64_t n = st->status == TS_OK ? st->n_total : 0;
+  const uint64_t total = n ? out_off[n] : 0, chunks = n ? chunk_off[n] : 0;
+  const bool over = total > out_cap || chunks > chunk_cap;
+  st->gate = over ? 1u : 0u;
+  st->need_out = total;
+  st->need_chunks = chunks;
+  st->n_chunks = over ? 0 : chunks;  // the chunk count the CRC pass and the check read
+  if (over && st->status == TS_OK) st->status = TS_HOST;
+}
+
+// the reference's order of outcomes, once every checksum is known
+__global__ void __launch_bounds__(64) k_ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
+                                                 uint64_t* __restrict__ n_out) {
+  if (threadIdx.x != 0) return;
+  lcrc_tscan_dev s = *st;
+  if (s.status == TS_OK) {
+    const uint64_t n = s.n_total;
+    const lcrc_tblk_dev ix = blk[n - 1];  // the index block, last
+    if (ix.status == 1) {
+      s.status = TS_CORRUPT;
+      s.code = TSM_CHECKSUM;  // Table::open: "block checksum mismatch"
+    } else if (s.pcode) {
+      s.status = TS_CORRUPT;
+      s.code = s.pcode;
+    } else if (s.has_filter && blk[n - 2].status != 0) {
+      // read_meta: a metaindex that does not read cleanly names no filter -- drop the filter block
+      blk[n - 3] = blk[n - 2];
+      blk[n - 2] = blk[n - 1];
+      s.n_total = n - 1;
+    }
+  }
+  *st = s;
+  *n_out = s.status == TS_OK ? s.n_total : s.status == TS_CAPACITY ? s.n_data : 0;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2320,6 +2597,39 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
   return hipGetLastError();
 }
 
+// ---- asynchronous table scan (lcrc_table_scan_async) ----
+hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
+                               lcrc_tscan_dev* st, hipStream_t s) {
+  hipLaunchKernelGGL(lcrc_dev::k_ts_open, dim3(1), dim3(64), 0, s, file, file_len, *key, cap, st);
+  return hipGetLastError();
+}
+// grid: a bound on the restart segments (the workgroups past the device count return at once)
+hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
+                                uint64_t* flag, uint64_t bound, hipStream_t s) {
+  const uint64_t g = bound / 256 + 1;
+  hipLaunchKernelGGL(lcrc_dev::k_ts_count, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
+                     count, flag);
+  return hipGetLastError();
+}
+hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
+                               const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
+                               uint64_t bound, hipStream_t s) {
+  hipLaunchKernelGGL(lcrc_dev::k_ts_count_total, dim3(1), dim3(64), 0, s, st, pos, fpos, cap);
+  const uint64_t g = bound / 256 + 1;
+  hipLaunchKernelGGL(lcrc_dev::k_ts_emit, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
+                     pos, fpos, out, descs, cap);
+  return hipGetLastError();
+}
+hipError_t lcrc_launch_ts_gate(lcrc_tscan_dev* st, const uint64_t* out_off, const uint64_t* chunk_off, uint64_t out_cap,
+                               uint64_t chunk_cap, hipStream_t s) {
+  hipLaunchKernelGGL(lcrc_dev::k_ts_gate, dim3(1), dim3(64), 0, s, st, out_off, chunk_off, out_cap, chunk_cap);
+  return hipGetLastError();
+}
+hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, hipStream_t s) {
+  hipLaunchKernelGGL(lcrc_dev::k_ts_final, dim3(1), dim3(64), 0, s, st, blk, n_out);
+  return hipGetLastError();
+}
+
 // n_dev (device, nullable): the actual count when it is only known on the device; n is then a bound
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
@@ -2378,27 +2688,29 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
 }
 
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
-                                   uint64_t* nchunks, uint8_t* status, uint32_t* maxes, hipStream_t st) {
+                                   uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
+                                   hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(lcrc_dev::k_snappy_size, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, frames, n, size,
-                     nchunks, status, maxes);
+                     nchunks, status, maxes, n_dev);
   return hipGetLastError();
 }
 
 // out_a / out_b: n + 1 entries (exclusive scans, totals at [n]); part: 2 * ceil(n / 256) scratch words
+// n_dev (nullable): the count produced on the device, n is then its bound (the grid is sized by n + 1)
 hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
-                             uint64_t* part, hipStream_t st) {
-  const uint64_t g = (n + 255) / 256;
+                             uint64_t* part, const uint64_t* n_dev, hipStream_t st) {
+  const uint64_t g = n_dev ? n / 256 + 1 : (n + 255) / 256;
   if (g == 0) return hipMemsetAsync(out_a, 0, 8, st) == hipSuccess ? hipMemsetAsync(out_b, 0, 8, st) : hipErrorUnknown;
-  hipLaunchKernelGGL(lcrc_dev::k_scan2_local, dim3((unsigned)g), dim3(256), 0, st, a, b, n, out_a, out_b, part);
-  hipLaunchKernelGGL(lcrc_dev::k_scan2_add, dim3((unsigned)g), dim3(256), 0, st, n, out_a, out_b, part);
+  hipLaunchKernelGGL(lcrc_dev::k_scan2_local, dim3((unsigned)g), dim3(256), 0, st, a, b, n, out_a, out_b, part, n_dev);
+  hipLaunchKernelGGL(lcrc_dev::k_scan2_add, dim3((unsigned)g), dim3(256), 0, st, n, out_a, out_b, part, n_dev);
   return hipGetLastError();
 }
 
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
-                                     uint32_t max_out, hipStream_t st) {
+                                     uint32_t max_out, const uint64_t* n_dev, const uint32_t* gate, hipStream_t st) {
   using lcrc_dev::SN_MAX;
   if (n == 0) return hipSuccess;
   const uint64_t g = n < 16384 ? n : 16384;  // one wave per frame, grid-stride
@@ -2407,7 +2719,7 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
   const uint32_t out_cap = max_out < SN_MAX ? (max_out + 15) & ~15u : SN_MAX;
   const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
   hipLaunchKernelGGL(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
-                     chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap);
+                     chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, gate);
   return hipGetLastError();
 }
 
@@ -2434,18 +2746,18 @@ hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uin
 }
 
 hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
-                                  const uint8_t* file, lcrc_desc_dev* frames, hipStream_t st) {
+                                  const uint8_t* file, lcrc_desc_dev* frames, const uint64_t* n_dev, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(lcrc_dev::k_tbl_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, crc, mismatch,
-                     file, frames);
+                     file, frames, n_dev);
   return hipGetLastError();
 }
 
 hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, uint32_t* unsorted,
-                                   uint32_t gen, hipStream_t st) {
+                                   uint32_t gen, const uint64_t* n_dev, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(lcrc_dev::k_tbl_content, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, fstatus,
-                     unsorted, gen);
+                     unsorted, gen, n_dev);
   return hipGetLastError();
 }
 

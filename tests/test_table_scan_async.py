@@ -1,0 +1,223 @@
+"""The device-only whole-table scan (lcrc_table_scan_async): Table::open with paranoid_checks
+(src/sstable/table.rs:39-103) + read_block_from_file with verify_checksum for every block
+(src/sstable/format.rs:146-171), enqueued with no host round trip. Results, verdicts and the reference's
+messages against the oracle's restatement (oracle.table_scan_expect) on tables from the oracle's writer; the
+cases the device walk hands back to the host (LCRC_TSCAN_HOST) are checked to be exactly those it documents;
+and the scan captured in a HIP graph and replayed.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from test_table_scan import FILTER, _as_tuples, _handcrafted, _kvs
+
+OK, CORRUPT, HOST, CAPACITY = 0, 1, 2, 3
+
+
+class _Scan:
+    """Device buffers for one async scan: the file, the result array, the count and the status words."""
+
+    def __init__(self, lcrc, f, cap):
+        self.lcrc = lcrc
+        self.n = len(f)
+        self.file = lcrc.DeviceBuffer.from_host(np.frombuffer(f, np.uint8).copy() if f else np.zeros(1, np.uint8))
+        self.cap = cap
+        self.blocks = lcrc.DeviceBuffer(max(cap, 1) * lcrc.TBLK_DTYPE.itemsize)
+        self.count = lcrc.DeviceBuffer(8)
+        self.status = lcrc.DeviceBuffer(8)
+
+    def run(self, eng, filter_name=None):
+        eng.table_scan_async(self.file, self.n, self.blocks, self.cap, self.count, self.status, filter_name)
+        eng.sync()
+        return self.read()
+
+    def read(self):
+        st = self.status.download(np.uint32, 2)
+        n = int(self.count.download(np.uint64, 1)[0])
+        got = self.blocks.download(self.lcrc.TBLK_DTYPE, n) if st[0] == OK and n else None
+        return int(st[0]), int(st[1]), n, got
+
+    def close(self):
+        for b in (self.file, self.blocks, self.count, self.status):
+            b.close()
+
+
+def _expect_async(lcrc, eng, orc, f, filt=None, cap=None, decoded=1 << 22, mode=0, masked=False):
+    """Run the async scan and compare with the oracle; returns the status."""
+    want, werr = orc.table_scan_expect(f, filt, mode, masked)
+    eng.table_scan_reserve(len(f), cap if cap is not None else 4096, decoded)
+    s = _Scan(lcrc, f, cap if cap is not None else 4096)
+    try:
+        st, code, n, got = s.run(eng, filt)
+        if st == OK:
+            assert werr is None
+            assert sorted(_as_tuples(got)) == want
+        elif st == CORRUPT:
+            assert lcrc.lib().lcrc_table_scan_message(code).decode() == werr
+        elif st == CAPACITY:
+            assert werr is None and n == len(want)
+        return st
+    finally:
+        s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("compression", [0, 1])
+@pytest.mark.parametrize("filt", [None, FILTER])
+@pytest.mark.parametrize("block_size", [256, 4096, 65536])
+def test_async_clean(lcrc, orc, engines, compression, filt, block_size):
+    f, _ = orc.table_build(_kvs(4000, block_size + compression), block_size=block_size, compression=compression,
+                           filter_name=filt, filter_block=os.urandom(300))
+    assert _expect_async(lcrc, engines[lcrc.MODE_REF], orc, f, filt) == OK
+
+
+@pytest.mark.gpu
+def test_async_masked_c(lcrc, orc):
+    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
+    try:
+        f, _ = orc.table_build(_kvs(2000, 7), compression=1, filter_name=FILTER, filter_block=b"q" * 64,
+                               mode=1, masked=True)
+        assert _expect_async(lcrc, eng, orc, f, FILTER, mode=1, masked=True) == OK
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_async_block_and_structural_corruption(lcrc, orc, engines):
+    eng = engines[lcrc.MODE_REF]
+    f, blocks = orc.table_build(_kvs(3000, 11), block_size=1024, compression=1, filter_name=FILTER,
+                                filter_block=b"z" * 200)
+    data = [b for b in blocks if b[2] == 0]
+    g = bytearray(f)
+    for off, n, _ in (data[0], data[len(data) // 2], data[-1]):
+        g[off + n // 2] ^= 0x10
+    assert _expect_async(lcrc, eng, orc, bytes(g), FILTER) == OK  # block-level verdicts, no error
+    ih = [b for b in blocks if b[2] == 3][0]
+    mh = [b for b in blocks if b[2] == 2][0]
+    cases = {"short": f[-47:], "magic": f[:-1] + bytes([f[-1] ^ 1])}
+    g = bytearray(f)
+    g[ih[0] + 1] ^= 0x20
+    cases["index crc"] = bytes(g)
+    g = bytearray(f)
+    g[ih[0] + ih[1]] = 7
+    cases["index type"] = bytes(g)
+    g = bytearray(f)
+    g[mh[0] + 2] ^= 0x04  # a metaindex that does not verify: read_meta drops the filter
+    cases["meta crc"] = bytes(g)
+    for name, case in cases.items():
+        st = _expect_async(lcrc, eng, orc, case, FILTER)
+        assert st in (OK, CORRUPT), name
+    assert _expect_async(lcrc, eng, orc, cases["short"]) == CORRUPT
+    assert _expect_async(lcrc, eng, orc, cases["index crc"], FILTER) == CORRUPT
+
+
+@pytest.mark.gpu
+def test_async_handles_and_host_cases(lcrc, orc, engines):
+    """Handles past the file, a Snappy index, malformed varints: either the device's verdict equals the
+    oracle's, or the scan says LCRC_TSCAN_HOST for exactly the cases it documents; the synchronous wrapper
+    then gives the oracle's answer in every case."""
+    eng = engines[lcrc.MODE_REF]
+    v = orc.varint
+    cases = {
+        "past end": (_handcrafted(orc, [(b"a", v(0) + v(100)), (b"b", v(10 ** 6) + v(50))]), (OK, HOST)),
+        "bad varint": (_handcrafted(orc, [(b"a", b"\xff\xff")]), (CORRUPT,)),
+        "snappy index": (_handcrafted(orc, [(b"a", v(0) + v(100))], index_type=1), (HOST,)),
+        "no filter entry": (_handcrafted(orc, [(b"a", v(0) + v(100))], meta_entries=[(b"filterother", v(0) + v(1))]),
+                            (OK,)),
+    }
+    for name, (f, allowed) in cases.items():
+        st = _expect_async(lcrc, eng, orc, f, FILTER)
+        assert st in allowed, name
+        got, err = _sync(lcrc, eng, f, FILTER)
+        want, werr = orc.table_scan_expect(f, FILTER)
+        assert err == werr and (got is None or _as_tuples(got) == want), name
+
+
+def _sync(lcrc, eng, f, filt):
+    dev = lcrc.DeviceBuffer.from_host(np.frombuffer(f, np.uint8).copy())
+    try:
+        return eng.table_scan(dev, len(f), filt), None
+    except lcrc.TableCorruption as e:
+        return None, str(e)
+    finally:
+        dev.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("interval", [1, 16, 1000])
+def test_async_index_restart_intervals(lcrc, orc, engines, interval):
+    f, _ = orc.table_build(_kvs(6000, 41), block_size=512, compression=1, index_restart_interval=interval)
+    st = _expect_async(lcrc, engines[lcrc.MODE_REF], orc, f)
+    assert st == (HOST if interval == 1000 else OK)  # one segment over 4 KiB: the host walk
+
+
+@pytest.mark.gpu
+def test_async_capacity_and_workspace(lcrc, orc, engines):
+    eng = engines[lcrc.MODE_REF]
+    f, blocks = orc.table_build(_kvs(3000, 13), block_size=512, compression=1, filter_name=FILTER,
+                                filter_block=b"k" * 30)
+    assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks) - 1) == CAPACITY
+    assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks)) == OK
+    # decoded frames over the reserved workspace: handed to the host, and the sync wrapper grows it
+    eng2 = lcrc.Engine(0, lcrc.MODE_REF)
+    try:
+        assert _expect_async(lcrc, eng2, orc, f, FILTER, decoded=16) == HOST
+        got, err = _sync(lcrc, eng2, f, FILTER)
+        assert err is None and _as_tuples(got) == orc.table_scan_expect(f, FILTER)[0]
+        assert _expect_async(lcrc, eng2, orc, f, FILTER, decoded=0) == OK  # the grown workspace stays
+    finally:
+        eng2.close()
+
+
+@pytest.mark.gpu
+def test_async_compressed_content(lcrc, orc, engines):
+    f, blocks = orc.table_build(_kvs(3000, 31), block_size=2048, compression=1)
+    g = bytearray(f)
+    comp = [b for b in blocks if b[2] == 0 and g[b[0] + b[1]] == 1]
+    for off, n, _ in comp[:2]:
+        g[off + n - 3] ^= 0x5A
+        g[off + n + 1:off + n + 5] = orc.crc(bytes(g[off:off + n + 1]), 0).to_bytes(4, "little")
+    off, n, _ = comp[2]
+    g[off + n] = 7
+    g[off + n + 1:off + n + 5] = orc.crc(bytes(g[off:off + n + 1]), 0).to_bytes(4, "little")
+    assert _expect_async(lcrc, engines[lcrc.MODE_REF], orc, bytes(g)) == OK
+
+
+@pytest.mark.gpu
+def test_async_graph_replay(lcrc, orc):
+    """The whole scan captured in one HIP graph after lcrc_table_scan_reserve and replayed: the same
+    blocks, count and status as the direct call, for a clean and (new file contents, same buffers) a corrupt
+    table."""
+    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
+    f, blocks = orc.table_build(_kvs(5000, 3), block_size=1024, compression=1, filter_name=FILTER,
+                                filter_block=b"p" * 500, mode=1, masked=True)
+    want, _ = orc.table_scan_expect(f, FILTER, 1, True)
+    cap = len(blocks) + 8
+    eng.table_scan_reserve(len(f), cap, 1 << 22)
+    s = _Scan(lcrc, f, cap)
+    g = None
+    try:
+        st, _, n, got = s.run(eng, FILTER)
+        assert st == OK and sorted(_as_tuples(got)) == want
+        g = eng.graph_capture(lambda: eng.table_scan_async(s.file, s.n, s.blocks, s.cap, s.count, s.status, FILTER))
+        for _ in range(2):
+            s.blocks.zero()
+            s.count.zero()
+            eng.graph_launch(g)
+            eng.sync()
+            st, _, n, got = s.read()
+            assert st == OK and sorted(_as_tuples(got)) == want
+        ih = [b for b in blocks if b[2] == 3][0]
+        bad = bytearray(f)
+        bad[ih[0] + 3] ^= 1
+        s.file.upload(np.frombuffer(bytes(bad), np.uint8))
+        eng.graph_launch(g)
+        eng.sync()
+        st, code, _, _ = s.read()
+        assert st == CORRUPT and lcrc.lib().lcrc_table_scan_message(code).decode() == "block checksum mismatch"
+    finally:
+        if g is not None:
+            eng.graph_destroy(g)
+        s.close()
+        eng.close()
