@@ -422,7 +422,7 @@ def workload_table(m, synth, engs, rank, device, args):
 
     run.keep = (pinned, scanners, res)
     cfg = {"workload": "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)",
-           "blocks": len(blocks), "file_bytes": int(len(f)),
+           "blocks": len(blocks), "file_bytes": int(len(f)), "crc": "crc-32/iso-hdlc (crc32fast), the reference's trailers",
            "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else "lcrc_table_scan_async"}
     return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None,
                     per_step_sync=bool(args.table_sync), engines=scanners)
@@ -632,7 +632,8 @@ def main(argv=None):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 bytes, seeds in leveldb-rust_amd/synth.py)",
-        "config": dict(w.cfg, crc="crc32c, LevelDB-masked" if mode == m.MODE_C else "crc-32/iso-hdlc (crc32fast)",
+        "config": dict(w.cfg, crc=w.cfg.get("crc") or ("crc32c, LevelDB-masked" if mode == m.MODE_C else
+                                                          "crc-32/iso-hdlc (crc32fast)"),
                        parallelism=f"{world} independent shard(s), no collective", streams=len(engs)),
         "pct_hbm_peak": round(100.0 * (w.nbytes * args.steps * world / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
         "per_gpu": per_gpu,

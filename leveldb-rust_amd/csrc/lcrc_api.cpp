@@ -33,13 +33,16 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                lcrc_tscan_dev* st, hipStream_t s);
 hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
-                                uint64_t* flag, uint64_t bound, hipStream_t s);
+                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero, uint32_t* zero2,
+                                hipStream_t s);
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
                                const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t bound, hipStream_t s);
-hipError_t lcrc_launch_ts_gate(lcrc_tscan_dev* st, const uint64_t* out_off, const uint64_t* chunk_off, uint64_t out_cap,
-                               uint64_t chunk_cap, hipStream_t s);
-hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, hipStream_t s);
+hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
+                                 const uint8_t* file, lcrc_desc_dev* frames, uint64_t* size, uint64_t* nchunks,
+                                 uint8_t* fstatus, const uint64_t* n_dev, hipStream_t s);
+hipError_t lcrc_launch_ts_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, lcrc_tscan_dev* st,
+                                  uint64_t* n_out, uint32_t* status_out, hipStream_t s);
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
@@ -57,7 +60,8 @@ hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, u
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
-                                     uint32_t max_out, const uint64_t* n_dev, const uint32_t* gate, hipStream_t st);
+                                     uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
+                                     uint64_t ts_chunk_cap, hipStream_t st);
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
 hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
@@ -665,7 +669,7 @@ static int snappy_run(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* f
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
-                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, st));
+                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, 0, 0, st));
   // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
   if (ctx->general == 1) {
     static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
@@ -954,39 +958,42 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   HIPCHK(lcrc_launch_ts_open(file, file_len, &key, cap, S, st));
   // the index block's restart segments: entry counts, their scan, the handles and the verify descriptors
   const uint64_t* nres_dev = &S->nres;
-  HIPCHK(lcrc_launch_ts_count(file, file_len, S, ctx->idx_count.p, ctx->idx_flag.p, cap, st));
+  HIPCHK(lcrc_launch_ts_count(file, file_len, S, ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->tbl_mm.p, cap / 32 + 1,
+                              (uint32_t*)ctx->sn_max.p, st));
   HIPCHK(lcrc_launch_scan2(ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->idx_pos.p, ctx->idx_fpos.p, ctx->sn_part.p,
                            nres_dev, st));
   HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_pos.p, ctx->idx_fpos.p, blk, ctx->tbl_descs.p, cap, cap, st));
   // ONE batched verify of every block (data, filter, metaindex, index) over the file
   const uint64_t* ntot = &S->n_total;
   if (cap) {
-    HIPCHK(hipMemsetAsync(ctx->tbl_mm.p, 0, (cap / 32 + 1) * sizeof(uint32_t), st));
-    HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr, st));
-    HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_BATCH_GRID_DIV, file, file_len, ctx->tbl_descs.p, cap, 0, 0,
-                              nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
-                              ctx->tbl_crcs.p, ctx->tbl_mm.p, ntot, nullptr, st));
-    // read_block_from_file's type dispatch; Snappy frames decoded and their chunks' masked CRC-32C checked
-    HIPCHK(lcrc_launch_tbl_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ntot, st));
-    HIPCHK(hipMemsetAsync(ctx->sn_max.p, 0, 8, st));
-    HIPCHK(lcrc_launch_snappy_size(file, ctx->tbl_frames.p, cap, ctx->sn_size.p, ctx->sn_nch.p, ctx->sn_status.p,
-                                   ctx->sn_max.p, ntot, st));
+    if (ctx->general == 1) {  // LCRC_GENERAL=ranges: the one-pass kernel
+      HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, file, file_len, ctx->tbl_descs.p, cap, 0, 0, nullptr, ctx->d_tab,
+                                ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
+                                ctx->tbl_crcs.p, ctx->tbl_mm.p, ntot, nullptr, st));
+    } else {
+      HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
+                                 st));
+      HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, file, file_len, ctx->tbl_descs.p, cap, 0, 0,
+                                nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
+                                ctx->tbl_crcs.p, ctx->tbl_mm.p, ntot, nullptr, st));
+    }
+    // read_block_from_file's type dispatch and the Snappy framing walk; the frames decoded (the decoded total
+    // checked against the workspace on the device) and their chunks' masked CRC-32C checked
+    HIPCHK(lcrc_launch_ts_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ctx->sn_size.p,
+                                 ctx->sn_nch.p, ctx->sn_status.p, ntot, st));
     HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_part.p,
                              ntot, st));
-    HIPCHK(lcrc_launch_ts_gate(S, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->ts_decoded_cap, ctx->ts_chunk_cap, st));
     HIPCHK(lcrc_launch_snappy_decode(file, ctx->tbl_frames.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_out.p,
-                                     ctx->sn_status.p, ctx->sn_cdesc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, 1u << 30,
-                                     1u << 30, ntot, &S->gate, st));
+                                     ctx->sn_status.p, ctx->sn_cdesc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, 8192, 8192,
+                                     ntot, S, ctx->ts_decoded_cap, ctx->ts_chunk_cap, st));  // 8 KiB LDS staging each way
     HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, ctx->sn_out.p, ctx->ts_decoded_cap, ctx->sn_cdesc.p, ctx->ts_chunk_cap,
                               0, 0, nullptr, tab_c, x4096_c, lcrc::POLY_C, lcrc::CRC_INIT, lcrc::CRC_XOROUT,
                               LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr, &S->n_chunks, nullptr, st));
     HIPCHK(lcrc_launch_snappy_check(ctx->sn_ccrc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, &S->n_chunks, ctx->ts_chunk_cap,
                                     ctx->sn_status.p, st));
-    HIPCHK(lcrc_launch_tbl_content(blk, cap, ctx->sn_status.p, &S->unsorted, 1, ntot, st));
   }
-  // the reference's order of outcomes; the count and status for the caller
-  HIPCHK(lcrc_launch_ts_final(S, blk, n_blocks, st));
-  HIPCHK(hipMemcpyAsync(status, S, 2 * sizeof(uint32_t), hipMemcpyDefault, st));
+  // the frames' verdicts, then (last workgroup) the reference's order of outcomes, the count and the status
+  HIPCHK(lcrc_launch_ts_content(blk, cap, ctx->sn_status.p, S, n_blocks, status, st));
   return LCRC_OK;
 }
 
@@ -1028,7 +1035,7 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
       HIPCHK(hipStreamSynchronize(st));
       if (hs->status == 3) {  // capacity: grow to what the table needs and scan again
         cap = std::max<uint64_t>(hs->n_data + 16, cap * 2);
-      } else if (hs->status == 2 && hs->gate) {  // decoded frames over the workspace: grow it, scan again
+      } else if (hs->status == 2 && hs->gate == 1) {  // decoded frames over the workspace: grow it, scan again
         if ((rc = ts_reserve(ctx, file_len, cap, hs->need_out + hs->need_out / 4 + 4096, hs->need_chunks + 64)))
           return rc;
       } else {

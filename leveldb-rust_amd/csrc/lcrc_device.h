@@ -74,6 +74,8 @@ struct lcrc_tscan_dev {
   uint64_t n_chunks;  // Snappy data chunks of the compressed blocks (0 when over the capacity)
   uint32_t unsorted, gate;
   uint64_t need_out, need_chunks;  // the decoded bytes and chunks the Snappy frames need (set by the gate)
+  uint32_t idx_only;  // a restart segment the device walk cannot vouch for: only the index block is verified
+  uint32_t arrive;    // k_ts_content's arrival counter (the last workgroup applies the outcome; reset by it)
 };
 struct lcrc_tscan_key {  // the metaindex key read_meta looks for: "filter" + the policy name
   uint32_t len;          // 0: no filter policy

@@ -1622,18 +1622,14 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
   return false;
 }
 
-// pass 1: decoded size, data-chunk count and framing verdict of every frame
-__global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__ base,
-                                                     const lcrc_desc_dev* __restrict__ frames, uint64_t n,
-                                                     uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
-                                                     uint8_t* __restrict__ status, uint32_t* __restrict__ maxes,
-                                                     const uint64_t* __restrict__ n_dev) {
-  if (n_dev) n = *n_dev < n ? *n_dev : n;  // the count produced on the device (async table scan)
-  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint8_t* p = f < n ? base + frames[f].offset : base;
-  const uint32_t len = f < n ? frames[f].length : 0u;
-  uint64_t total = 0, chunks = 0;
-  uint32_t max_in = 0, max_out = 0;  // largest compressed data (after the crc) / decoded chunk
+// the framing walk of one frame p[0, len): decoded size, data-chunk count, largest compressed data (after the
+// crc) and decoded chunk; false when the framing is malformed
+__device__ __forceinline__ bool snappy_frame_size(const uint8_t* __restrict__ p, uint32_t len, uint64_t& total,
+                                                  uint64_t& chunks, uint32_t& max_in, uint32_t& max_out) {
+  total = 0;
+  chunks = 0;
+  max_in = 0;
+  max_out = 0;
   bool ok = true, seen_id = false;
   uint32_t at = 0;
   while (ok && at < len) {
@@ -1668,6 +1664,22 @@ __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__
     }
     at += cl;
   }
+  return ok;
+}
+
+// pass 1: decoded size, data-chunk count and framing verdict of every frame
+__global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__ base,
+                                                     const lcrc_desc_dev* __restrict__ frames, uint64_t n,
+                                                     uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
+                                                     uint8_t* __restrict__ status, uint32_t* __restrict__ maxes,
+                                                     const uint64_t* __restrict__ n_dev) {
+  if (n_dev) n = *n_dev < n ? *n_dev : n;  // the count produced on the device
+  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint8_t* p = f < n ? base + frames[f].offset : base;
+  const uint32_t len = f < n ? frames[f].length : 0u;
+  uint64_t total, chunks;
+  uint32_t max_in, max_out;
+  const bool ok = snappy_frame_size(p, len, total, chunks, max_in, max_out);
   if (f < n) {
     size[f] = ok ? total : 0;
     nchunks[f] = ok ? chunks : 0;
@@ -1934,10 +1946,25 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
                                                            uint32_t* __restrict__ cexp, uint32_t* __restrict__ cframe,
                                                            uint32_t in_lim, uint32_t out_cap,
                                                            const uint64_t* __restrict__ n_dev,
-                                                           const uint32_t* __restrict__ gate) {
+                                                           lcrc_tscan_dev* __restrict__ ts, uint64_t ts_out_cap,
+                                                           uint64_t ts_chunk_cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sn_lds[];
-  if (gate && *gate) return;  // the decoded total does not fit the output (async table scan: host fallback)
   if (n_dev) n = *n_dev < n ? *n_dev : n;
+  if (ts) {
+    // async table scan: the decoded total and the chunk count against the workspace, decided alike by every
+    // workgroup from the scans; workgroup 0 records it (over: the host path; no chunk: nothing to decode)
+    const uint64_t m = ts->status == 0 ? n : 0;
+    const uint64_t total = m ? out_off[m] : 0, chunks = m ? chunk_off[m] : 0;
+    const bool over = total > ts_out_cap || chunks > ts_chunk_cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      ts->need_out = total;
+      ts->need_chunks = chunks;
+      ts->gate = over ? 1u : chunks == 0 ? 2u : 0u;
+      ts->n_chunks = over ? 0 : chunks;  // the chunk count the CRC pass and the check read
+      if (over && ts->status == 0) ts->status = 2;  // TS_HOST
+    }
+    if (over || chunks == 0) return;
+  }
   uint8_t* const lin = sn_lds;
   uint8_t* const lout = sn_lds + in_lim + SN_SLACK;
   const uint32_t lane = __lane_id();
@@ -2366,7 +2393,12 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
 // pass 1 over the restart segments, the count taken from the device state (grid-stride)
 __global__ void __launch_bounds__(256) k_ts_count(const uint8_t* __restrict__ file, uint64_t file_len,
                                                   const lcrc_tscan_dev* __restrict__ st, uint64_t* __restrict__ count,
-                                                  uint64_t* __restrict__ flag) {
+                                                  uint64_t* __restrict__ flag, uint32_t* __restrict__ zero,
+                                                  uint64_t nzero, uint32_t* __restrict__ zero2) {
+  // the batch's mismatch bitmap and the Snappy maxima start at zero (no memset launches)
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (uint64_t)gridDim.x * blockDim.x)
+    zero[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
   if (st->status != TS_OK) return;
   const uint64_t nres = st->nres;
   const uint8_t* d = file + st->idx_off;
@@ -2375,25 +2407,64 @@ __global__ void __launch_bounds__(256) k_ts_count(const uint8_t* __restrict__ fi
     idx_segment<false>(d, len, (uint32_t)nres, file_len, count, flag, nullptr, nullptr, nullptr, i);
 }
 
-// after the scan of the counts: the data-block total, the capacity check, the fallback flags; then pass 2
-// writes the handles and thread 0 appends the filter, metaindex and index blocks with their descriptors
+// after the scan of the counts: the data-block total, the capacity check and the fallback flags (decided
+// alike by every workgroup from the scan; workgroup 0 records them), then pass 2 writes the handles and
+// thread 0 appends the filter, metaindex and index blocks with their descriptors
 __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
                                                  lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ pos,
                                                  const uint64_t* __restrict__ fpos, lcrc_tblk_dev* __restrict__ out,
                                                  lcrc_desc_dev* __restrict__ descs, uint64_t cap) {
-  if (st->status != TS_OK) return;
+  const uint32_t status = st->status;  // as k_ts_open left it (workgroup 0 changes it only to a non-OK value)
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  if (status != TS_OK) {
+    if (lead) st->n_total = 0;
+    return;
+  }
   const uint64_t nres = st->nres;
   const uint64_t nd = nres ? pos[nres] : 0;
-  if (nres && fpos[nres]) return;  // a segment the device walk cannot vouch for: k_ts_final reports it
-  const uint64_t ntot = nd + (st->has_filter ? 3 : 2);
-  if (ntot > cap) return;
+  const bool hf = st->has_filter;
+  const uint64_t ntot = nd + (hf ? 3 : 2);
+  if (nres && fpos[nres]) {
+    // a segment the device walk cannot vouch for. The reference checks the index block's checksum before its
+    // contents: verify it alone, and let the host walk give the contents' message only if it holds
+    if (lead) {
+      st->n_total = cap ? 1 : 0;
+      if (!cap) {
+        st->status = TS_HOST;
+        return;
+      }
+      st->idx_only = 1;
+      lcrc_tblk_dev b = {};
+      b.offset = st->idx_off;
+      b.size = st->idx_size;
+      b.kind = 3;  // LCRC_TBLK_INDEX
+      lcrc_desc_dev dd;
+      dd.offset = st->idx_off;
+      dd.length = (uint32_t)(st->idx_size + 1);  // in the file: checked by k_ts_open
+      dd.expect_rel = (int32_t)(st->idx_size + 1);
+      out[0] = b;
+      descs[0] = dd;
+    }
+    return;
+  }
+  if (ntot > cap) {
+    if (lead) {
+      st->status = TS_CAPACITY;
+      st->n_data = ntot;  // the capacity needed (reported); n_total stays 0: nothing is verified
+      st->n_total = 0;
+    }
+    return;
+  }
+  if (lead) {
+    st->n_data = nd;
+    st->n_total = ntot;
+  }
   const uint8_t* d = file + st->idx_off;
   const uint32_t len = (uint32_t)st->idx_size;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nres; i += (uint64_t)gridDim.x * blockDim.x)
     idx_segment<true>(d, len, (uint32_t)nres, file_len, nullptr, nullptr, pos, out, descs, i);
   if (blockIdx.x == 0 && threadIdx.x < 3) {
     const uint32_t k = threadIdx.x;  // 0 filter (if any), then metaindex, index
-    const bool hf = st->has_filter;
     if (k == 0 && !hf) return;
     const uint64_t at = nd + (hf ? k : k - 1);
     const uint64_t off = k == 0 ? st->filt_off : k == 1 ? st->meta_off : st->idx_off;
@@ -2420,50 +2491,54 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
   }
 }
 
-// the result count for the batch kernels (status, capacity and fallback resolved first)
-__global__ void __launch_bounds__(64) k_ts_count_total(lcrc_tscan_dev* __restrict__ st,
-                                                       const uint64_t* __restrict__ pos,
-                                                       const uint64_t* __restrict__ fpos, uint64_t cap) {
-  if (threadIdx.x != 0) return;
-  st->n_total = 0;
-  if (st->status != TS_OK) return;
-  const uint64_t nres = st->nres;
-  if (nres && fpos[nres]) {
-    st->status = TS_HOST;
-    return;
+// read_block_from_file's type dispatch for every block (k_tbl_finish) and, in the same thread, the framing
+// walk of the block's Snappy frame (k_snappy_size)
+__global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
+                                                   const uint32_t* __restrict__ crc,
+                                                   const uint32_t* __restrict__ mismatch,
+                                                   const uint8_t* __restrict__ file, lcrc_desc_dev* __restrict__ frames,
+                                                   uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
+                                                   uint8_t* __restrict__ fstatus, const uint64_t* __restrict__ n_dev) {
+  n = *n_dev < n ? *n_dev : n;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  lcrc_tblk_dev b = blk[i];
+  uint32_t foff = 0, flen = 0;
+  if (b.status != 2) {
+    b.crc = crc[i];
+    b.type = file[b.offset + b.size];
+    b.status = (mismatch[i >> 5] >> (i & 31)) & 1;
+    if (b.status == 0 && b.type > 1) b.status = 4;  // LCRC_TBLK_BAD_TYPE
+    if (b.status == 0 && b.type == 1) flen = (uint32_t)b.size;
   }
-  const uint64_t nd = nres ? pos[nres] : 0;
-  const uint64_t ntot = nd + (st->has_filter ? 3 : 2);
-  st->n_data = nd;
-  if (ntot > cap) {
-    st->status = TS_CAPACITY;
-    st->n_data = ntot;  // the capacity needed (reported); n_total stays 0: nothing is verified
-    return;
-  }
-  st->n_total = ntot;
+  lcrc_desc_dev f;
+  f.offset = flen ? b.offset : 0;
+  f.length = flen;
+  f.expect_rel = LCRC_NO_EXPECT_DEV;
+  blk[i] = b;
+  frames[i] = f;
+  uint64_t total, chunks;
+  uint32_t mi, mo;
+  const bool ok = snappy_frame_size(file + f.offset, flen, total, chunks, mi, mo);
+  (void)foff;
+  size[i] = ok ? total : 0;
+  nchunks[i] = ok ? chunks : 0;
+  fstatus[i] = ok ? 0 : 1;
 }
 
-// the Snappy frames' decoded total against the output capacity: gate the decode (host fallback when over)
-__global__ void __launch_bounds__(64) k_ts_gate(lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ out_off,
-                                                const uint64_t* __restrict__ chunk_off, uint64_t out_cap,
-                                                uint64_t chunk_cap) {
-  if (threadIdx.x != 0) return;
-  const uint64_t n = st->status == TS_OK ? st->n_total : 0;
-  const uint64_t total = n ? out_off[n] : 0, chunks = n ? chunk_off[n] : 0;
-  const bool over = total > out_cap || chunks > chunk_cap;
-  st->gate = over ? 1u : 0u;
-  st->need_out = total;
-  st->need_chunks = chunks;
-  st->n_chunks = over ? 0 : chunks;  // the chunk count the CRC pass and the check read
-  if (over && st->status == TS_OK) st->status = TS_HOST;
-}
-
-// the reference's order of outcomes, once every checksum is known
-__global__ void __launch_bounds__(64) k_ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
-                                                 uint64_t* __restrict__ n_out) {
-  if (threadIdx.x != 0) return;
+// the reference's order of outcomes, once every checksum is known; the count and the status for the caller
+__device__ void ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk, uint64_t* __restrict__ n_out,
+                         uint32_t* __restrict__ status_out) {
   lcrc_tscan_dev s = *st;
-  if (s.status == TS_OK) {
+  if (s.status == TS_OK && s.idx_only) {
+    if (blk[0].status == 1) {
+      s.status = TS_CORRUPT;
+      s.code = TSM_CHECKSUM;
+    } else {
+      s.status = TS_HOST;
+    }
+    s.n_total = 0;
+  } else if (s.status == TS_OK) {
     const uint64_t n = s.n_total;
     const lcrc_tblk_dev ix = blk[n - 1];  // the index block, last
     if (ix.status == 1) {
@@ -2481,6 +2556,30 @@ __global__ void __launch_bounds__(64) k_ts_final(lcrc_tscan_dev* __restrict__ st
   }
   *st = s;
   *n_out = s.status == TS_OK ? s.n_total : s.status == TS_CAPACITY ? s.n_data : 0;
+  status_out[0] = s.status;
+  status_out[1] = s.code;
+}
+
+// the Snappy frames' verdicts into the blocks' status and the order check (k_tbl_content); the last
+// workgroup to finish then applies ts_final (a self-resetting arrival counter in the state)
+__global__ void __launch_bounds__(256) k_ts_content(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
+                                                    const uint8_t* __restrict__ fstatus, lcrc_tscan_dev* __restrict__ st,
+                                                    uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out) {
+  __shared__ uint32_t last;
+  const uint64_t m = st->n_total < n ? st->n_total : n;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) {
+    if (i > 0 && blk[i - 1].offset > blk[i].offset) st->unsorted = 1;
+    if (fstatus[i]) blk[i].status = 3;  // LCRC_TBLK_BAD_CONTENT
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&st->arrive, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  st->arrive = 0;
+  ts_final(st, blk, n_out, status_out);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2605,28 +2704,34 @@ hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcr
 }
 // grid: a bound on the restart segments (the workgroups past the device count return at once)
 hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
-                                uint64_t* flag, uint64_t bound, hipStream_t s) {
+                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero, uint32_t* zero2,
+                                hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
   hipLaunchKernelGGL(lcrc_dev::k_ts_count, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
-                     count, flag);
+                     count, flag, zero, nzero, zero2);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
                                const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t bound, hipStream_t s) {
-  hipLaunchKernelGGL(lcrc_dev::k_ts_count_total, dim3(1), dim3(64), 0, s, st, pos, fpos, cap);
   const uint64_t g = bound / 256 + 1;
   hipLaunchKernelGGL(lcrc_dev::k_ts_emit, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
                      pos, fpos, out, descs, cap);
   return hipGetLastError();
 }
-hipError_t lcrc_launch_ts_gate(lcrc_tscan_dev* st, const uint64_t* out_off, const uint64_t* chunk_off, uint64_t out_cap,
-                               uint64_t chunk_cap, hipStream_t s) {
-  hipLaunchKernelGGL(lcrc_dev::k_ts_gate, dim3(1), dim3(64), 0, s, st, out_off, chunk_off, out_cap, chunk_cap);
+hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
+                                 const uint8_t* file, lcrc_desc_dev* frames, uint64_t* size, uint64_t* nchunks,
+                                 uint8_t* fstatus, const uint64_t* n_dev, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lcrc_dev::k_ts_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, blk, n, crc, mismatch,
+                     file, frames, size, nchunks, fstatus, n_dev);
   return hipGetLastError();
 }
-hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, hipStream_t s) {
-  hipLaunchKernelGGL(lcrc_dev::k_ts_final, dim3(1), dim3(64), 0, s, st, blk, n_out);
+// grid sized by the bound n (at least one workgroup: the last to arrive writes the outcome)
+hipError_t lcrc_launch_ts_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, lcrc_tscan_dev* st,
+                                  uint64_t* n_out, uint32_t* status_out, hipStream_t s) {
+  hipLaunchKernelGGL(lcrc_dev::k_ts_content, dim3((unsigned)(n / 256 + 1)), dim3(256), 0, s, blk, n, fstatus, st, n_out,
+                     status_out);
   return hipGetLastError();
 }
 
@@ -2710,7 +2815,8 @@ hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, u
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
-                                     uint32_t max_out, const uint64_t* n_dev, const uint32_t* gate, hipStream_t st) {
+                                     uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
+                                     uint64_t ts_chunk_cap, hipStream_t st) {
   using lcrc_dev::SN_MAX;
   if (n == 0) return hipSuccess;
   const uint64_t g = n < 16384 ? n : 16384;  // one wave per frame, grid-stride
@@ -2719,7 +2825,8 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
   const uint32_t out_cap = max_out < SN_MAX ? (max_out + 15) & ~15u : SN_MAX;
   const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
   hipLaunchKernelGGL(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
-                     chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, gate);
+                     chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, ts, ts_out_cap,
+                     ts_chunk_cap);
   return hipGetLastError();
 }
 

@@ -121,7 +121,7 @@ def test_async_handles_and_host_cases(lcrc, orc, engines):
     v = orc.varint
     cases = {
         "past end": (_handcrafted(orc, [(b"a", v(0) + v(100)), (b"b", v(10 ** 6) + v(50))]), (OK, HOST)),
-        "bad varint": (_handcrafted(orc, [(b"a", b"\xff\xff")]), (CORRUPT,)),
+        "bad varint": (_handcrafted(orc, [(b"a", b"\xff\xff")]), (CORRUPT, HOST)),
         "snappy index": (_handcrafted(orc, [(b"a", v(0) + v(100))], index_type=1), (HOST,)),
         "no filter entry": (_handcrafted(orc, [(b"a", v(0) + v(100))], meta_entries=[(b"filterother", v(0) + v(1))]),
                             (OK,)),
