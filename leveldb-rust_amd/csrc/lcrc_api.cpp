@@ -33,16 +33,17 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                lcrc_tscan_dev* st, hipStream_t s);
 hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
-                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero, uint32_t* zero2,
+                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero,
                                 hipStream_t s);
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
                                const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t bound, hipStream_t s);
+                               uint64_t vcap, uint64_t bound, hipStream_t s);
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* size, uint64_t* nchunks,
-                                 uint8_t* fstatus, const uint64_t* n_dev, hipStream_t s);
-hipError_t lcrc_launch_ts_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, lcrc_tscan_dev* st,
-                                  uint64_t* n_out, uint32_t* status_out, hipStream_t s);
+                                 uint8_t* fstatus, const lcrc_tscan_dev* st, const uint32_t* gtab, uint32_t flags,
+                                 hipStream_t s);
+hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, uint32_t* status_out,
+                               hipStream_t s);
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
@@ -171,6 +172,7 @@ struct lcrc_ctx {
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
   void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
   uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
+  int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan (LCRC_TS_BLOCKS_DIV, measurement)
 };
 
 namespace {
@@ -183,6 +185,7 @@ int upload_tables(int mode, uint32_t** d_tab) {
   for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 16ull << m, tab.data() + TAB_ZPIECE + m * 1024);
   for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 256ull << m, tab.data() + TAB_ZWIN + m * 1024);
   lcrc::make_shift_tables(poly, 4096, tab.data() + TAB_Z4096);
+  lcrc::make_shift_tables(poly, LCRC_TS_PIECE, tab.data() + TAB_Z64K);
   // k_windows builds its LDS image from columns (entries 1, 2, 4, .., 128) of the byte tables it uses
   for (int t = 0; t < 20; ++t) {
     const uint32_t src = t < 4 ? TAB_SLICE + t * 256                    // S0: T_p
@@ -295,6 +298,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   ctx->poly = poly;
   ctx->x4096 = lcrc::x8n(4096, poly);
   if (const char* g = getenv("LCRC_GENERAL")) ctx->general = !strcmp(g, "ranges") ? 1 : !strcmp(g, "blocks") ? 2 : 0;
+  if (const char* g = getenv("LCRC_TS_BLOCKS_DIV")) ctx->ts_blocks_div = std::max(1, atoi(g));
   *out = ctx;
   return LCRC_OK;
 }
@@ -907,15 +911,21 @@ static uint64_t ts_chunk_cap(size_t max_blocks, uint64_t decoded_cap) {
   return 2ull * max_blocks + decoded_cap / 1024 + 64;
 }
 
+// the batched verify's descriptors: the blocks and the pieces of a long filter / metaindex / index block
+static uint64_t ts_verify_cap(size_t max_blocks, uint64_t file_len) {
+  return max_blocks + 1 + file_len / LCRC_TS_PIECE + 3;
+}
+
 static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap, uint64_t chunks) {
   int rc = set_device(ctx);
   if (rc) return rc;
   const uint64_t nb = max_blocks + 1;
+  const uint64_t nv = ts_verify_cap(max_blocks, max_file_len);
   const uint64_t cc = std::max<uint64_t>(std::max(ts_chunk_cap(max_blocks, decoded_cap), chunks), ctx->ts_chunk_cap);
   decoded_cap = std::max<uint64_t>(decoded_cap, ctx->ts_decoded_cap);
   if ((rc = ctx->ts_state.ensure(1)) || (rc = ctx->idx_count.ensure(nb)) || (rc = ctx->idx_flag.ensure(nb)) ||
       (rc = ctx->idx_pos.ensure(nb)) || (rc = ctx->idx_fpos.ensure(nb)) || (rc = ctx->sn_part.ensure(2 * (nb / 256 + 2))) ||
-      (rc = ctx->tbl_descs.ensure(nb)) || (rc = ctx->tbl_crcs.ensure(nb)) || (rc = ctx->tbl_mm.ensure(nb / 32 + 1)) ||
+      (rc = ctx->tbl_descs.ensure(nv)) || (rc = ctx->tbl_crcs.ensure(nv)) || (rc = ctx->tbl_mm.ensure(nv / 32 + 1)) ||
       (rc = ctx->tbl_frames.ensure(nb)) || (rc = ctx->sn_size.ensure(nb)) || (rc = ctx->sn_nch.ensure(nb)) ||
       (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) || (rc = ctx->sn_status.ensure(nb)) ||
       (rc = ctx->sn_max.ensure(2)) || (rc = ctx->sn_cdesc.ensure(cc)) || (rc = ctx->sn_cexp.ensure(cc)) ||
@@ -958,29 +968,32 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   HIPCHK(lcrc_launch_ts_open(file, file_len, &key, cap, S, st));
   // the index block's restart segments: entry counts, their scan, the handles and the verify descriptors
   const uint64_t* nres_dev = &S->nres;
-  HIPCHK(lcrc_launch_ts_count(file, file_len, S, ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->tbl_mm.p, cap / 32 + 1,
-                              (uint32_t*)ctx->sn_max.p, st));
+  const uint64_t vcap = ts_verify_cap(cap, file_len);
+  HIPCHK(lcrc_launch_ts_count(file, file_len, S, ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->tbl_mm.p, vcap / 32 + 1,
+                              st));
   HIPCHK(lcrc_launch_scan2(ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->idx_pos.p, ctx->idx_fpos.p, ctx->sn_part.p,
                            nres_dev, st));
-  HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_pos.p, ctx->idx_fpos.p, blk, ctx->tbl_descs.p, cap, cap, st));
-  // ONE batched verify of every block (data, filter, metaindex, index) over the file
+  HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_pos.p, ctx->idx_fpos.p, blk, ctx->tbl_descs.p, cap, vcap, cap,
+                             st));
+  // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
   const uint64_t* ntot = &S->n_total;
+  const uint64_t* nver = &S->n_verify;
   if (cap) {
     if (ctx->general == 1) {  // LCRC_GENERAL=ranges: the one-pass kernel
-      HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, file, file_len, ctx->tbl_descs.p, cap, 0, 0, nullptr, ctx->d_tab,
+      HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, file, file_len, ctx->tbl_descs.p, vcap, 0, 0, nullptr, ctx->d_tab,
                                 ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
-                                ctx->tbl_crcs.p, ctx->tbl_mm.p, ntot, nullptr, st));
+                                ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     } else {
       HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
                                  st));
-      HIPCHK(lcrc_launch_blocks(false, ctx->grid_b, file, file_len, ctx->tbl_descs.p, cap, 0, 0,
+      HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / ctx->ts_blocks_div, file, file_len, ctx->tbl_descs.p, vcap, 0, 0,
                                 nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
-                                ctx->tbl_crcs.p, ctx->tbl_mm.p, ntot, nullptr, st));
+                                ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     }
     // read_block_from_file's type dispatch and the Snappy framing walk; the frames decoded (the decoded total
     // checked against the workspace on the device) and their chunks' masked CRC-32C checked
     HIPCHK(lcrc_launch_ts_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ctx->sn_size.p,
-                                 ctx->sn_nch.p, ctx->sn_status.p, ntot, st));
+                                 ctx->sn_nch.p, ctx->sn_status.p, S, ctx->d_tab, ctx->flags, st));
     HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_part.p,
                              ntot, st));
     HIPCHK(lcrc_launch_snappy_decode(file, ctx->tbl_frames.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_out.p,
@@ -991,9 +1004,10 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
                               LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr, &S->n_chunks, nullptr, st));
     HIPCHK(lcrc_launch_snappy_check(ctx->sn_ccrc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, &S->n_chunks, ctx->ts_chunk_cap,
                                     ctx->sn_status.p, st));
+    HIPCHK(lcrc_launch_tbl_content(blk, cap, ctx->sn_status.p, &S->unsorted, 1, ntot, st));
   }
-  // the frames' verdicts, then (last workgroup) the reference's order of outcomes, the count and the status
-  HIPCHK(lcrc_launch_ts_content(blk, cap, ctx->sn_status.p, S, n_blocks, status, st));
+  // the reference's order of outcomes; the count and the status for the caller
+  HIPCHK(lcrc_launch_ts_final(S, blk, n_blocks, status, st));
   return LCRC_OK;
 }
 

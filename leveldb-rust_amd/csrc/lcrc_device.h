@@ -22,7 +22,8 @@ enum : int {
   TAB_XCH = 14497,    // x^(8 * 4096 * k) mod P for k = 0..4095 (k_ranges: place a shared range's chunk)
   TAB_SCOLS = 18600,  // the queued fast path's block shifts as columns: Z_{256 k}, k = 0..15, byte position q =
                       // 0..3 (table index 4 k + q, entry b = Z_{256 k}(b << 8 q)), 8 columns each
-  TAB_TOTAL = 19112,
+  TAB_Z64K = 19112,   // Z65536 (the async table scan joins the 64 KiB pieces of a long block)
+  TAB_TOTAL = 20136,
 };
 
 struct lcrc_desc_dev {  // == lcrc_desc
@@ -75,8 +76,13 @@ struct lcrc_tscan_dev {
   uint32_t unsorted, gate;
   uint64_t need_out, need_chunks;  // the decoded bytes and chunks the Snappy frames need (set by the gate)
   uint32_t idx_only;  // a restart segment the device walk cannot vouch for: only the index block is verified
-  uint32_t arrive;    // k_ts_content's arrival counter (the last workgroup applies the outcome; reset by it)
+  uint32_t pad;
+  uint64_t n_verify;  // descriptors of the batched verify: the n_total blocks and the pieces below
+  // filter, metaindex, index: a block longer than LCRC_TS_PIECE is verified as pieces of that size (one row of
+  // the batch kernel each, instead of one row folding thousands of windows), combined afterwards
+  uint32_t pbase[3], pcnt[3];
 };
+#define LCRC_TS_PIECE 65536
 struct lcrc_tscan_key {  // the metaindex key read_meta looks for: "filter" + the policy name
   uint32_t len;          // 0: no filter policy
   uint8_t key[124];

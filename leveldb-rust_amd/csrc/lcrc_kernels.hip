@@ -2394,11 +2394,10 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
 __global__ void __launch_bounds__(256) k_ts_count(const uint8_t* __restrict__ file, uint64_t file_len,
                                                   const lcrc_tscan_dev* __restrict__ st, uint64_t* __restrict__ count,
                                                   uint64_t* __restrict__ flag, uint32_t* __restrict__ zero,
-                                                  uint64_t nzero, uint32_t* __restrict__ zero2) {
-  // the batch's mismatch bitmap and the Snappy maxima start at zero (no memset launches)
+                                                  uint64_t nzero) {
+  // the batch's mismatch bitmap starts at zero (no memset launch)
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (uint64_t)gridDim.x * blockDim.x)
     zero[i] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
   if (st->status != TS_OK) return;
   const uint64_t nres = st->nres;
   const uint8_t* d = file + st->idx_off;
@@ -2413,7 +2412,7 @@ __global__ void __launch_bounds__(256) k_ts_count(const uint8_t* __restrict__ fi
 __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
                                                  lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ pos,
                                                  const uint64_t* __restrict__ fpos, lcrc_tblk_dev* __restrict__ out,
-                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap) {
+                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap, uint64_t vcap) {
   const uint32_t status = st->status;  // as k_ts_open left it (workgroup 0 changes it only to a non-OK value)
   const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
   if (status != TS_OK) {
@@ -2429,6 +2428,7 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     // contents: verify it alone, and let the host walk give the contents' message only if it holds
     if (lead) {
       st->n_total = cap ? 1 : 0;
+      st->n_verify = st->n_total;
       if (!cap) {
         st->status = TS_HOST;
         return;
@@ -2455,9 +2455,23 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     }
     return;
   }
+  // the filter, metaindex and index blocks (k = 0, 1, 2): in the file, and split into pieces when long
+  uint64_t offk[3], sizek[3], npk[3];
+  bool ink[3];
+  uint64_t npieces = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    offk[k] = k == 0 ? st->filt_off : k == 1 ? st->meta_off : st->idx_off;
+    sizek[k] = k == 0 ? st->filt_size : k == 1 ? st->meta_size : st->idx_size;
+    ink[k] = (k > 0 || hf) && offk[k] <= file_len && sizek[k] + 5 <= file_len - offk[k] && sizek[k] + 1 <= 0x7FFFFFFFull;
+    npk[k] = ink[k] && sizek[k] + 1 > LCRC_TS_PIECE ? (sizek[k] + LCRC_TS_PIECE) / LCRC_TS_PIECE : 0;
+    npieces += npk[k];
+  }
+  const bool split = ntot + npieces <= vcap;
   if (lead) {
     st->n_data = nd;
     st->n_total = ntot;
+    st->n_verify = ntot + (split ? npieces : 0);
   }
   const uint8_t* d = file + st->idx_off;
   const uint32_t len = (uint32_t)st->idx_size;
@@ -2467,8 +2481,22 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     const uint32_t k = threadIdx.x;  // 0 filter (if any), then metaindex, index
     if (k == 0 && !hf) return;
     const uint64_t at = nd + (hf ? k : k - 1);
-    const uint64_t off = k == 0 ? st->filt_off : k == 1 ? st->meta_off : st->idx_off;
-    const uint64_t size = k == 0 ? st->filt_size : k == 1 ? st->meta_size : st->idx_size;
+    const uint64_t off = offk[k], size = sizek[k];
+    const bool in = ink[k];
+    if (split && npk[k]) {
+      // the first piece takes the remainder, so that every later piece is joined by the same Z65536
+      const uint64_t first = ntot + (k > 0 ? npk[0] : 0) + (k > 1 ? npk[1] : 0);
+      const uint64_t r = size + 1 - (npk[k] - 1) * LCRC_TS_PIECE;
+      st->pbase[k] = (uint32_t)first;
+      st->pcnt[k] = (uint32_t)npk[k];
+      for (uint64_t q = 0; q < npk[k]; ++q) {
+        lcrc_desc_dev pd;
+        pd.offset = q ? off + r + (q - 1) * LCRC_TS_PIECE : off;
+        pd.length = (uint32_t)(q ? LCRC_TS_PIECE : r);
+        pd.expect_rel = LCRC_NO_EXPECT_DEV;
+        descs[first + q] = pd;
+      }
+    }
     lcrc_tblk_dev b;
     b.offset = off;
     b.size = size;
@@ -2478,10 +2506,10 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     b.status = 0;
     b.reserved = 0;
     lcrc_desc_dev dd;
-    const bool in = off <= file_len && size + 5 <= file_len - off && size + 1 <= 0x7FFFFFFFull;
+    const bool whole = in && !(split && npk[k]);  // a split block's own descriptor is empty
     dd.offset = in ? off : 0;
-    dd.length = in ? (uint32_t)(size + 1) : 0;
-    dd.expect_rel = in ? (int32_t)(size + 1) : LCRC_NO_EXPECT_DEV;
+    dd.length = whole ? (uint32_t)(size + 1) : 0;
+    dd.expect_rel = whole ? (int32_t)(size + 1) : LCRC_NO_EXPECT_DEV;
     if (!in) {
       b.status = 2;  // LCRC_TBLK_TRUNCATED
       b.type = 0xFF;
@@ -2498,16 +2526,51 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
                                                    const uint32_t* __restrict__ mismatch,
                                                    const uint8_t* __restrict__ file, lcrc_desc_dev* __restrict__ frames,
                                                    uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
-                                                   uint8_t* __restrict__ fstatus, const uint64_t* __restrict__ n_dev) {
-  n = *n_dev < n ? *n_dev : n;
+                                                   uint8_t* __restrict__ fstatus, const lcrc_tscan_dev* __restrict__ st,
+                                                   const uint32_t* __restrict__ gtab, uint32_t flags) {
+  __shared__ uint32_t z64k[1024];
+  n = st->n_total < n ? st->n_total : n;
+  const uint64_t nd = st->n_data;
+  const bool hf = st->has_filter;
+  // the workgroup holding a split block's entry stages Z65536 in LDS (uniform decision)
+  bool stage = false;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k) {
+    const uint64_t e = nd + k - (hf ? 0 : 1);
+    stage |= st->pcnt[k] && (k > 0 || hf) && e < n && e / blockDim.x == blockIdx.x;
+  }
+  if (stage) {
+    for (uint32_t j = threadIdx.x; j < 1024; j += blockDim.x) z64k[j] = gtab[TAB_Z64K + j];
+    __syncthreads();
+  }
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   lcrc_tblk_dev b = blk[i];
-  uint32_t foff = 0, flen = 0;
+  uint32_t flen = 0;
   if (b.status != 2) {
     b.crc = crc[i];
     b.type = file[b.offset + b.size];
     b.status = (mismatch[i >> 5] >> (i & 31)) & 1;
+    const uint32_t k = i < nd ? 3u : (uint32_t)(i - nd) + (hf ? 0u : 1u);
+    if (k < 3 && st->pcnt[k]) {
+      // a block verified as pieces: crc(A || B) = Z_|B|(crc(A)) ^ crc(B) (init = xorout = ~0); every piece
+      // after the first is 64 KiB long
+      const uint32_t* pc = crc + st->pbase[k];
+      const uint32_t np = st->pcnt[k];
+      const bool masked = flags & LCRC_FLAG_MASK;
+      auto unmask = [&](uint32_t v) {
+        if (!masked) return v;
+        const uint32_t r = v - 0xa282ead8u;
+        return (r >> 17) | (r << 15);
+      };
+      uint32_t c = unmask(pc[0]);
+      for (uint32_t q = 1; q < np; ++q)
+        c = z64k[c & 0xff] ^ z64k[256 + ((c >> 8) & 0xff)] ^ z64k[512 + ((c >> 16) & 0xff)] ^ z64k[768 + (c >> 24)] ^
+            unmask(pc[q]);
+      if (masked) c = mask32c(c);
+      b.crc = c;
+      b.status = c != load_le32(file + b.offset + b.size + 1);
+    }
     if (b.status == 0 && b.type > 1) b.status = 4;  // LCRC_TBLK_BAD_TYPE
     if (b.status == 0 && b.type == 1) flen = (uint32_t)b.size;
   }
@@ -2520,7 +2583,6 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
   uint64_t total, chunks;
   uint32_t mi, mo;
   const bool ok = snappy_frame_size(file + f.offset, flen, total, chunks, mi, mo);
-  (void)foff;
   size[i] = ok ? total : 0;
   nchunks[i] = ok ? chunks : 0;
   fstatus[i] = ok ? 0 : 1;
@@ -2560,26 +2622,9 @@ __device__ void ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restr
   status_out[1] = s.code;
 }
 
-// the Snappy frames' verdicts into the blocks' status and the order check (k_tbl_content); the last
-// workgroup to finish then applies ts_final (a self-resetting arrival counter in the state)
-__global__ void __launch_bounds__(256) k_ts_content(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
-                                                    const uint8_t* __restrict__ fstatus, lcrc_tscan_dev* __restrict__ st,
-                                                    uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out) {
-  __shared__ uint32_t last;
-  const uint64_t m = st->n_total < n ? st->n_total : n;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m) {
-    if (i > 0 && blk[i - 1].offset > blk[i].offset) st->unsorted = 1;
-    if (fstatus[i]) blk[i].status = 3;  // LCRC_TBLK_BAD_CONTENT
-  }
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&st->arrive, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  __threadfence();
-  st->arrive = 0;
-  ts_final(st, blk, n_out, status_out);
+__global__ void __launch_bounds__(64) k_ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
+                                                 uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out) {
+  if (threadIdx.x == 0) ts_final(st, blk, n_out, status_out);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2704,34 +2749,33 @@ hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcr
 }
 // grid: a bound on the restart segments (the workgroups past the device count return at once)
 hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
-                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero, uint32_t* zero2,
+                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero,
                                 hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
   hipLaunchKernelGGL(lcrc_dev::k_ts_count, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
-                     count, flag, zero, nzero, zero2);
+                     count, flag, zero, nzero);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
                                const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t bound, hipStream_t s) {
+                               uint64_t vcap, uint64_t bound, hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
   hipLaunchKernelGGL(lcrc_dev::k_ts_emit, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
-                     pos, fpos, out, descs, cap);
+                     pos, fpos, out, descs, cap, vcap);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* size, uint64_t* nchunks,
-                                 uint8_t* fstatus, const uint64_t* n_dev, hipStream_t s) {
+                                 uint8_t* fstatus, const lcrc_tscan_dev* st, const uint32_t* gtab, uint32_t flags,
+                                 hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(lcrc_dev::k_ts_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, blk, n, crc, mismatch,
-                     file, frames, size, nchunks, fstatus, n_dev);
+                     file, frames, size, nchunks, fstatus, st, gtab, flags);
   return hipGetLastError();
 }
-// grid sized by the bound n (at least one workgroup: the last to arrive writes the outcome)
-hipError_t lcrc_launch_ts_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, lcrc_tscan_dev* st,
-                                  uint64_t* n_out, uint32_t* status_out, hipStream_t s) {
-  hipLaunchKernelGGL(lcrc_dev::k_ts_content, dim3((unsigned)(n / 256 + 1)), dim3(256), 0, s, blk, n, fstatus, st, n_out,
-                     status_out);
+hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, uint32_t* status_out,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(lcrc_dev::k_ts_final, dim3(1), dim3(64), 0, s, st, blk, n_out, status_out);
   return hipGetLastError();
 }
 

@@ -221,3 +221,30 @@ def test_async_graph_replay(lcrc, orc):
             eng.graph_destroy(g)
         s.close()
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,masked", [(0, False), (1, True)])
+def test_async_long_meta_blocks(lcrc, orc, mode, masked):
+    """An index block and a filter block longer than LCRC_TS_PIECE are verified as 64 KiB pieces and combined
+    (crc(A || B) = x^(8|B|) crc(A) ^ crc(B)): same CRCs and verdicts as the oracle, clean and corrupted."""
+    eng = lcrc.Engine(0, mode, lcrc.FLAG_MASK if masked else 0)
+    try:
+        kvs = _kvs(40000, 77, vlen=12)
+        f, blocks = orc.table_build(kvs, block_size=128, compression=0, filter_name=FILTER,
+                                    filter_block=os.urandom(200_003), mode=mode, masked=masked)
+        ih = [b for b in blocks if b[2] == 3][0]
+        fb = [b for b in blocks if b[2] == 1][0]
+        assert ih[1] + 1 > 2 * 65536 and fb[1] + 1 > 3 * 65536  # several pieces each, a partial last one
+        assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks) + 4, mode=mode, masked=masked) == OK
+        g = bytearray(f)
+        g[fb[0] + 70000] ^= 0x08  # inside the filter's second piece: that block's status only
+        assert _expect_async(lcrc, eng, orc, bytes(g), FILTER, cap=len(blocks) + 4, mode=mode, masked=masked) == OK
+        g = bytearray(f)
+        g[ih[0] + ih[1] - 100] ^= 0x01  # inside the index's last piece: Table::open fails
+        assert _expect_async(lcrc, eng, orc, bytes(g), FILTER, cap=len(blocks) + 4, mode=mode, masked=masked) in (
+            CORRUPT, HOST)
+        got, err = _sync(lcrc, eng, bytes(g), FILTER)
+        assert err == "block checksum mismatch"
+    finally:
+        eng.close()
