@@ -15,11 +15,11 @@ tail -1 "$OUT/smoke.log"
 # the driver's headline command, then the other BASELINE configs
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --extra-out "profiles/${R}_bench_fixed_c.json" > "$OUT/bench_fixed.json" 2> "$OUT/bench_fixed.err" || { tail -20 "$OUT/bench_fixed.err"; exit 1; }
 cat "$OUT/bench_fixed.json"
-for c in mixed wal; do
+for c in mixed wal table; do
   timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --config $c --extra-out "profiles/${R}_bench_${c}_c.json" > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }
   cut -c1-400 "$OUT/bench_$c.json"
 done
-for c in fixed mixed wal; do
+for c in fixed mixed wal table; do
   timeout -k 10 900 bash tools/profile_round.sh $R $c c > "$OUT/prof_$c.log" 2>&1 || { tail -20 "$OUT/prof_$c.log"; exit 1; }
   python3 -c "import json;s=json.load(open('profiles/${R}_${c}_c_summary.json'));print('$c', s.get('kernel'), s.get('avg_us'), s.get('frac'), s.get('bench_line'))"
 done
