@@ -28,6 +28,7 @@
  *                                          kernel, D2H, double-buffered)
  *   lcrc_wal_scan / lcrc_wal_scan_async <- the header parse + CRC verify of (2) for every physical record
  *                                          of a device-resident log file, 32 KiB block by block
+ *   lcrc_tb_* + lcrc_batch_seal         <- TableBuilder (table.rs:344-529) with the trailers sealed in batch
  *   lcrc_table_scan[_async]             <- Table::open with paranoid_checks (table.rs:39-103) followed by
  *                                          read_block_from_file(verify_checksum) (format.rs:146-171) of
  *                                          every data, filter, metaindex and index block: one batched verify
@@ -247,6 +248,24 @@ const char* lcrc_table_scan_message(uint32_t code);
  * also receives the values. Covered ranges must not contain another descriptor's CRC slot. */
 int lcrc_batch_seal(lcrc_ctx* ctx, uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
                     uint32_t* out_crc, void* stream);
+
+/* The SSTable writer (TableBuilder, src/sstable/table.rs:344-529: data blocks with restart points, the
+ * filter block written raw under the table's compression type (table.rs:383-391), metaindex, index with
+ * shortest separators, footer) in host memory. host_seal != 0 computes every trailer crc on the host
+ * (write_raw_block, table.rs:504-529); host_seal == 0 leaves the 4 crc bytes zero, to be filled on the device
+ * by one lcrc_batch_seal over lcrc_tb_seal_descs' descriptors. compression: 0 none, 1 Snappy framing. */
+void* lcrc_tb_create(uint32_t block_size, int restart_interval, uint8_t compression, int mode, uint32_t flags,
+                     int host_seal);
+void lcrc_tb_destroy(void* tb);
+int lcrc_tb_add(void* tb, const uint8_t* key, size_t klen, const uint8_t* val, size_t vlen); /* keys ascending */
+void lcrc_tb_flush(void* tb);                                                                 /* end a data block */
+int lcrc_tb_finish(void* tb, const char* filter_name, const uint8_t* filter, size_t filter_len);
+size_t lcrc_tb_size(void* tb);
+const uint8_t* lcrc_tb_data(void* tb); /* the file's bytes (lcrc_tb_size of them) */
+/* the blocks that carry a trailer, in file order (crc 0 unless sealed on the host); returns their count */
+size_t lcrc_tb_blocks(void* tb, lcrc_tblk* out, size_t cap);
+/* one lcrc_batch_seal descriptor {offset, n + 1, n + 1} per block; returns their count */
+size_t lcrc_tb_seal_descs(void* tb, lcrc_desc* out, size_t cap);
 
 /* Snappy framing, on the device: the `snap` crate's FrameDecoder as read_block_from_file uses it for
  * compressed blocks (src/sstable/format.rs:194-206; written by FrameEncoder, table.rs:481-497). Decodes the
