@@ -145,14 +145,17 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_run(dist, prepare, steps, warmup, engines=()):
+def timed_run(dist, prepare, steps, warmup, engines=(), synchronous=False):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
     `prepare(first, count)` returns the submissions for steps first .. first+count-1 as (submit, launches,
     steps) triples (argument marshalling done before the clock starts). The wall clock covers all K steps.
-    The GPU clock -- HIP events on the first engine's stream -- starts when the FIRST submission's work has
-    finished (an event enqueued behind it) and stops at the end: it measures the launches of submissions
-    2..n back to back, without the host latency before the first kernel. Returns (max-over-ranks wall
-    seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock covers)."""
+    The GPU clock -- HIP events on the first engine's stream -- covers every launch of the timed region: the
+    stream is held at a gate with the start event behind it while the first submission is enqueued, then the
+    gate opens, so the events span the kernels back to back, without the host latency before the first one
+    and without an event marker between two launches (which would hold the next launch until the previous
+    drains). A synchronous submission (it waits for its own stream) cannot be held at a gate: the events then
+    simply bracket the region. Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches
+    and steps the GPU clock covers)."""
     if warmup:
         for sub, _, _ in prepare(0, warmup):
             sub()
@@ -161,10 +164,17 @@ def timed_run(dist, prepare, steps, warmup, engines=()):
         e.sync()
     dist.barrier()
     t0 = time.perf_counter()
-    subs[0][0]()
-    timed = engines and len(subs) > 1
-    if timed:
+    timed = bool(engines)
+    gated = timed and not synchronous
+    if gated:
+        engines[0].timer_arm()
+    elif timed:
         engines[0].timer_start()
+    try:
+        subs[0][0]()
+    finally:
+        if gated:
+            engines[0].timer_go()
     for sub, _, _ in subs[1:]:
         sub()
     for e in engines:
@@ -172,8 +182,8 @@ def timed_run(dist, prepare, steps, warmup, engines=()):
     elapsed = time.perf_counter() - t0
     gpu_ms = engines[0].timer_stop() if timed else None
     dist.barrier()
-    cov_launches = sum(n for _, n, _ in subs[1:])
-    cov_steps = sum(k for _, _, k in subs[1:])
+    cov_launches = sum(n for _, n, _ in subs)
+    cov_steps = sum(k for _, _, k in subs)
     return dist.max(elapsed), elapsed, gpu_ms, cov_launches, cov_steps
 
 
@@ -609,7 +619,8 @@ def main(argv=None):
         per = w.launches(1)
         prepare = lambda f, c: [(lambda i=i: w.run(i, 1), per, 1) for i in range(f, f + c)]  # noqa: E731
     timers = w.engines if w.engines else engs
-    elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, timers)
+    elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, timers,
+                                                                      synchronous=w.per_step_sync)
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
     # this rank's fingerprint and rate, gathered over gloo (no RCCL)
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
@@ -648,11 +659,12 @@ def main(argv=None):
             "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(args.config, args.mode),
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
-            "timing": ("HIP events on the engine stream: from the end of the timed region's first submission to "
-                       "its end, / the launches in between (back to back, dispatch gaps included)" if one_stream else
-                       "HIP events on the first engine's stream from the end of the first step to the end of the "
-                       f"timed region, / steps; with {len(timers)} streams the steps overlap, so this is wall per "
-                       "step of the whole pipeline, not one kernel's duration"),
+            "timing": ("HIP events on the engine stream around every launch of the timed region (the stream held "
+                       "at a gate until the first submission is enqueued), / the launches: back to back, dispatch "
+                       "gaps included" if one_stream else
+                       "HIP events on the first engine's stream around the timed region (held at a gate until its "
+                       f"first submission is enqueued), / steps; with {len(timers)} streams the steps overlap, so "
+                       "this is wall per step of the whole pipeline, not one kernel's duration"),
             "profile": load_profile(args.config, args.mode),
         }
     else:

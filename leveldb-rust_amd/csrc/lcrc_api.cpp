@@ -131,6 +131,7 @@ struct lcrc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;
   hipEvent_t t0 = nullptr, t1 = nullptr;
+  uint32_t* gate = nullptr;  // pinned: the stream waits for it to become 1 (lcrc_timer_arm / lcrc_timer_go)
   uint32_t* d_tab = nullptr;
   uint32_t init = lcrc::CRC_INIT, xorout = lcrc::CRC_XOROUT, fin4096 = 0;
   uint32_t poly = 0, x4096 = 0;  // this mode's polynomial and x^(8*4096) mod P (k_ranges' chunk shift)
@@ -289,6 +290,9 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
     return bail(fail_hip(e, "hipHostMalloc"));
   if ((e = hipHostMalloc(&ctx->ts_host, sizeof(lcrc_tscan_dev), hipHostMallocDefault)) != hipSuccess)
     return bail(fail_hip(e, "hipHostMalloc"));
+  if ((e = hipHostMalloc((void**)&ctx->gate, 64, hipHostMallocDefault)) != hipSuccess)
+    return bail(fail_hip(e, "hipHostMalloc"));
+  *(volatile uint32_t*)ctx->gate = 0;
   if ((e = hipMalloc(&ctx->ts_count_status, 4 * sizeof(uint32_t))) != hipSuccess) return bail(fail_hip(e, "hipMalloc"));
 
   // constant tables for this mode
@@ -342,6 +346,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->ts_blocks.release();
   ctx->ts_count.release();
   if (ctx->ts_host) (void)hipHostFree(ctx->ts_host);
+  if (ctx->gate) (void)hipHostFree(ctx->gate);
   if (ctx->ts_count_status) (void)hipFree(ctx->ts_count_status);
   if (ctx->d_tab) (void)hipFree(ctx->d_tab);
   if (ctx->t0) (void)hipEventDestroy(ctx->t0);
@@ -1298,6 +1303,24 @@ int lcrc_timer_stop(lcrc_ctx* ctx, float* ms) {
   HIPCHK(hipEventRecord(ctx->t1, ctx->stream));
   HIPCHK(hipEventSynchronize(ctx->t1));
   HIPCHK(hipEventElapsedTime(ms, ctx->t0, ctx->t1));
+  *(volatile uint32_t*)ctx->gate = 0;
+  return LCRC_OK;
+}
+// The stream holds at the gate; the start event follows it, so work enqueued now starts back to back when
+// lcrc_timer_go opens the gate: the events then span the kernels alone, with no host submission latency and no
+// marker between two launches. lcrc_timer_go must follow (a held stream never drains).
+int lcrc_timer_arm(lcrc_ctx* ctx) {
+  if (!ctx) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  *(volatile uint32_t*)ctx->gate = 0;
+  HIPCHK(hipStreamWaitValue32(ctx->stream, ctx->gate, 1, hipStreamWaitValueGte, 0xFFFFFFFFu));
+  HIPCHK(hipEventRecord(ctx->t0, ctx->stream));
+  return LCRC_OK;
+}
+int lcrc_timer_go(lcrc_ctx* ctx) {
+  if (!ctx) return LCRC_EINVAL;
+  __atomic_store_n(ctx->gate, 1u, __ATOMIC_SEQ_CST);
   return LCRC_OK;
 }
 
