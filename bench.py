@@ -55,6 +55,9 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", choices=["fixed", "mixed", "wal", "table", "snappy", "seal"], default="fixed")
+    p.add_argument("--marker-timer", action="store_true",
+                   help="fixed config: time the roofline with event markers after the first submission instead of "
+                        "events carried by the launches")
     p.add_argument("--table-sync", action="store_true",
                    help="table config: time the synchronous lcrc_table_scan (results to pinned host memory)")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
@@ -145,17 +148,17 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_run(dist, prepare, steps, warmup, engines=(), synchronous=False):
+def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
     `prepare(first, count)` returns the submissions for steps first .. first+count-1 as (submit, launches,
     steps) triples (argument marshalling done before the clock starts). The wall clock covers all K steps.
-    The GPU clock -- HIP events on the first engine's stream -- covers every launch of the timed region: the
-    stream is held at a gate with the start event behind it while the first submission is enqueued, then the
-    gate opens, so the events span the kernels back to back, without the host latency before the first one
-    and without an event marker between two launches (which would hold the next launch until the previous
-    drains). A synchronous submission (it waits for its own stream) cannot be held at a gate: the events then
-    simply bracket the region. Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches
-    and steps the GPU clock covers)."""
+    The GPU clock is HIP events on the first engine's stream. kernel_events (the queued fast path): the first
+    and the last submission's launches carry the events themselves (lcrc_timer_kernels ->
+    hipExtLaunchKernelGGL), from the first launch's start to the last one's end: every launch of the timed
+    region, back to back, with no host latency and no marker packet in between. Otherwise the clock starts when
+    the first submission's work has finished (an event enqueued behind it) and covers submissions 2..n.
+    Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock
+    covers)."""
     if warmup:
         for sub, _, _ in prepare(0, warmup):
             sub()
@@ -163,27 +166,25 @@ def timed_run(dist, prepare, steps, warmup, engines=(), synchronous=False):
     for e in engines:
         e.sync()
     dist.barrier()
+    carried = bool(engines) and kernel_events
     t0 = time.perf_counter()
-    timed = bool(engines)
-    gated = timed and not synchronous
-    if gated:
-        engines[0].timer_arm()
-    elif timed:
-        engines[0].timer_start()
-    try:
-        subs[0][0]()
-    finally:
-        if gated:
-            engines[0].timer_go()
-    for sub, _, _ in subs[1:]:
+    for k, (sub, _, _) in enumerate(subs):
+        if carried and k == 0:
+            engines[0].timer_kernels(0)
+        if carried and k == len(subs) - 1:
+            engines[0].timer_kernels(1)
         sub()
+        if not carried and k == 0 and engines and len(subs) > 1:
+            engines[0].timer_start()
     for e in engines:
         e.sync()
     elapsed = time.perf_counter() - t0
+    timed = carried or (bool(engines) and len(subs) > 1)
     gpu_ms = engines[0].timer_stop() if timed else None
     dist.barrier()
-    cov_launches = sum(n for _, n, _ in subs)
-    cov_steps = sum(k for _, _, k in subs)
+    first = 0 if carried else 1
+    cov_launches = sum(n for _, n, _ in subs[first:])
+    cov_steps = sum(k for _, _, k in subs[first:])
     return dist.max(elapsed), elapsed, gpu_ms, cov_launches, cov_steps
 
 
@@ -222,12 +223,14 @@ class Workload:
     launches the dominant kernel makes for `count` steps; sample / crcs: the CPU baseline's sample and the
     device's CRCs of that sample; xor(): xor of the device CRCs of step 0 (per-rank shard fingerprint)."""
 
-    def __init__(self, run, nbytes, cfg, launches=None, sample=None, crcs=None, per_step_sync=False, engines=None):
+    def __init__(self, run, nbytes, cfg, launches=None, sample=None, crcs=None, per_step_sync=False, engines=None,
+                 kernel_events=False):
         self.run, self.nbytes, self.cfg = run, nbytes, cfg
         self.launches = launches or (lambda count: count)
         self.sample, self.crcs = sample, crcs
         self.per_step_sync = per_step_sync
         self.engines = engines  # the engines the steps run on, when not the bench's own
+        self.kernel_events = kernel_events  # the launches can carry the roofline's events (queued fast path)
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -271,7 +274,8 @@ def workload_fixed(m, synth, engs, rank, device, args):
 
     cfg = {"workload": f"{nblk // 1024}K x 4 KiB blocks, device-resident (BASELINE configs[1])", "blocks": nblk,
            "block_bytes": blen, "batches_rotated": NBUF, "layout": "back-to-back", "submission": sub}
-    return Workload(run, nblk * blen, cfg, launches, ("uniform", host[0], nblk, blen), crcs)
+    return Workload(run, nblk * blen, cfg, launches, ("uniform", host[0], nblk, blen), crcs,
+                    kernel_events=q != 1 and len(engs) == 1 and not args.marker_timer)
 
 
 def workload_fixed_host(m, synth, rank, args):
@@ -620,7 +624,7 @@ def main(argv=None):
         prepare = lambda f, c: [(lambda i=i: w.run(i, 1), per, 1) for i in range(f, f + c)]  # noqa: E731
     timers = w.engines if w.engines else engs
     elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, timers,
-                                                                      synchronous=w.per_step_sync)
+                                                                      kernel_events=w.kernel_events)
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
     # this rank's fingerprint and rate, gathered over gloo (no RCCL)
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
@@ -659,12 +663,14 @@ def main(argv=None):
             "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(args.config, args.mode),
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
-            "timing": ("HIP events on the engine stream around every launch of the timed region (the stream held "
-                       "at a gate until the first submission is enqueued), / the launches: back to back, dispatch "
-                       "gaps included" if one_stream else
-                       "HIP events on the first engine's stream around the timed region (held at a gate until its "
-                       f"first submission is enqueued), / steps; with {len(timers)} streams the steps overlap, so "
-                       "this is wall per step of the whole pipeline, not one kernel's duration"),
+            "timing": ("HIP events carried by the launches themselves (hipExtLaunchKernelGGL): first launch's "
+                       "start to last launch's end over every launch of the timed region, / the launches (back to "
+                       "back, dispatch gaps included)" if w.kernel_events else
+                       "HIP events on the engine stream: from the end of the timed region's first submission to "
+                       "its end, / the launches in between (back to back, dispatch gaps included)" if one_stream else
+                       "HIP events on the first engine's stream from the end of the first step to the end of the "
+                       f"timed region, / steps; with {len(timers)} streams the steps overlap, so this is wall per "
+                       "step of the whole pipeline, not one kernel's duration"),
             "profile": load_profile(args.config, args.mode),
         }
     else:

@@ -287,12 +287,12 @@ int lcrc_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int lcrc_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int lcrc_memset_d(void* dst, int value, size_t bytes);
 int lcrc_device_sync(void);
-/* Event timing on the context stream (milliseconds between two recorded events). lcrc_timer_arm holds the
- * stream at a gate and records the start event behind it; the work enqueued next starts when lcrc_timer_go
- * opens the gate (call it before any synchronisation). */
+/* Event timing on the context stream (milliseconds between two recorded events). Or carried by the fast-path
+ * launches themselves (lcrc_batch_uniform_queue): lcrc_timer_kernels(ctx, 0) before the first timed submission
+ * (its launch records the start), lcrc_timer_kernels(ctx, 1) before the last (its launches record the end);
+ * no marker between launches. lcrc_timer_stop ends either form. */
 int lcrc_timer_start(lcrc_ctx* ctx);
-int lcrc_timer_arm(lcrc_ctx* ctx);
-int lcrc_timer_go(lcrc_ctx* ctx);
+int lcrc_timer_kernels(lcrc_ctx* ctx, int edge);
 int lcrc_timer_stop(lcrc_ctx* ctx, float* ms);
 
 /* HIP graphs of the context's own stream: lcrc_graph_begin starts capturing the calls made on the context

@@ -92,7 +92,7 @@ ABI_SYMBOLS = [
     "lcrc_tb_create", "lcrc_tb_destroy", "lcrc_tb_add", "lcrc_tb_flush", "lcrc_tb_finish", "lcrc_tb_size",
     "lcrc_tb_data", "lcrc_tb_blocks", "lcrc_tb_seal_descs",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
-    "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_arm", "lcrc_timer_go", "lcrc_timer_stop",
+    "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_kernels", "lcrc_timer_stop",
     "lcrc_graph_begin", "lcrc_graph_end", "lcrc_graph_launch", "lcrc_graph_destroy",
     "lcrc_last_error", "lcrc_version",
 ]
@@ -154,8 +154,7 @@ def lib():
     sig("lcrc_memset_d", i32, vp, i32, sz)
     sig("lcrc_device_sync", i32)
     sig("lcrc_timer_start", i32, vp)
-    sig("lcrc_timer_arm", i32, vp)
-    sig("lcrc_timer_go", i32, vp)
+    sig("lcrc_timer_kernels", i32, vp, i32)
     sig("lcrc_timer_stop", i32, vp, ctypes.POINTER(ctypes.c_float))
     sig("lcrc_graph_begin", i32, vp)
     sig("lcrc_graph_end", i32, vp, ctypes.POINTER(vp))
@@ -561,12 +560,10 @@ class Engine:
     def timer_start(self):
         _check(lib().lcrc_timer_start(self.ctx), "lcrc_timer_start")
 
-    def timer_arm(self):
-        """Hold the stream at a gate (the start event behind it) until timer_go()."""
-        _check(lib().lcrc_timer_arm(self.ctx), "lcrc_timer_arm")
-
-    def timer_go(self):
-        _check(lib().lcrc_timer_go(self.ctx), "lcrc_timer_go")
+    def timer_kernels(self, edge):
+        """Fast-path launches carry the timer's events: edge 0 = the next launch records the start, edge 1 = the
+        launches from the next one on record the end."""
+        _check(lib().lcrc_timer_kernels(self.ctx, int(edge)), "lcrc_timer_kernels")
 
     def timer_stop(self):
         ms = ctypes.c_float(0)

@@ -29,7 +29,8 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
                               uint32_t init, uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
                               const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st);
 hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
-                                     uint32_t fin, uint32_t flags, hipStream_t st);
+                                     uint32_t fin, uint32_t flags, hipStream_t st, hipEvent_t t_start,
+                                     hipEvent_t t_stop);
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                lcrc_tscan_dev* st, hipStream_t s);
 hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
@@ -131,7 +132,7 @@ struct lcrc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;
   hipEvent_t t0 = nullptr, t1 = nullptr;
-  uint32_t* gate = nullptr;  // pinned: the stream waits for it to become 1 (lcrc_timer_arm / lcrc_timer_go)
+  bool tk_start = false, tk_stop = false, tk_any = false;  // lcrc_timer_kernels: launches that record t0 / t1
   uint32_t* d_tab = nullptr;
   uint32_t init = lcrc::CRC_INIT, xorout = lcrc::CRC_XOROUT, fin4096 = 0;
   uint32_t poly = 0, x4096 = 0;  // this mode's polynomial and x^(8*4096) mod P (k_ranges' chunk shift)
@@ -290,9 +291,6 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
     return bail(fail_hip(e, "hipHostMalloc"));
   if ((e = hipHostMalloc(&ctx->ts_host, sizeof(lcrc_tscan_dev), hipHostMallocDefault)) != hipSuccess)
     return bail(fail_hip(e, "hipHostMalloc"));
-  if ((e = hipHostMalloc((void**)&ctx->gate, 64, hipHostMallocDefault)) != hipSuccess)
-    return bail(fail_hip(e, "hipHostMalloc"));
-  *(volatile uint32_t*)ctx->gate = 0;
   if ((e = hipMalloc(&ctx->ts_count_status, 4 * sizeof(uint32_t))) != hipSuccess) return bail(fail_hip(e, "hipMalloc"));
 
   // constant tables for this mode
@@ -346,7 +344,6 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->ts_blocks.release();
   ctx->ts_count.release();
   if (ctx->ts_host) (void)hipHostFree(ctx->ts_host);
-  if (ctx->gate) (void)hipHostFree(ctx->gate);
   if (ctx->ts_count_status) (void)hipFree(ctx->ts_count_status);
   if (ctx->d_tab) (void)hipFree(ctx->d_tab);
   if (ctx->t0) (void)hipEventDestroy(ctx->t0);
@@ -501,7 +498,15 @@ int lcrc_batch_uniform_queue(lcrc_ctx* ctx, const lcrc_ujob* jobs, size_t njobs,
       q[m].nblk = j.n;
       ++m;
     }
-    if (m) HIPCHK(lcrc_launch_windows_queue(ctx->grid_a, q, m, ctx->d_tab, ctx->fin4096, ctx->flags & LCRC_FLAG_MASK, st));
+    if (m) {
+      // kernel-carried timing (lcrc_timer_kernels): the launch after edge 0 records the start event, the launches
+      // after edge 1 the stop event (the last one recorded wins)
+      hipEvent_t ts = ctx->tk_start ? ctx->t0 : nullptr, te = ctx->tk_stop ? ctx->t1 : nullptr;
+      HIPCHK(lcrc_launch_windows_queue(ctx->grid_a, q, m, ctx->d_tab, ctx->fin4096, ctx->flags & LCRC_FLAG_MASK, st,
+                                       ts, te));
+      if (ts) ctx->tk_any = true;
+      ctx->tk_start = false;
+    }
   }
   return LCRC_OK;
 }
@@ -1300,27 +1305,28 @@ int lcrc_timer_start(lcrc_ctx* ctx) {
 }
 int lcrc_timer_stop(lcrc_ctx* ctx, float* ms) {
   if (!ctx || !ms) return LCRC_EINVAL;
-  HIPCHK(hipEventRecord(ctx->t1, ctx->stream));
+  if (ctx->tk_stop) {  // kernel-carried: the events are the first and last launches' own start and end
+    const bool any = ctx->tk_any;
+    ctx->tk_start = ctx->tk_stop = ctx->tk_any = false;
+    if (!any) return LCRC_EINVAL;
+  } else {
+    HIPCHK(hipEventRecord(ctx->t1, ctx->stream));
+  }
   HIPCHK(hipEventSynchronize(ctx->t1));
   HIPCHK(hipEventElapsedTime(ms, ctx->t0, ctx->t1));
-  *(volatile uint32_t*)ctx->gate = 0;
   return LCRC_OK;
 }
-// The stream holds at the gate; the start event follows it, so work enqueued now starts back to back when
-// lcrc_timer_go opens the gate: the events then span the kernels alone, with no host submission latency and no
-// marker between two launches. lcrc_timer_go must follow (a held stream never drains).
-int lcrc_timer_arm(lcrc_ctx* ctx) {
-  if (!ctx) return LCRC_EINVAL;
-  int rc = set_device(ctx);
-  if (rc) return rc;
-  *(volatile uint32_t*)ctx->gate = 0;
-  HIPCHK(hipStreamWaitValue32(ctx->stream, ctx->gate, 1, hipStreamWaitValueGte, 0xFFFFFFFFu));
-  HIPCHK(hipEventRecord(ctx->t0, ctx->stream));
-  return LCRC_OK;
-}
-int lcrc_timer_go(lcrc_ctx* ctx) {
-  if (!ctx) return LCRC_EINVAL;
-  __atomic_store_n(ctx->gate, 1u, __ATOMIC_SEQ_CST);
+// Fast-path launches carry the timer's events themselves (hipExtLaunchKernelGGL): edge 0 -- the next launch
+// records t0 at its start; edge 1 -- the launches from the next one on record t1 at their end (the last one
+// wins). No marker packet between launches, no host latency before the first kernel. Ended by lcrc_timer_stop.
+int lcrc_timer_kernels(lcrc_ctx* ctx, int edge) {
+  if (!ctx || edge < 0 || edge > 1) return LCRC_EINVAL;
+  if (edge == 0) {
+    ctx->tk_start = true;
+    ctx->tk_any = false;
+  } else {
+    ctx->tk_stop = true;
+  }
   return LCRC_OK;
 }
 

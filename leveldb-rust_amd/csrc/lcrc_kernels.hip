@@ -20,6 +20,7 @@
 //   * k_wal_parse walks the 7-byte headers of every 32 KiB log block (src/db/log.rs:204-279) into
 //     record descriptors for k_blocks.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -2712,8 +2713,11 @@ hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, u
 
 // A queue of uniform 4 KiB batches (lcrc_batch_uniform_queue), at most MAX_QJOBS per launch: jobs[k] =
 // {base, out, expected, mismatch, nblk} (host array, copied into the kernel arguments).
+// t_start / t_stop (nullable): events recorded by the dispatch itself (hipExtLaunchKernelGGL: the kernel's own
+// start and end, no marker packet between launches)
 hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
-                                     uint32_t fin, uint32_t flags, hipStream_t st) {
+                                     uint32_t fin, uint32_t flags, hipStream_t st, hipEvent_t t_start,
+                                     hipEvent_t t_stop) {
   using lcrc_dev::QJobsArg;
   if (njobs == 0 || njobs > (uint32_t)lcrc_dev::MAX_QJOBS) return njobs ? hipErrorInvalidValue : hipSuccess;
   QJobsArg a;
@@ -2737,7 +2741,11 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
   grid *= lcrc_dev::A_WG_PER_CU;
   const uint64_t need = (reg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
   const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
-  hipLaunchKernelGGL(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, a, gtab, fin, flags);
+  if (t_start || t_stop)
+    hipExtLaunchKernelGGL(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, t_start, t_stop, 0, a, gtab,
+                          fin, flags);
+  else
+    hipLaunchKernelGGL(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, a, gtab, fin, flags);
   return hipGetLastError();
 }
 

@@ -77,7 +77,30 @@ def main(outdir, rnd, config, mode):
                                      "frac": line["roofline"]["frac"], "launch_us": line["roofline"]["launch_us"],
                                      "launches": line["roofline"].get("launches"),
                                      "streams": line["config"].get("streams")}
-            summary["agreement"] = round(summary["frac"] / line["roofline"]["frac"], 4)
+            # the bench line's quantity, recomputed from the kernel trace of the same run: its HIP events span
+            # the timed region's launches (kernel-carried events: the first one's start to the last one's end;
+            # otherwise from the end of the first launch to the end of the last), dispatch gaps included
+            nl = line["roofline"].get("launches") or 0
+            trace = find(os.path.join(outdir, "trace"), "*kernel_trace.csv")
+            if trace and nl:
+                ts = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace))
+                            if r["Kernel_Name"].split("(")[0] == dom[0])
+                kernel_events = "carried by the launches" in line["roofline"].get("timing", "")
+                timed = ts[-(nl + 1):] if len(ts) > nl else []
+                span = None
+                if kernel_events and len(ts) >= nl:  # first launch's start to the last one's end
+                    span = (ts[-1][1] - ts[-nl][0]) / 1e3 / nl
+                elif timed:
+                    span = (timed[-1][1] - timed[0][1]) / 1e3 / nl
+                if span:
+                    summary["trace_launch_us"] = round(span, 3)
+                    summary["trace_gap_us"] = round(span - summary["avg_us"], 3)
+                    summary["frac_from_trace"] = round(bpl / (span * 1e3) / 8000.0, 4)
+                    summary["agreement"] = round(summary["frac_from_trace"] / line["roofline"]["frac"], 4)
+            summary["note"] = ("frac: the dominant kernel's average duration alone (rocprofv3 kernel trace); "
+                               "frac_from_trace: the bench line's measure (its timed launches, first to last, per "
+                               "launch) on the same trace -- the difference is the dispatch "
+                               "gap between two in-order launches; agreement = frac_from_trace / line frac")
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     # the dominant kernel's traffic for bench.py
