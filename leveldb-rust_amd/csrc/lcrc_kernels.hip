@@ -140,8 +140,43 @@ __device__ __forceinline__ uint32_t zlook(const void* L, uint32_t tab_byte_off, 
 //          move is also the select (one instruction per register)
 //   bit 4: v_permlane16_swap (odd rows of a <-> even rows of b), bit 5: v_permlane32_swap (one
 //          instruction per register pair)
+// Lane bit 3 (register pairs j, j + 1): per output one v_cndmask_b32 with a DPP source (row_shr:8 / row_shl:8
+// folded into the select) writing a fresh register -- the bank-masked v_mov_b32_dpp form needs its destination to
+// hold the kept value first, i.e. a copy per pair (32 more VALU per region). VCC holds the lanes whose bit 3 is
+// clear (0x00ff00ff per half), then set. bound_ctrl: a source lane outside the row reads 0 (the write happens and
+// the select discards it).
+__device__ __forceinline__ void transpose_pair3(u32x4& a, u32x4& b) {
+  u32x4 na, nb;
+  __asm__ volatile(
+      "s_nop 1\n\t"
+      "s_mov_b32 vcc_lo, 0x00ff00ff\n\t"
+      "s_mov_b32 vcc_hi, 0x00ff00ff\n\t"
+      "v_cndmask_b32_dpp %0, %8, %12, vcc row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %1, %9, %13, vcc row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %2, %10, %14, vcc row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %3, %11, %15, vcc row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_mov_b32 vcc_lo, 0xff00ff00\n\t"
+      "s_mov_b32 vcc_hi, 0xff00ff00\n\t"
+      "v_cndmask_b32_dpp %4, %12, %8, vcc row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %5, %13, %9, vcc row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %6, %14, %10, vcc row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %7, %15, %11, vcc row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=&v"(na.x), "=&v"(na.y), "=&v"(na.z), "=&v"(na.w), "=&v"(nb.x), "=&v"(nb.y), "=&v"(nb.z), "=&v"(nb.w)
+      : "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w)
+      : "vcc");
+  a = na;
+  b = nb;
+}
+
 template <int LB, int D = 1 << (LB - 3)>  // D: the register-index bit paired with lane bit LB
 __device__ __forceinline__ void transpose_stage(u32x4 (&v)[8]) {
+#ifndef LCRC_T3_MOVDPP
+  if constexpr (LB == 3) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) transpose_pair3(v[j], v[j + 1]);
+    return;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (j & D) continue;
@@ -149,11 +184,16 @@ __device__ __forceinline__ void transpose_stage(u32x4 (&v)[8]) {
     for (int q = 0; q < 4; ++q) {
       uint32_t a = v[j][q], b = v[j + D][q];
       if constexpr (LB == 3) {
+#ifndef LCRC_T3_MOVDPP
+        static_assert(D == 1, "stage 3 pairs registers j, j + 1");
+        continue;  // the whole register pair at once below (transpose_stage3)
+#else
         // lanes 8..15 of each row (banks 2, 3) have bit 3 set
         uint32_t na = (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)b, 0x118, 0xF, 0xC, false);
         uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)a, 0x108, 0xF, 0x3, false);
         v[j][q] = na;
         v[j + D][q] = nb;
+#endif
       } else if constexpr (LB == 4) {
         auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
         v[j][q] = r[0];
