@@ -259,12 +259,25 @@ __device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t 
   for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j_off<L4>(j));
 }
 
-// Transpose + walk one half-tile already in registers, starting chain a from register value `init`:
+// Transpose + walk one half-tile already in registers, from the register value `init` of the lane's window:
 // returns walk(init, 128 B half of window l). As each register pair is consumed it is refilled from `rs`
 // (the same half of the next region), so every wave keeps between one and two half-tiles in flight.
-template <bool REFILL = true, bool L4 = false>
+//
+// The transpose stops after lane bits 3 and 4 (LCRC_T5_FULL: all three): lane l then holds the 64 B chunk
+// l >> 5 of the half of windows (l & 31) (registers 0..3) and (l & 31) + 32 (registers 4..7), contiguous, so
+// the two chains walk them unchanged; one v_permlane32_swap of the two chain values (lane bit 5) then gives
+// every lane both chunks of its own window l, joined by Z64. The init register goes the other way: the chunk-0
+// lanes (l < 32) start window l from init[l] and window l + 32 from init[l + 32], the chunk-1 lanes from 0.
+// 16 permlane32 swaps per half become two.
+#ifndef LCRC_T5_FULL
+#define LCRC_T5_JOIN 1
+#else
+#define LCRC_T5_JOIN 0
+#endif
+template <bool REFILL = true, bool L4 = false, bool INIT = true>
 __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4 (&v)[8], uint32_t init,
                                               __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+  constexpr bool JOIN = LCRC_T5_JOIN && !L4;
 #ifndef LCRC_PROBE_NOTRANSPOSE  // ablation build: walk the pieces as loaded (wrong CRCs, timing only)
   if constexpr (L4) {
     transpose_stage<4, 1>(v);
@@ -272,7 +285,7 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
   } else {
     transpose_stage<3>(v);
     transpose_stage<4>(v);
-    transpose_stage<5>(v);
+    if constexpr (!JOIN) transpose_stage<5>(v);
   }
 #endif
 #ifdef LCRC_PROBE_NOWALK  // ablation build: fold the data with xor only
@@ -291,7 +304,13 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
 #define LCRC_REFILL_DELAY 0
 #endif
   constexpr int D = LCRC_REFILL_DELAY;
-  uint32_t xa = v[0].x ^ init, xb = v[4].x;
+  uint32_t ia = INIT ? init : 0u, ib = 0u;
+  if constexpr (JOIN && INIT) {  // lanes < 32: init[l] and init[l + 32]; lanes >= 32: 0 and 0
+    const auto r = __builtin_amdgcn_permlane32_swap(init, 0u, false, false);
+    ia = r[0];
+    ib = r[1];
+  }
+  uint32_t xa = v[0].x ^ ia, xb = v[4].x ^ ib;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     xa = step4x(L, R, xa, v[j].y);
@@ -308,7 +327,12 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the refill here: hipcc would otherwise sink it past the walk
   }
-  const uint32_t res = zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two quarters
+  if constexpr (JOIN) {  // both chunks of the lane's own window: chunk 0 in xa, chunk 1 in xb
+    const auto r = __builtin_amdgcn_permlane32_swap(xa, xb, false, false);
+    xa = r[0];
+    xb = r[1];
+  }
+  const uint32_t res = zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two 64 B chunks
 #pragma unroll
   for (int j = 4 - D; j < 4; ++j) {
     if (!REFILL) break;
@@ -702,7 +726,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
     const __amdgpu_buffer_rsrc_t rsn = src.rsrc(tn, hn);
     const uint32_t ev = expect_of<FINAL>(src, t, ht, lane);
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t x = walk_half<true, KW_L4>(L, R, va, 0u, rsn, voff_a);
+    const uint32_t x = walk_half<true, KW_L4, false>(L, R, va, 0u, rsn, voff_a);
 #ifdef LCRC_PROBE_CLOCK
     if (!s_first) s_first = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -725,7 +749,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
       const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t2, h2);
       const uint32_t ev = expect_of<FINAL>(src, t, ht, lane);
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t x = walk_half<true, KW_L4>(L, R, va, 0u, rsn, voff_a);
+      const uint32_t x = walk_half<true, KW_L4, false>(L, R, va, 0u, rsn, voff_a);
       __builtin_amdgcn_sched_barrier(0);
       const uint32_t p = walk_half<true, KW_L4>(L, R, vb, x, rsn, voff_b);
       finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
@@ -736,7 +760,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
       const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t3, h3);
       const uint32_t ev = expect_of<FINAL>(src, t1, h1, lane);
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t x = walk_half<true, KW_L4>(L, R, vc, 0u, rsn, voff_a);
+      const uint32_t x = walk_half<true, KW_L4, false>(L, R, vc, 0u, rsn, voff_a);
       __builtin_amdgcn_sched_barrier(0);
       const uint32_t p = walk_half<true, KW_L4>(L, R, vd, x, rsn, voff_b);
       finish_region<FINAL, SHIFT>(L, R, SR, p, t1, h1, lane, src, fin, flags, ev);
@@ -1355,7 +1379,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
         }
       }
     }
-    const uint32_t x = walk_half<false>(L, R, va, 0u, no_rs, voff_a);
+    const uint32_t x = walk_half<false, false, false>(L, R, va, 0u, no_rs, voff_a);
     uint32_t p = walk_half<false>(L, R, vb, x, no_rs, voff_b);
     p = tree_level<0>(L, R, p, lane);
     p = tree_level<1>(L, R, p, lane);
