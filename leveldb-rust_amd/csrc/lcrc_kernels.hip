@@ -237,26 +237,84 @@ __shared__ u32x4 lcrc_probe_tile[256];
 #define LCRC_REFILL(rs, off) __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LCRC_LOAD_AUX)
 #endif
 
-// Two load layouts of a 16 KiB region (half h = bytes [128 h, 128 h + 128) of every 256 B window):
-//  L8 (k_ranges): instruction j, lane l = 8c + k reads region byte 2048 j + 256 k + 128 h + 16 c -- eight
-//      whole 128 B lines per instruction; an 8x8 transpose (lane bits 3..5 x register bits 0..2) follows.
-//  L4 (k_windows): instruction j, lane l = 16b + a reads byte 256 (a + 16 (j & 3)) + 128 h + 16 ((j & 4) | b)
-//      -- the four lanes a, a+16, a+32, a+48 read one 64 B half-line, sixteen half-lines per instruction (the
-//      same sixteen 64 B units as L8's eight lines); a 4x4 transpose (lane bits 4, 5 x register bits 0, 1: two
-//      permlane swaps per register pair, no DPP stage) leaves lane l with half h of window l, as L8 does.
-template <bool L4>
+// Load layouts of a 16 KiB region (half h = bytes [128 h, 128 h + 128) of every 256 B window). All read eight
+// whole 128 B lines (or sixteen 64 B halves) per instruction; they differ in which lane gets which 16 B piece,
+// i.e. in which transposes follow.
+//  L8 (k_ranges): instruction j, lane l = 8c + k reads region byte 2048 j + 256 k + 128 h + 16 c; a transpose
+//      over lane bits 3, 4 (register bits 0, 1) and a lane-bit-5 chunk join (walk_half) leave lane l with half h
+//      of window l.
+//  L4: instruction j, lane l = 16b + a reads byte 256 (a + 16 (j & 3)) + 128 h + 16 ((j & 4) | b) -- the four
+//      lanes a, a+16, a+32, a+48 read one 64 B half-line; a 4x4 transpose (lane bits 4, 5 x register bits 0, 1).
+//  LX (k_windows, k_windows_q): piece c = c0 + 2 c1 + 4 c2 of a line goes to lane bit 4 (c0), 5 (c1) and 3 (c2):
+//      lane l = k + 8 c2 + 16 c0 + 32 c1 reads byte 2048 pi(j) + 256 k + 128 h + 16 c, pi swapping bits 0 and 2
+//      of j. The two permlane transposes (lane bits 4, 5 x register bits 0, 1; no DPP stage) leave lane l with
+//      the contiguous 64 B chunk c2 of windows W0 and W0 + 8; a row_ror:8 chunk join gives it window
+//      w(l) = (l & 15) | ((l >> 5) & 1) << 4 | ((l >> 4) & 1) << 5: its 4 KiB block's 16 windows stay in one DPP
+//      row, block (lane >> 4) with its two bits swapped.
+constexpr int LAY_L8 = 0, LAY_L4 = 1, LAY_LX = 2;
+template <int LAY>
 __device__ __forceinline__ uint32_t lane_voff(uint32_t lane, uint32_t h) {
-  return L4 ? 256u * (lane & 15) + 16u * ((lane >> 4) & 3) + 128u * h : 256u * (lane & 7) + 16u * (lane >> 3) + 128u * h;
+  if constexpr (LAY == LAY_L4) return 256u * (lane & 15) + 16u * ((lane >> 4) & 3) + 128u * h;
+  if constexpr (LAY == LAY_LX)
+    return 256u * (lane & 7) + 16u * (((lane >> 4) & 1) | (((lane >> 5) & 1) << 1) | (((lane >> 3) & 1) << 2)) + 128u * h;
+  return 256u * (lane & 7) + 16u * (lane >> 3) + 128u * h;
 }
-template <bool L4>
+template <int LAY>
 __device__ __forceinline__ constexpr uint32_t j_off(int j) {
-  return L4 ? 4096u * (j & 3) + 16u * (j & 4) : 2048u * j;
+  return LAY == LAY_L4 ? 4096u * (j & 3) + 16u * (j & 4)
+         : LAY == LAY_LX ? 2048u * (((j & 1) << 2) | (j & 2) | ((j >> 2) & 1))
+                         : 2048u * j;
+}
+// the window a lane holds after walk_half, and the block (of the region's four) its 16-lane row finishes
+template <int LAY>
+__device__ __forceinline__ uint32_t window_of_lane(uint32_t lane) {
+  return LAY == LAY_LX ? (lane & 15) | (((lane >> 5) & 1) << 4) | (((lane >> 4) & 1) << 5) : lane;
+}
+template <int LAY>
+__device__ __forceinline__ uint32_t block_of_row(uint32_t lane) {
+  return window_of_lane<LAY>(lane) >> 4;
 }
 
-template <bool L4 = false>
+#ifndef LCRC_KW_LAYOUT
+#define LCRC_KW_LAYOUT 2
+#endif
+constexpr int KW_LAY = LCRC_KW_LAYOUT;  // k_windows' load layout (see lane_voff): 0 L8, 1 L4, 2 LX
+
+template <int LAY = LAY_L8>
 __device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j_off<L4>(j));
+  for (int j = 0; j < 8; ++j) v[j] = LCRC_REFILL(rs, voff + j_off<LAY>(j));
+}
+
+// LX chunk join over lane bit 3: lanes with bit 3 clear hold chunk 0 of their own window in xa and chunk 0 of
+// the partner's (lane ^ 8) window in xb; lanes with bit 3 set hold chunk 1 of the partner's window in xa and of
+// their own in xb. Out: c0 = own chunk 0, c1 = own chunk 1 (two v_cndmask_b32 with a row_ror:8 DPP source).
+__device__ __forceinline__ void join_lx(uint32_t xa, uint32_t xb, uint32_t& c0, uint32_t& c1) {
+  __asm__ volatile(
+      "s_nop 1\n\t"
+      "s_mov_b32 vcc_lo, 0x00ff00ff\n\t"
+      "s_mov_b32 vcc_hi, 0x00ff00ff\n\t"
+      "v_cndmask_b32_dpp %0, %3, %2, vcc row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_mov_b32 vcc_lo, 0xff00ff00\n\t"
+      "s_mov_b32 vcc_hi, 0xff00ff00\n\t"
+      "v_cndmask_b32_dpp %1, %2, %3, vcc row_ror:8 row_mask:0xf bank_mask:0xf"
+      : "=&v"(c0), "=&v"(c1)
+      : "v"(xa), "v"(xb)
+      : "vcc");
+}
+// LX init routing: lanes with bit 3 clear start their window from init and the partner's from init[lane ^ 8];
+// lanes with bit 3 set (chunk 1) start both from 0
+__device__ __forceinline__ void init_lx(uint32_t init, uint32_t& ia, uint32_t& ib) {
+  const uint32_t zero = 0;
+  __asm__ volatile(
+      "s_nop 1\n\t"
+      "s_mov_b32 vcc_lo, 0xff00ff00\n\t"
+      "s_mov_b32 vcc_hi, 0xff00ff00\n\t"
+      "v_cndmask_b32_e32 %0, %2, %3, vcc\n\t"
+      "v_cndmask_b32_dpp %1, %2, %3, vcc row_ror:8 row_mask:0xf bank_mask:0xf"
+      : "=&v"(ia), "=&v"(ib)
+      : "v"(init), "v"(zero)
+      : "vcc");
 }
 
 // Transpose + walk one half-tile already in registers, from the register value `init` of the lane's window:
@@ -274,12 +332,12 @@ __device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t 
 #else
 #define LCRC_T5_JOIN 0
 #endif
-template <bool REFILL = true, bool L4 = false, bool INIT = true>
+template <bool REFILL = true, int LAY = LAY_L8, bool INIT = true>
 __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4 (&v)[8], uint32_t init,
                                               __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
-  constexpr bool JOIN = LCRC_T5_JOIN && !L4;
+  constexpr bool JOIN = LCRC_T5_JOIN && LAY == LAY_L8;
 #ifndef LCRC_PROBE_NOTRANSPOSE  // ablation build: walk the pieces as loaded (wrong CRCs, timing only)
-  if constexpr (L4) {
+  if constexpr (LAY != LAY_L8) {  // L4, LX: lane bits 4, 5 x register bits 0, 1
     transpose_stage<4, 1>(v);
     transpose_stage<5, 2>(v);
   } else {
@@ -293,7 +351,7 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     p ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-    v[j] = LCRC_REFILL(rs, voff + j_off<L4>(j));
+    v[j] = LCRC_REFILL(rs, voff + j_off<LAY>(j));
   }
   return p;
 #else
@@ -310,6 +368,7 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     ia = r[0];
     ib = r[1];
   }
+  if constexpr (LAY == LAY_LX && INIT) init_lx(init, ia, ib);
   uint32_t xa = v[0].x ^ ia, xb = v[4].x ^ ib;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -322,8 +381,8 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     xa = step4x(L, R, xa, j < 3 ? v[j + 1].x : 0u);
     xb = step4x(L, R, xb, j < 3 ? v[5 + j].x : 0u);
     if (REFILL && j - D >= 0) {
-      v[j - D] = LCRC_REFILL(rs, voff + j_off<L4>(j - D));
-      v[4 + j - D] = LCRC_REFILL(rs, voff + j_off<L4>(4 + j - D));
+      v[j - D] = LCRC_REFILL(rs, voff + j_off<LAY>(j - D));
+      v[4 + j - D] = LCRC_REFILL(rs, voff + j_off<LAY>(4 + j - D));
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the refill here: hipcc would otherwise sink it past the walk
   }
@@ -332,12 +391,18 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     xa = r[0];
     xb = r[1];
   }
+  if constexpr (LAY == LAY_LX) {
+    uint32_t c0, c1;
+    join_lx(xa, xb, c0, c1);
+    xa = c0;
+    xb = c1;
+  }
   const uint32_t res = zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two 64 B chunks
 #pragma unroll
   for (int j = 4 - D; j < 4; ++j) {
     if (!REFILL) break;
-    v[j] = LCRC_REFILL(rs, voff + j_off<L4>(j));
-    v[4 + j] = LCRC_REFILL(rs, voff + j_off<L4>(4 + j));
+    v[j] = LCRC_REFILL(rs, voff + j_off<LAY>(j));
+    v[4 + j] = LCRC_REFILL(rs, voff + j_off<LAY>(4 + j));
   }
   return res;
 #endif
@@ -364,7 +429,7 @@ __device__ __forceinline__ void finish_region(const void* L, const Rot& R, const
                                               uint32_t h, uint32_t lane, const Src& src, uint32_t fin,
                                               uint32_t flags, uint32_t ev) {
   if (!FINAL) {
-    src.out_of(h)[t * 64 + lane] = p;
+    src.out_of(h)[t * 64 + window_of_lane<KW_LAY>(lane)] = p;
     return;
   }
   if constexpr (SHIFT) {
@@ -385,7 +450,7 @@ __device__ __forceinline__ void finish_region(const void* L, const Rot& R, const
     p = tree_level<3>(L, R, p, lane);
   }
   bool ok;
-  const uint64_t blk = src.block(t, h, lane >> 4, ok);
+  const uint64_t blk = src.block(t, h, block_of_row<KW_LAY>(lane), ok);
   if ((lane & 15) == 0 && ok) {
     uint32_t crc = p ^ fin;
     if (flags & LCRC_FLAG_MASK) crc = mask32c(crc);
@@ -618,16 +683,12 @@ __device__ __forceinline__ uint32_t expect_of(const Src& src, uint64_t t, uint32
   uint32_t ev = 0;
   if (FINAL && src.expected_of(h)) {
     bool ok;
-    const uint64_t blk = src.block(t, h, lane >> 4, ok);
+    const uint64_t blk = src.block(t, h, block_of_row<KW_LAY>(lane), ok);
     if ((lane & 15) == 0 && ok) ev = src.expected_of(h)[blk];
   }
   return ev;
 }
 
-#ifndef LCRC_KW_L4
-#define LCRC_KW_L4 0
-#endif
-constexpr bool KW_L4 = LCRC_KW_L4;  // k_windows' load layout (see lane_voff)
 
 template <bool FINAL, bool SHIFT, class Src>
 __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __restrict__ gtab, uint32_t fin,
@@ -656,7 +717,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   // 1, 2, 4, .., 128 of the global image), read with SCALAR loads -- vector-memory returns reach a CU in
   // issue order, and a table read through the vector path would wait for every HBM load issued before it.
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t voff_a = lane_voff<KW_L4>(lane, 0), voff_b = lane_voff<KW_L4>(lane, 1);
+  const uint32_t voff_a = lane_voff<KW_LAY>(lane, 0), voff_b = lane_voff<KW_LAY>(lane, 1);
   ShiftCols scols{};
   if (SHIFT) scols = load_shift_cols(gtab, lane);  // issued before the region loads: returns first
 #ifndef LCRC_DEEP
@@ -666,9 +727,9 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   {
     const __amdgpu_buffer_rsrc_t rs0 = src.rsrc(t, ht);
     __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_L4>(va, rs0, voff_a);
+    load_half<KW_LAY>(va, rs0, voff_a);
     __builtin_amdgcn_sched_barrier(0);  // issue order va, vb: the loop's vmcnt bookkeeping assumes it
-    load_half<KW_L4>(vb, rs0, voff_b);
+    load_half<KW_LAY>(vb, rs0, voff_b);
     __builtin_amdgcn_sched_barrier(0);
   }
 #else
@@ -682,13 +743,13 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
     const __amdgpu_buffer_rsrc_t rs0 = src.rsrc(t, ht);
     const __amdgpu_buffer_rsrc_t rs1 = src.rsrc(t1, h1);
     __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_L4>(va, rs0, voff_a);
+    load_half<KW_LAY>(va, rs0, voff_a);
     __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_L4>(vb, rs0, voff_b);
+    load_half<KW_LAY>(vb, rs0, voff_b);
     __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_L4>(vc, rs1, voff_a);
+    load_half<KW_LAY>(vc, rs1, voff_a);
     __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_L4>(vd, rs1, voff_b);
+    load_half<KW_LAY>(vd, rs1, voff_b);
     __builtin_amdgcn_sched_barrier(0);
   }
 #endif
@@ -726,13 +787,13 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
     const __amdgpu_buffer_rsrc_t rsn = src.rsrc(tn, hn);
     const uint32_t ev = expect_of<FINAL>(src, t, ht, lane);
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t x = walk_half<true, KW_L4, false>(L, R, va, 0u, rsn, voff_a);
+    const uint32_t x = walk_half<true, KW_LAY, false>(L, R, va, 0u, rsn, voff_a);
 #ifdef LCRC_PROBE_CLOCK
     if (!s_first) s_first = __builtin_amdgcn_s_memrealtime();
 #endif
     __builtin_amdgcn_sched_barrier(0);
     const uint64_t tnn = take_region(&wg_ticket, share, lane);
-    const uint32_t p = walk_half<true, KW_L4>(L, R, vb, x, rsn, voff_b);
+    const uint32_t p = walk_half<true, KW_LAY>(L, R, vb, x, rsn, voff_b);
     finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
     t = tn;
     ht = hn;
@@ -749,9 +810,9 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
       const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t2, h2);
       const uint32_t ev = expect_of<FINAL>(src, t, ht, lane);
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t x = walk_half<true, KW_L4, false>(L, R, va, 0u, rsn, voff_a);
+      const uint32_t x = walk_half<true, KW_LAY, false>(L, R, va, 0u, rsn, voff_a);
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t p = walk_half<true, KW_L4>(L, R, vb, x, rsn, voff_b);
+      const uint32_t p = walk_half<true, KW_LAY>(L, R, vb, x, rsn, voff_b);
       finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
     }
     const uint64_t t3 = take_region(&wg_ticket, share, lane);
@@ -760,9 +821,9 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
       const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t3, h3);
       const uint32_t ev = expect_of<FINAL>(src, t1, h1, lane);
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t x = walk_half<true, KW_L4, false>(L, R, vc, 0u, rsn, voff_a);
+      const uint32_t x = walk_half<true, KW_LAY, false>(L, R, vc, 0u, rsn, voff_a);
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t p = walk_half<true, KW_L4>(L, R, vd, x, rsn, voff_b);
+      const uint32_t p = walk_half<true, KW_LAY>(L, R, vd, x, rsn, voff_b);
       finish_region<FINAL, SHIFT>(L, R, SR, p, t1, h1, lane, src, fin, flags, ev);
     }
     t = t2;
