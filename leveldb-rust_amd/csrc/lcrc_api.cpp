@@ -45,6 +45,7 @@ hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t*
                                  hipStream_t s);
 hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, uint32_t* status_out,
                                hipStream_t s);
+int lcrc_blocks_per_cu();
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* win, const uint32_t* gtab, uint32_t init,
@@ -188,6 +189,10 @@ int upload_tables(int mode, uint32_t** d_tab) {
   for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 256ull << m, tab.data() + TAB_ZWIN + m * 1024);
   lcrc::make_shift_tables(poly, 4096, tab.data() + TAB_Z4096);
   lcrc::make_shift_tables(poly, LCRC_TS_PIECE, tab.data() + TAB_Z64K);
+  {
+    const uint64_t kb4[12] = {16, 32, 48, 64, 128, 192, 256, 512, 768, 1024, 2048, 3072};
+    for (int t = 0; t < 12; ++t) lcrc::make_shift_tables(poly, kb4[t], tab.data() + TAB_KB4 + t * 1024);
+  }
   // k_windows builds its LDS image from columns (entries 1, 2, 4, .., 128) of the byte tables it uses
   for (int t = 0; t < 20; ++t) {
     const uint32_t src = t < 4 ? TAB_SLICE + t * 256                    // S0: T_p
@@ -276,7 +281,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   // next batch's k_windows workgroups (76 KiB) fit beside them (config 3 on two streams: 4,198 GiB/s against
   // 3,681 with 4 per CU, at +4 % per launch alone); the WAL scan, whose k_blocks follows its own window
   // pass, uses all 4.
-  ctx->grid_b = prop.multiProcessorCount * 4;
+  ctx->grid_b = prop.multiProcessorCount * lcrc_blocks_per_cu();  // k_blocks: every resident workgroup
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return bail(fail_hip(e, "hipStreamCreate"));
   if ((e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking)) != hipSuccess)
@@ -393,11 +398,11 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
                                st));
     win = ctx->win.p;
   }
-#ifndef LCRC_BATCH_GRID_DIV
-#define LCRC_BATCH_GRID_DIV 2  // half the grid: a full one cuts config 3 k_blocks alone 22.0 -> 18.0 us but
-                               // crowds a concurrent batch on another stream (2-stream wall 4.1-4.3K -> 3.8K GiB/s)
+#ifndef LCRC_BATCH_WG_PER_CU
+#define LCRC_BATCH_WG_PER_CU 2  // 16 waves per CU: a full 32-wave grid cut config 3 k_blocks alone 22.0 -> 18.0 us but
+                                // crowded a concurrent batch on another stream (2-stream wall 4.1-4.3K -> 3.8K GiB/s)
 #endif
-  HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_BATCH_GRID_DIV, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
+  HIPCHK(lcrc_launch_blocks(false, std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU), base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
                             ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK, out_crc,
                             out_mismatch, nullptr, nullptr, st));
   return LCRC_OK;

@@ -891,7 +891,18 @@ __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, co
 // used, and 512-thread workgroups (4 per CU by LDS) keep 32 waves per CU in flight.
 // ---------------------------------------------------------------------------------------------------
 constexpr int B_THREADS = 512;
+// k_blocks' LDS image (40 KiB): slice tables T0..T3, the binary row-tree shifts Z16..Z128 and Z256..Z2048, Z4096.
+// LCRC_KB_TREE4 (measured slower, kept for reference): a 56 KiB image with 4-way two-level row trees -- lane g
+// shifted by Z_{16 (3 - g % 4)}, four lanes xored by DPP, lane 4 k shifted by Z_{64 (3 - k)}, four xored: 8
+// lookups instead of 16, but config 3 3,957 vs 4,640 GiB/s, WAL 2,600 vs 3,148 (lane-dependent table bases
+// conflict in the banks, and only two workgroups fit a CU).
+#ifdef LCRC_KB_TREE4
+constexpr int KL_Z4096 = 1024, KL_PA = 2048, KL_PB = 5120, KL_WA = 8192, KL_WB = 11264;
+constexpr int B_LDS_DWORDS = 14336;
+#else
+constexpr int KL_Z4096 = TAB_Z4096;
 constexpr int B_LDS_DWORDS = TAB_COLS;  // slice and shift tables (not the column block)
+#endif
 constexpr int B_BATCH = 8;  // window values per lane loaded ahead of the fold
 
 #ifdef LCRC_PROBE_BLOCKS_NOCONFLICT  // ablation build: every k_blocks lookup reads entry r & 0x3 (wrong CRCs)
@@ -968,6 +979,20 @@ __device__ __forceinline__ uint32_t row_bcast0(uint32_t v, uint32_t lane) {
   return lane < 32 ? (lane < 16 ? r0 : r1) : (lane < 48 ? r2 : r3);
 }
 
+#ifdef LCRC_KB_TREE4
+// Σ_g Z_{u (15 - g)}(v_g) over a 16-lane row into lane 0 (u = 16 for pieces, 256 for windows): tables at tA
+// (Z_u, Z_2u, Z_3u) and tB (Z_4u, Z_8u, Z_12u)
+__device__ __forceinline__ uint32_t row_join4(const uint32_t* L, uint32_t v, uint32_t g, int tA, int tB) {
+  if ((g & 3) != 3) v = zl(L, tA + (int)(2 - (g & 3)) * 1024, v);
+  v ^= row_down(v, 0);
+  v ^= row_down(v, 1);  // lane 4 k: the four shifted values of its group
+  if ((g & 3) == 0 && (g >> 2) != 3) v = zl(L, tB + (int)(2 - (g >> 2)) * 1024, v);
+  v ^= row_down(v, 2);
+  v ^= row_down(v, 3);  // lane 0: all sixteen
+  return v;
+}
+#endif
+
 // walk(R0, base[a, e)) from the row's loaded pieces, returned to every lane of the row; a == e -> R0.
 // Must be called by all 64 lanes (contains cross-lane ops).
 __device__ uint32_t row_walk(const uint32_t* L, const RowPiece& p, bool empty_range, uint32_t R0, uint32_t g,
@@ -993,12 +1018,16 @@ __device__ uint32_t row_walk(const uint32_t* L, const RowPiece& p, bool empty_ra
   cv = step4(L, cv, wq[1]);
   cv = step4(L, cv, wq[2]);
   cv = step4(L, cv, wq[3]) ^ rh;
+#ifdef LCRC_KB_TREE4
+  cv = row_join4(L, cv, g, KL_PA, KL_PB);
+#else
   // row tree: level m joins lane g with g + 2^m, shifting the left part by 16*2^m bytes
 #pragma unroll
   for (int m = 0; m < 4; ++m) {  // only the combining lanes look up (exec-masked: fewer bank conflicts)
     const uint32_t pn = row_down(cv, m);
     if ((g & ((2u << m) - 1)) == 0) cv = zl(L, TAB_ZPIECE + m * 1024, cv) ^ pn;
   }
+#endif
   const uint32_t res = row_bcast0(cv, lane);
   return empty_range ? R0 : res;
 }
@@ -1059,8 +1088,16 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
   int32_t xrel_nx;
   bool oob_nx;
   load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx, oob_nx);
+#ifdef LCRC_KB_TREE4
+  for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS) {
+    const uint32_t w = 4 * i;  // slice | Z4096 | the 4-way tree shifts
+    const uint32_t src = w < 1024 ? TAB_SLICE + w : w < 2048 ? TAB_Z4096 + (w - 1024) : TAB_KB4 + (w - 2048);
+    ((u32x4*)L)[i] = *(const u32x4*)(gtab + src);
+  }
+#else
   for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS)
     ((u32x4*)L)[i] = ((const u32x4*)gtab)[i];
+#endif
   __syncthreads();
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long b_tab = __builtin_amdgcn_s_memrealtime();
@@ -1123,14 +1160,18 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
         for (int j = 0; j < B_BATCH; ++j) {
           const uint32_t q = q0 + j;
-          if (q < rounds) a = zl(L, TAB_Z4096, a) ^ (16u * q + g == npad ? head : vals[j]);
+          if (q < rounds) a = zl(L, KL_Z4096, a) ^ (16u * q + g == npad ? head : vals[j]);
         }
       }
+#ifdef LCRC_KB_TREE4
+      a = row_join4(L, a, g, KL_WA, KL_WB);
+#else
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const uint32_t pn = row_down(a, m);
         if ((g & ((2u << m) - 1)) == 0) a = zl(L, TAB_ZWIN + m * 1024, a) ^ pn;
       }
+#endif
       const uint32_t mid = row_bcast0(a, lane);
       acc = single ? head : mid;
       // tail: the partial last window, walked from the folded value
@@ -2910,6 +2951,12 @@ hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t
                                hipStream_t s) {
   hipLaunchKernelGGL(lcrc_dev::k_ts_final, dim3(1), dim3(64), 0, s, st, blk, n_out, status_out);
   return hipGetLastError();
+}
+
+// k_blocks workgroups resident per CU (by its LDS image)
+int lcrc_blocks_per_cu() {
+  const int by_lds = 163840 / (lcrc_dev::B_LDS_DWORDS * 4);
+  return by_lds < 4 ? by_lds : 4;
 }
 
 // n_dev (device, nullable): the actual count when it is only known on the device; n is then a bound
