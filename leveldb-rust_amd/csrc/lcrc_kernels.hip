@@ -1087,16 +1087,30 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
   uint32_t len_nx;
   int32_t xrel_nx;
   bool oob_nx;
-  load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx, oob_nx);
 #ifdef LCRC_KB_TREE4
+  load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx, oob_nx);
   for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS) {
     const uint32_t w = 4 * i;  // slice | Z4096 | the 4-way tree shifts
     const uint32_t src = w < 1024 ? TAB_SLICE + w : w < 2048 ? TAB_Z4096 + (w - 1024) : TAB_KB4 + (w - 2048);
     ((u32x4*)L)[i] = *(const u32x4*)(gtab + src);
   }
 #else
-  for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS)
-    ((u32x4*)L)[i] = ((const u32x4*)gtab)[i];
+  {
+    // every load first, then every store: one L2 round trip for the image instead of one per 8 KiB
+    constexpr int PER = (B_LDS_DWORDS / 4 + B_THREADS - 1) / B_THREADS;
+    u32x4 t[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = threadIdx.x + k * B_THREADS;
+      if (i < B_LDS_DWORDS / 4) t[k] = ((const u32x4*)gtab)[i];
+    }
+    load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx, oob_nx);  // the first descriptor in the same round trip
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = threadIdx.x + k * B_THREADS;
+      if (i < B_LDS_DWORDS / 4) ((u32x4*)L)[i] = t[k];
+    }
+  }
 #endif
   __syncthreads();
 #ifdef LCRC_PROBE_CLOCK
