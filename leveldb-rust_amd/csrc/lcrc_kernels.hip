@@ -24,8 +24,6 @@
 #include <stdint.h>
 #include <string.h>
 
-#include <atomic>
-
 #include "lcrc_device.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -503,25 +501,6 @@ __device__ __forceinline__ uint64_t take_region(uint32_t* lctr, const Share& sh,
   return sh.region(v);
 }
 
-#ifdef LCRC_TAIL_POOL
-// Tail pool (experiment): the last `npool` regions of a queued launch are not dealt to workgroups but claimed
-// one at a time from a device counter once a wave's workgroup share is done, so CUs that stream faster take
-// more of the tail. pool[0] = claims, pool[1] = waves done; the last wave out resets both.
-__device__ uint32_t lcrc_qpool[2 * 32];
-template <class Src>
-__device__ __forceinline__ uint64_t take_region_tail(uint32_t* lctr, const Share& sh, uint32_t lane, const Src& src) {
-  const uint64_t r = take_region(lctr, sh, lane);
-  if (r != NO_REGION || !src.pool) return r;
-  uint32_t v = 0;
-  if (lane == 0) v = atomicAdd(src.pool, 1u);
-  v = __builtin_amdgcn_readfirstlane(v);
-  return v < src.npool ? src.nreg - src.npool + v : NO_REGION;
-}
-#define TAKE_REGION(c, sh, lane) take_region_tail(c, sh, lane, src)
-#else
-#define TAKE_REGION(c, sh, lane) take_region(c, sh, lane)
-#endif
-
 // Entry e of a linear byte table from its 8 columns c[i] = table[1 << i] (wave-uniform): xor of the
 // columns of the set bits of e.
 __device__ __forceinline__ uint32_t lin8(const uint32_t* __restrict__ col, uint32_t e) {
@@ -634,10 +613,6 @@ struct WinOne {
   uint64_t nblk;
   const uint32_t* expected;
   uint32_t* mismatch;
-#ifdef LCRC_TAIL_POOL
-  static constexpr uint32_t* pool = nullptr;
-  static constexpr uint32_t npool = 0;
-#endif
   __device__ __forceinline__ uint64_t regions() const { return nreg; }
   __device__ __forceinline__ uint32_t find(uint64_t, uint32_t) const { return 0; }
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(uint64_t t, uint32_t) const {
@@ -667,20 +642,12 @@ struct QJobsArg {
   QJobDev j[MAX_QJOBS];
   uint64_t nreg;
   uint32_t n;
-#ifdef LCRC_TAIL_POOL
-  uint32_t npool;
-  uint32_t* pool;
-#endif
 };
 
 struct WinQueue {
   const QJobDev* J;
   uint32_t nj;
   uint64_t nreg;
-#ifdef LCRC_TAIL_POOL
-  uint32_t* pool;
-  uint32_t npool;
-#endif
   __device__ __forceinline__ uint64_t regions() const { return nreg; }
   __device__ __forceinline__ uint32_t find(uint64_t t, uint32_t from) const {
     uint32_t j = from;
@@ -730,11 +697,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   const uint32_t lane = __lane_id();
   const uint32_t tid = threadIdx.x;
   const uint64_t nreg = src.regions();
-#ifdef LCRC_TAIL_POOL
-  const Share share = make_share(nreg - src.npool);  // this workgroup's regions
-#else
   const Share share = make_share(nreg);  // this workgroup's regions
-#endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long s_first = 0;
@@ -813,7 +776,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
 #endif
 
 #ifndef LCRC_DEEP
-  uint64_t tn = TAKE_REGION(&wg_ticket, share, lane);
+  uint64_t tn = take_region(&wg_ticket, share, lane);
   uint32_t hn = src.find(tn, ht);
   // tn = the region the refills load (ticket taken after the prologue or in the previous iteration);
   // the ticket for the one after is taken between the two walks.
@@ -829,7 +792,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
     if (!s_first) s_first = __builtin_amdgcn_s_memrealtime();
 #endif
     __builtin_amdgcn_sched_barrier(0);
-    const uint64_t tnn = TAKE_REGION(&wg_ticket, share, lane);
+    const uint64_t tnn = take_region(&wg_ticket, share, lane);
     const uint32_t p = walk_half<true, KW_LAY>(L, R, vb, x, rsn, voff_b);
     finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
     t = tn;
@@ -840,7 +803,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
 #else
   // va/vb: region t, vc/vd: region t1; walking a half refills it with the same half of the region two
   // ahead (t2 for va/vb, t3 for vc/vd): a refill has three half-walks to arrive instead of one
-  uint64_t t2 = TAKE_REGION(&wg_ticket, share, lane);
+  uint64_t t2 = take_region(&wg_ticket, share, lane);
   uint32_t h2 = src.find(t2, h1);
   while (t != NO_REGION) {
     {
@@ -852,7 +815,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
       const uint32_t p = walk_half<true, KW_LAY>(L, R, vb, x, rsn, voff_b);
       finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
     }
-    const uint64_t t3 = TAKE_REGION(&wg_ticket, share, lane);
+    const uint64_t t3 = take_region(&wg_ticket, share, lane);
     const uint32_t h3 = src.find(t3, h2);
     if (t1 != NO_REGION) {
       const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t3, h3);
@@ -867,17 +830,8 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
     ht = h2;
     t1 = t3;
     h1 = h3;
-    t2 = TAKE_REGION(&wg_ticket, share, lane);
+    t2 = take_region(&wg_ticket, share, lane);
     h2 = src.find(t2, h3);
-  }
-#endif
-#ifdef LCRC_TAIL_POOL
-  if (src.pool && lane == 0) {
-    const uint32_t d = atomicAdd(src.pool + 1, 1u);
-    if (d == gridDim.x * (A_THREADS / 64) - 1) {
-      atomicExch(src.pool, 0u);
-      atomicExch(src.pool + 1, 0u);
-    }
   }
 #endif
 #ifdef LCRC_PROBE_CLOCK
@@ -919,11 +873,7 @@ __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, co
 #ifndef LCRC_Q_TREE
   __shared__ __attribute__((aligned(16))) uint32_t L[AQ_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
-#ifdef LCRC_TAIL_POOL
-  WinQueue src{jobs.j, jobs.n, jobs.nreg, jobs.pool, jobs.npool};
-#else
   WinQueue src{jobs.j, jobs.n, jobs.nreg};
-#endif
   windows_body<true, true>(src, gtab, fin, flags, L, &wg_ticket);
 #else  // ablation: the block tree of the single-batch kernel
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
@@ -2971,15 +2921,6 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
   grid *= lcrc_dev::A_WG_PER_CU;
   const uint64_t need = (reg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
   const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
-#ifdef LCRC_TAIL_POOL
-  if (reg >= (uint64_t)g * 32 && reg > (uint64_t)LCRC_TAIL_POOL * 4) {
-    static std::atomic<uint32_t> slot{0};
-    uint32_t* pool = nullptr;
-    if (hipGetSymbolAddress((void**)&pool, HIP_SYMBOL(lcrc_dev::lcrc_qpool)) != hipSuccess) return hipErrorInvalidValue;
-    a.pool = pool + 2 * (slot.fetch_add(1) % 32);
-    a.npool = LCRC_TAIL_POOL;
-  }
-#endif
   if (t_start || t_stop)
     hipExtLaunchKernelGGL(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, t_start, t_stop, 0, a, gtab,
                           fin, flags);
