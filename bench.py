@@ -159,14 +159,21 @@ def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
     the first submission's work has finished (an event enqueued behind it) and covers submissions 2..n.
     Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock
     covers)."""
+    carried = bool(engines) and kernel_events
     if warmup:
-        for sub, _, _ in prepare(0, warmup):
+        wsubs = prepare(0, warmup)
+        for k, (sub, _, _) in enumerate(wsubs):
+            if carried and k == 0:  # the warmup goes through the timed region's launch path, events included
+                engines[0].timer_kernels(0)
+            if carried and k == len(wsubs) - 1:
+                engines[0].timer_kernels(1)
             sub()
+        if carried:
+            engines[0].timer_stop()
     subs = prepare(warmup, steps)
     for e in engines:
         e.sync()
     dist.barrier()
-    carried = bool(engines) and kernel_events
     t0 = time.perf_counter()
     for k, (sub, _, _) in enumerate(subs):
         if carried and k == 0:

@@ -488,11 +488,14 @@ int lcrc_batch_uniform_queue(lcrc_ctx* ctx, const lcrc_ujob* jobs, size_t njobs,
         return rc;
     return LCRC_OK;
   }
-  lcrc_qjob_host q[32];
+#ifndef LCRC_MAX_QJOBS
+#define LCRC_MAX_QJOBS 32
+#endif
+  lcrc_qjob_host q[LCRC_MAX_QJOBS];
   size_t k = 0;
   while (k < njobs) {
     uint32_t m = 0;
-    for (; k < njobs && m < 32; ++k) {
+    for (; k < njobs && m < LCRC_MAX_QJOBS; ++k) {
       const lcrc_ujob& j = jobs[k];
       if (j.out_mismatch && j.n) HIPCHK(hipMemsetAsync(j.out_mismatch, 0, ((j.n + 31) / 32) * sizeof(uint32_t), st));
       if (j.n == 0) continue;

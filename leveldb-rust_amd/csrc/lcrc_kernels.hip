@@ -632,7 +632,10 @@ struct WinOne {
   __device__ __forceinline__ uint32_t* mismatch_of(uint32_t) const { return mismatch; }
 };
 
-constexpr int MAX_QJOBS = 32;  // batches per queued launch (kernel-argument space: 32 x 48 B)
+#ifndef LCRC_MAX_QJOBS
+#define LCRC_MAX_QJOBS 32
+#endif
+constexpr int MAX_QJOBS = LCRC_MAX_QJOBS;  // batches per queued launch (kernel-argument space: 32 x 48 B)
 struct QJobDev {
   const uint8_t* base;
   uint32_t* out;

@@ -30,9 +30,9 @@ m.lib().lcrc_probe_stamps(st)
 full = np.frombuffer(st, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
 ok = full[:, 0] != 0
 t0 = full[ok, 0].min()
-rr = (full[:, :4] - t0) / 100.0  # 100 MHz ticks -> us: entry, tables, first half, end
+rr = (full[:, :6] - t0) / 100.0  # 100 MHz ticks -> us: entry, tables, first half, end, loads issued, built
 print(f"Q {Q}: event {ms * 1000:.1f} us, waves {ok.sum()}")
-for k, name in ((0, "entry"), (1, "tables"), (3, "end")):
+for k, name in ((0, "entry"), (4, "issued"), (5, "built"), (1, "tables"), (2, "first"), (3, "end")):
     print(f"  {name:7s}", np.percentile(rr[ok, k], [0, 10, 50, 90, 100]).round(2))
 ids = full[:, 6:8]
 xcc = ids[:, 1] & 0xF
