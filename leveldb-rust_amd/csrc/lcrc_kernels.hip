@@ -473,10 +473,13 @@ __device__ __forceinline__ void finish_region(const void* L, const Rot& R, const
 // one device counter) took 269 us instead of 205: same-address device atomics serialise.
 constexpr uint64_t NO_REGION = ~0ull;
 
-// A workgroup's share: regions lo + v * step for tickets v < count.
+// A workgroup's share: regions lo + v * step below `end` (tickets v).
 struct Share {
-  uint64_t lo, step, count;
-  __device__ __forceinline__ uint64_t region(uint64_t v) const { return v < count ? lo + v * step : NO_REGION; }
+  uint64_t lo, step, end;
+  __device__ __forceinline__ uint64_t region(uint64_t v) const {
+    const uint64_t r = lo + v * step;
+    return r < end ? r : NO_REGION;
+  }
 };
 
 __device__ __forceinline__ Share make_share(uint64_t nreg) {
@@ -484,15 +487,15 @@ __device__ __forceinline__ Share make_share(uint64_t nreg) {
 #ifndef LCRC_REGION_CONTIG
   // regions dealt round-robin over the workgroups: at any moment the whole chip streams one contiguous
   // stretch of the buffer (memory skeleton: 39.9 us per 256 MiB against 41.4-42.0 with a contiguous
-  // range per workgroup, tools/probe/probe_skel.hip)
+  // range per workgroup, tools/probe/probe_skel.hip). No ticket count: a 64-bit division in the prologue.
   sh.lo = blockIdx.x;
   sh.step = gridDim.x;
-  sh.count = nreg > sh.lo ? (nreg - sh.lo + gridDim.x - 1) / gridDim.x : 0;
+  sh.end = nreg;
 #else
   const uint64_t per = (nreg + gridDim.x - 1) / gridDim.x;
   sh.lo = (uint64_t)blockIdx.x * per;
   sh.step = 1;
-  sh.count = sh.lo < nreg ? (nreg - sh.lo < per ? nreg - sh.lo : per) : 0;
+  sh.end = sh.lo + per < nreg ? sh.lo + per : nreg;
 #endif
   return sh;
 }
@@ -540,13 +543,13 @@ __device__ __forceinline__ ShiftCols load_shift_cols(const uint32_t* __restrict_
 __device__ __forceinline__ void build_shift_tables(uint32_t* L, const ShiftCols& sc, uint32_t wv, uint32_t lane) {
   constexpr int WAVES = A_THREADS / 64;
   constexpr int PER = 256 / WAVES;
-  static_assert(PER == 32, "rows per wave");
+  static_assert(PER >= 2 && (PER & (PER - 1)) == 0, "rows per wave");
   const uint32_t col[8] = {sc.lo.x, sc.lo.y, sc.lo.z, sc.lo.w, sc.hi.x, sc.hi.y, sc.hi.z, sc.hi.w};
-  const uint32_t n0 = wv * PER;  // uniform; gray(n0) = its bits 4..7
+  const uint32_t n0 = wv * PER;  // uniform
   const uint32_t g0 = n0 ^ (n0 >> 1);
   uint32_t v = 0;
 #pragma unroll
-  for (int i = 4; i < 8; ++i)
+  for (int i = 0; i < 8; ++i)
     if ((g0 >> i) & 1) v ^= col[i];
   L[A_SHIFT / 4 + g0 * 64 + lane] = v;
 #pragma unroll
@@ -573,9 +576,30 @@ __device__ __forceinline__ Rot make_shift_rot(uint32_t lane) {
 // k_windows' LDS image built from the column block TAB_COLS. 80 wave passes of 64 entries each, one
 // byte table per pass (uniform columns -> scalar loads): passes 0..31 the replicated sets (set s,
 // position p), passes 32..79 the tree's Z256/Z512/Z1024 (same word order as the global TAB_ZWIN).
+// Without the tree (queued kernel) a wave makes 4 passes; their 32 columns can be loaded (SliceCols) before the
+// region loads are issued, so the build waits on no scalar load of its own.
+constexpr int SLICE_PASSES = 32 / (A_THREADS / 64);
+struct SliceCols {
+  uint32_t c[SLICE_PASSES][8];
+};
+__device__ __forceinline__ SliceCols load_slice_cols(const uint32_t* __restrict__ gtab, uint32_t wv) {
+  SliceCols sc;
+#pragma unroll
+  for (int k = 0; k < SLICE_PASSES; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sc.c[k][i] = gtab[TAB_COLS + ((wv + (A_THREADS / 64) * k) >> 2) * 8 + i];
+  return sc;
+}
+__device__ __forceinline__ uint32_t lin8v(const uint32_t (&c)[8], uint32_t e) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v ^= c[i] & (0u - ((e >> i) & 1u));
+  return v;
+}
+
 template <bool TREE = true>
 __device__ __forceinline__ void build_tables(uint32_t* L, const uint32_t* __restrict__ gtab, uint32_t wv,
-                                             uint32_t lane) {
+                                             uint32_t lane, const SliceCols* pre = nullptr) {
   constexpr int WAVES = A_THREADS / 64;
   static_assert(80 % WAVES == 0, "passes per wave");
 #pragma unroll
@@ -585,7 +609,8 @@ __device__ __forceinline__ void build_tables(uint32_t* L, const uint32_t* __rest
     if (P < 32) {
       const uint32_t set = P >> 4, p = (P >> 2) & 3;
       // S0: T_p | S1: Z64[3 - p]
-      const uint32_t v = lin8(gtab + TAB_COLS + (P >> 2) * 8, e);
+      const uint32_t v = (!TREE && pre) ? lin8v(pre->c[k < SLICE_PASSES ? k : 0], e)
+                                        : lin8(gtab + TAB_COLS + (P >> 2) * 8, e);
       u32x4* dst = (u32x4*)((char*)L + e * 256 + set * 128 + p * 32);
       dst[0] = u32x4{v, v, v, v};
       dst[1] = u32x4{v, v, v, v};
@@ -621,6 +646,10 @@ struct WinOne {
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(uint64_t t, uint32_t) const {
     return region_rsrc(base, span, t, nreg);
   }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t first(uint64_t t, uint32_t& h) const {
+    h = 0;
+    return rsrc(t, 0);
+  }
   // block q of region t: (output slot, valid)
   __device__ __forceinline__ uint64_t block(uint64_t t, uint32_t, uint32_t q, bool& ok) const {
     const uint64_t b = t * 4 + q;
@@ -654,6 +683,8 @@ struct WinQueue {
   const QJobDev* J;
   uint32_t nj;
   uint64_t nreg;
+  const uint8_t* b0;  // job 0's base and blocks, job 1's first region (first())
+  uint64_t n0, r1;
   __device__ __forceinline__ uint64_t regions() const { return nreg; }
   __device__ __forceinline__ uint32_t find(uint64_t t, uint32_t from) const {
     uint32_t j = from;
@@ -671,6 +702,18 @@ struct WinQueue {
       nrec = rem < (uint64_t)REGION ? (uint32_t)rem : (uint32_t)REGION;
     }
     return __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, (int)nrec, 0x00020000);
+  }
+  // a wave's first region: in the common case (job 0) from kernel-argument loads that do not wait on each other
+  // (find + rsrc are a chain of four dependent scalar round trips)
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t first(uint64_t t, uint32_t& h) const {
+    if (t < nreg && (nj == 1 || t < r1)) {
+      h = 0;
+      const uint64_t rem = n0 * 4096 - t * (uint64_t)REGION;
+      const uint32_t nrec = rem < (uint64_t)REGION ? (uint32_t)rem : (uint32_t)REGION;
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(b0 + t * (uint64_t)REGION), (short)0, (int)nrec, 0x00020000);
+    }
+    h = find(t, 0);
+    return rsrc(t, h);
   }
   __device__ __forceinline__ uint64_t block(uint64_t t, uint32_t j, uint32_t q, bool& ok) const {
     const uint64_t b = (t - J[j].reg0) * 4 + q;
@@ -726,12 +769,14 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   const uint32_t voff_a = lane_voff<KW_LAY>(lane, 0), voff_b = lane_voff<KW_LAY>(lane, 1);
   ShiftCols scols{};
   if (SHIFT) scols = load_shift_cols(gtab, lane);  // issued before the region loads: returns first
+  SliceCols slc;
+  if (SHIFT) slc = load_slice_cols(gtab, wv);  // scalar: the build then waits on nothing but these
 #ifndef LCRC_DEEP
   uint64_t t = share.region(wv);
-  uint32_t ht = src.find(t, 0);
+  uint32_t ht;
   u32x4 va[8], vb[8];
   {
-    const __amdgpu_buffer_rsrc_t rs0 = src.rsrc(t, ht);
+    const __amdgpu_buffer_rsrc_t rs0 = src.first(t, ht);
     __builtin_amdgcn_sched_barrier(0);
     load_half<KW_LAY>(va, rs0, voff_a);
     __builtin_amdgcn_sched_barrier(0);  // issue order va, vb: the loop's vmcnt bookkeeping assumes it
@@ -763,7 +808,7 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
 #endif
 #ifndef LCRC_PROBE_NOTABLES  // ablation build: no LDS image (wrong CRCs, timing only)
-  build_tables<!SHIFT>(L, gtab, wv, lane);
+  build_tables<!SHIFT>(L, gtab, wv, lane, SHIFT ? &slc : nullptr);
   if (SHIFT) build_shift_tables(L, scols, wv, lane);
 #endif
 #ifdef LCRC_PROBE_CLOCK
@@ -876,15 +921,17 @@ __global__ void __launch_bounds__(A_THREADS) k_windows(const uint8_t* __restrict
 // a queue of uniform 4 KiB batches in one launch (final CRCs only)
 __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, const uint32_t* __restrict__ gtab,
                                                         uint32_t fin, uint32_t flags) {
+  // every argument the prologue needs, loaded in one batch (MAX_QJOBS >= 2: j[1] is in the argument block)
+  WinQueue src{jobs.j, jobs.n, jobs.nreg, jobs.j[0].base, jobs.j[0].nblk, jobs.j[1].reg0};
+  __asm__ volatile("" ::"s"(src.nj), "s"(src.nreg), "s"(src.b0), "s"(src.n0), "s"(src.r1), "s"(gtab), "s"(fin),
+                   "s"(flags), "s"(gridDim.x));
 #ifndef LCRC_Q_TREE
   __shared__ __attribute__((aligned(16))) uint32_t L[AQ_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
-  WinQueue src{jobs.j, jobs.n, jobs.nreg};
   windows_body<true, true>(src, gtab, fin, flags, L, &wg_ticket);
 #else  // ablation: the block tree of the single-batch kernel
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
-  WinQueue src{jobs.j, jobs.n, jobs.nreg};
   windows_body<true, false>(src, gtab, fin, flags, L, &wg_ticket);
 #endif
 }

@@ -31,7 +31,10 @@ full = np.frombuffer(st, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
 ok = full[:, 0] != 0
 t0 = full[ok, 0].min()
 rr = (full[:, :6] - t0) / 100.0  # 100 MHz ticks -> us: entry, tables, first half, end, loads issued, built
-print(f"Q {Q}: event {ms * 1000:.1f} us, waves {ok.sum()}")
+m.lib().lcrc_probe_clock_mhz.restype = ctypes.c_double
+m.lib().lcrc_probe_clock_mhz.argtypes = [ctypes.c_int]
+print(f"Q {Q}: event {ms * 1000:.1f} us, waves {ok.sum()}, shader clock {m.lib().lcrc_probe_clock_mhz(256):.0f} MHz "
+      "(median over workgroups, tile loop)")
 for k, name in ((0, "entry"), (4, "issued"), (5, "built"), (1, "tables"), (2, "first"), (3, "end")):
     print(f"  {name:7s}", np.percentile(rr[ok, k], [0, 10, 50, 90, 100]).round(2))
 ids = full[:, 6:8]
