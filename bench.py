@@ -9,11 +9,13 @@ configs[1]) already resident in HBM; four such batches rotate so every step read
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed|mixed|wal|table|seal|snappy]
                     [--mode c|ref] [--queue Q] [--streams S]
 
-Submission (fixed config). By default the K timed steps are submitted through lcrc_batch_uniform_queue, the
-way a storage server hands over its pending verify batches: each step is its own complete batch (own
-buffer, own CRC output), and the engine streams up to 32 of them per launch of the fast-path kernel, so the
-LDS table image and the end-of-launch spread are paid once per launch instead of once per batch.
-`--queue 1` submits one lcrc_batch_uniform launch per step instead (rotated over --streams contexts).
+Submission (fixed config). By default every step is one lcrc_batch_uniform launch, the launches rotated over
+two engines (context + HIP stream): the fast-path kernel leaves LDS for a second workgroup per CU, so the next
+step's workgroups fill each CU as soon as this step's tail leaves it (no end-of-launch spread, no launch gap).
+`--queue Q` (Q > 1) hands Q steps at a time to lcrc_batch_uniform_queue instead, the way a storage server
+hands over its pending verify batches: up to 32 complete batches (own buffer, own CRC output) per launch of
+the queued kernel on one stream (measured at the driver's 20 steps: 5,800-5,960 GiB/s against 6,070-6,280
+for the default; sustained over thousands of steps both settle at ~6,100, tools/probe/sustain.py).
 
 N GPUs (BASELINE configs[4]): one process per GPU. Under torch.distributed.run the ranks come from the
 environment; `python bench.py --gpus N` without it spawns the N rank processes itself (before anything
@@ -22,8 +24,9 @@ collective on the data path -- gloo carries only the barrier, the max-over-ranks
 figures. `value` = all ranks' bytes / max-over-ranks time (weak scaling).
 
 Prints ONE JSON line on rank 0. `roofline.achieved` = algorithmic bytes per launch / average launch duration,
-where the average comes from HIP events recorded on the engine stream around the timed region itself
-(queued submission: one stream; the same launches rocprofv3's kernel trace reports -- tools/profile_round.sh
+where the average comes from HIP events that the first and last launches of the timed region record
+themselves (fixed config, both submissions; over two streams the span runs from the first launch's start to the
+latest end of any stream's last launch) -- the launches rocprofv3's kernel trace reports (tools/profile_round.sh
 profiles this exact command). `roofline.profile` repeats the figure from the committed rocprofv3 summary in
 profiles/ for the same config. `cpu_baseline` times the oracle's restatement of the reference's CPU CRC on
 this host's usable cores (rank 0, N=1 only) and cross-checks the device CRCs against it.
@@ -61,10 +64,10 @@ def parse(argv=None):
     p.add_argument("--table-sync", action="store_true",
                    help="table config: time the synchronous lcrc_table_scan (results to pinned host memory)")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
-    p.add_argument("--queue", type=int, default=5,
-                   help="fixed config: steps per lcrc_batch_uniform_queue submission (default 5 = the driver's warmup, so "
-                        "every launch -- warmup and timed -- has the same shape; 0: all timed steps in one "
-                        "submission, <= 32 per launch, launches balanced; 1: one lcrc_batch_uniform per step)")
+    p.add_argument("--queue", type=int, default=1,
+                   help="fixed config: 1 (default): one lcrc_batch_uniform launch per step; Q > 1: steps per "
+                        "lcrc_batch_uniform_queue submission (<= 32 per launch, launches balanced); 0: all timed "
+                        "steps in one queued submission")
     p.add_argument("--streams", type=int, default=0,
                    help="engines (context + HIP stream) the submissions rotate over (0: 1 queued, 2 per-step)")
     p.add_argument("--blocks", type=int, default=65536, help="fixed config: 4 KiB blocks per batch")
@@ -151,47 +154,70 @@ class Dist:
 def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
     `prepare(first, count)` returns the submissions for steps first .. first+count-1 as (submit, launches,
-    steps) triples (argument marshalling done before the clock starts). The wall clock covers all K steps.
-    The GPU clock is HIP events on the first engine's stream. kernel_events (the queued fast path): the first
-    and the last submission's launches carry the events themselves (lcrc_timer_kernels ->
-    hipExtLaunchKernelGGL), from the first launch's start to the last one's end: every launch of the timed
-    region, back to back, with no host latency and no marker packet in between. Otherwise the clock starts when
-    the first submission's work has finished (an event enqueued behind it) and covers submissions 2..n.
+    steps[, engine]) tuples (argument marshalling done before the clock starts). The wall clock covers all K
+    steps. kernel_events (the fixed config's fast path): the first submission's launch and every engine's last
+    one carry the events themselves (lcrc_timer_kernels -> hipExtLaunchKernelGGL), and the GPU clock runs from
+    the first launch's start to the latest end (lcrc_timer_span): every launch of the timed region, with no host
+    latency and no marker packet in between. Otherwise the clock is HIP events on the first engine's stream,
+    from the end of the first submission's work (an event enqueued behind it) over submissions 2..n.
     Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock
     covers)."""
     carried = bool(engines) and kernel_events
+
+    def eng_of(sub):  # the engine a submission goes to (4th element; 0 when absent)
+        return sub[3] if len(sub) > 3 else 0
+
+    def arm(subs):
+        """edge 0 before the first submission on its engine, edge 1 before each engine's last submission"""
+        first = {0: eng_of(subs[0])} if subs else {}
+        last = {}
+        for k, sub in enumerate(subs):
+            last[eng_of(sub)] = k
+        return first, {k: e for e, k in last.items()}
+
+    def submit(subs, marker):
+        """marker: (not carried) start the marker timer behind the first submission"""
+        first, last = arm(subs) if carried else ({}, {})
+        for k, sub in enumerate(subs):
+            if k in first:
+                engines[first[k]].timer_kernels(0)
+            if k in last:
+                engines[last[k]].timer_kernels(1)
+            sub[0]()
+            if marker and k == 0 and engines and len(subs) > 1:
+                engines[0].timer_start()
+        return first, last
+
+    def span(first, last):
+        """first launch's start to the latest end of any engine's last launch (ms); engines disarmed"""
+        e0 = engines[first[0]]
+        ms = max(e0.timer_span(engines[e]) for e in last.values())
+        for e in engines:
+            e.timer_kernels(2)
+        return ms
+
     if warmup:
         wsubs = prepare(0, warmup)
-        for k, (sub, _, _) in enumerate(wsubs):
-            if carried and k == 0:  # the warmup goes through the timed region's launch path, events included
-                engines[0].timer_kernels(0)
-            if carried and k == len(wsubs) - 1:
-                engines[0].timer_kernels(1)
-            sub()
+        fw, lw = submit(wsubs, False)  # the warmup goes through the timed region's launch path, events included
         if carried:
-            engines[0].timer_stop()
+            span(fw, lw)
     subs = prepare(warmup, steps)
     for e in engines:
         e.sync()
     dist.barrier()
     t0 = time.perf_counter()
-    for k, (sub, _, _) in enumerate(subs):
-        if carried and k == 0:
-            engines[0].timer_kernels(0)
-        if carried and k == len(subs) - 1:
-            engines[0].timer_kernels(1)
-        sub()
-        if not carried and k == 0 and engines and len(subs) > 1:
-            engines[0].timer_start()
+    first, last = submit(subs, not carried)
     for e in engines:
         e.sync()
     elapsed = time.perf_counter() - t0
-    timed = carried or (bool(engines) and len(subs) > 1)
-    gpu_ms = engines[0].timer_stop() if timed else None
+    if carried:
+        gpu_ms = span(first, last)
+    else:
+        gpu_ms = engines[0].timer_stop() if (bool(engines) and len(subs) > 1) else None
     dist.barrier()
     first = 0 if carried else 1
-    cov_launches = sum(n for _, n, _ in subs[first:])
-    cov_steps = sum(k for _, _, k in subs[first:])
+    cov_launches = sum(sub[1] for sub in subs[first:])
+    cov_steps = sum(sub[2] for sub in subs[first:])
     return dist.max(elapsed), elapsed, gpu_ms, cov_launches, cov_steps
 
 
@@ -252,12 +278,13 @@ def workload_fixed(m, synth, engs, rank, device, args):
 
     if q == 1:  # one lcrc_batch_uniform launch per step, rotated over the engines
         def run(first, count):
-            for i in range(first, first + count):
-                k = i % len(engs)
-                engs[k].batch_uniform(bufs[i % NBUF], nblk, blen, blen, outs[k][i % NBUF])
+            return [(lambda k=i % len(engs), i=i: engs[k].batch_uniform(bufs[i % NBUF], nblk, blen, blen,
+                                                                        outs[k][i % NBUF]), 1, 1, i % len(engs))
+                    for i in range(first, first + count)]
+        run.prepares = True
 
         launches = lambda count: count  # noqa: E731
-        sub = "one lcrc_batch_uniform launch per step"
+        sub = f"one lcrc_batch_uniform launch per step, rotated over {len(engs)} streams"
     else:
         def run(first, count):
             subs = []
@@ -266,7 +293,7 @@ def workload_fixed(m, synth, engs, rank, device, args):
                 jobs = [(bufs[i % NBUF], nblk, outs[k][i % NBUF]) for i in range(i0, i0 + n)]
                 for part in balanced_jobs(jobs):
                     arr = m.ujobs(part)
-                    subs.append((lambda e=engs[k], a=arr: e.batch_uniform_queue(a, blen, blen), 1, len(part)))
+                    subs.append((lambda e=engs[k], a=arr: e.batch_uniform_queue(a, blen, blen), 1, len(part), k))
             return subs
         run.prepares = True
 
@@ -282,7 +309,7 @@ def workload_fixed(m, synth, engs, rank, device, args):
     cfg = {"workload": f"{nblk // 1024}K x 4 KiB blocks, device-resident (BASELINE configs[1])", "blocks": nblk,
            "block_bytes": blen, "batches_rotated": NBUF, "layout": "back-to-back", "submission": sub}
     return Workload(run, nblk * blen, cfg, launches, ("uniform", host[0], nblk, blen), crcs,
-                    kernel_events=q != 1 and len(engs) == 1 and not args.marker_timer)
+                    kernel_events=not args.marker_timer)
 
 
 def workload_fixed_host(m, synth, rank, args):
@@ -528,8 +555,14 @@ def load_profile(config, mode):
         with open(path) as f:
             s = json.load(f)
         if "frac" in s and "kernel" in s:
-            return {"file": os.path.relpath(path, ROOT), "kernel": s["kernel"], "avg_us": s["avg_us"],
-                    "bytes_per_launch": s["bytes_per_launch"], "frac": s["frac"]}
+            out = {"file": os.path.relpath(path, ROOT), "kernel": s["kernel"], "avg_us": s["avg_us"],
+                   "bytes_per_launch": s["bytes_per_launch"], "frac": s["frac"]}
+            # the line's own measure recomputed from the profiled run's kernel trace (launches back to back;
+            # over several streams they overlap, and avg_us is one launch's duration inside that overlap)
+            for k in ("trace_launch_us", "frac_from_trace", "agreement"):
+                if k in s:
+                    out[k] = s[k]
+            return out
     return None
 
 
@@ -630,11 +663,12 @@ def main(argv=None):
         per = w.launches(1)
         prepare = lambda f, c: [(lambda i=i: w.run(i, 1), per, 1) for i in range(f, f + c)]  # noqa: E731
     timers = w.engines if w.engines else engs
+    # this rank's fingerprint (gathered over gloo with the rates below), taken before the timed region so that
+    # the timed launches are the last ones of the dominant kernel in a profiled run (tools/summarize_profile.py)
+    fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
     elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, timers,
                                                                       kernel_events=w.kernel_events)
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
-    # this rank's fingerprint and rate, gathered over gloo (no RCCL)
-    fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
     rows = dist.gather([rank, device, elapsed, fp])
     per_gpu = [{"rank": int(r[0]), "device": int(r[1]),
                 "gib_s": round(w.nbytes * args.steps / r[2] / 2 ** 30, 2),
@@ -671,8 +705,12 @@ def main(argv=None):
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
             "timing": ("HIP events carried by the launches themselves (hipExtLaunchKernelGGL): first launch's "
-                       "start to last launch's end over every launch of the timed region, / the launches (back to "
-                       "back, dispatch gaps included)" if w.kernel_events else
+                       "start to the last launch's end over every launch of the timed region, / the launches (back "
+                       "to back, dispatch gaps included" +
+                       (f"; {len(timers)} streams: consecutive launches overlap, the next one's workgroups filling "
+                        "the CUs this one's tail leaves, so this is the per-launch rate of the stream of launches, "
+                        "below any single launch's duration)" if len(timers) > 1 else ")")
+                       if w.kernel_events else
                        "HIP events on the engine stream: from the end of the timed region's first submission to "
                        "its end, / the launches in between (back to back, dispatch gaps included)" if one_stream else
                        "HIP events on the first engine's stream from the end of the first step to the end of the "

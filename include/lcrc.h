@@ -289,11 +289,14 @@ int lcrc_memset_d(void* dst, int value, size_t bytes);
 int lcrc_device_sync(void);
 /* Event timing on the context stream (milliseconds between two recorded events). Or carried by the fast-path
  * launches themselves (lcrc_batch_uniform_queue): lcrc_timer_kernels(ctx, 0) before the first timed submission
- * (its launch records the start), lcrc_timer_kernels(ctx, 1) before the last (its launches record the end);
- * no marker between launches. lcrc_timer_stop ends either form. */
+ * (its launch records the start), lcrc_timer_kernels(ctx, 1) before the last (its launches record the end),
+ * lcrc_timer_kernels(ctx, 2) disarms; no marker between launches. lcrc_timer_stop ends either form. */
 int lcrc_timer_start(lcrc_ctx* ctx);
 int lcrc_timer_kernels(lcrc_ctx* ctx, int edge);
 int lcrc_timer_stop(lcrc_ctx* ctx, float* ms);
+/* Kernel-carried timing across contexts (one stream each, same device): `first`'s start event (edge 0) to
+ * `last`'s stop event (edge 1), for submissions rotated over several streams (lcrc_batch_uniform included). */
+int lcrc_timer_span(lcrc_ctx* first, lcrc_ctx* last, float* ms);
 
 /* HIP graphs of the context's own stream: lcrc_graph_begin starts capturing the calls made on the context
  * with stream NULL (they must allocate nothing: reserve first), lcrc_graph_end instantiates them as one

@@ -93,6 +93,7 @@ ABI_SYMBOLS = [
     "lcrc_tb_data", "lcrc_tb_blocks", "lcrc_tb_seal_descs",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_kernels", "lcrc_timer_stop",
+    "lcrc_timer_span",
     "lcrc_graph_begin", "lcrc_graph_end", "lcrc_graph_launch", "lcrc_graph_destroy",
     "lcrc_last_error", "lcrc_version",
 ]
@@ -156,6 +157,7 @@ def lib():
     sig("lcrc_timer_start", i32, vp)
     sig("lcrc_timer_kernels", i32, vp, i32)
     sig("lcrc_timer_stop", i32, vp, ctypes.POINTER(ctypes.c_float))
+    sig("lcrc_timer_span", i32, vp, vp, ctypes.POINTER(ctypes.c_float))
     sig("lcrc_graph_begin", i32, vp)
     sig("lcrc_graph_end", i32, vp, ctypes.POINTER(vp))
     sig("lcrc_graph_launch", i32, vp, vp)
@@ -562,12 +564,18 @@ class Engine:
 
     def timer_kernels(self, edge):
         """Fast-path launches carry the timer's events: edge 0 = the next launch records the start, edge 1 = the
-        launches from the next one on record the end."""
+        launches from the next one on record the end, edge 2 = disarm."""
         _check(lib().lcrc_timer_kernels(self.ctx, int(edge)), "lcrc_timer_kernels")
 
     def timer_stop(self):
         ms = ctypes.c_float(0)
         _check(lib().lcrc_timer_stop(self.ctx, ctypes.byref(ms)), "lcrc_timer_stop")
+        return ms.value
+
+    def timer_span(self, last):
+        """ms from this engine's kernel-carried start event to `last`'s stop event (lcrc_timer_span)."""
+        ms = ctypes.c_float(0)
+        _check(lib().lcrc_timer_span(self.ctx, last.ctx, ctypes.byref(ms)), "lcrc_timer_span")
         return ms.value
 
     # convenience: host numpy in, host numpy out (copies; for tests)

@@ -22,7 +22,8 @@
 extern "C" {
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
                                uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
-                               const uint32_t* expected, uint32_t* mismatch, hipStream_t st);
+                               const uint32_t* expected, uint32_t* mismatch, hipStream_t st,
+                               hipEvent_t t_start = nullptr, hipEvent_t t_stop = nullptr);
 hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* gtab, uint32_t x4096, uint32_t poly,
@@ -134,6 +135,7 @@ struct lcrc_ctx {
   hipStream_t copy_stream = nullptr;
   hipEvent_t t0 = nullptr, t1 = nullptr;
   bool tk_start = false, tk_stop = false, tk_any = false;  // lcrc_timer_kernels: launches that record t0 / t1
+  bool tk_end = false;  // a launch after edge 1 recorded t1
   uint32_t* d_tab = nullptr;
   uint32_t init = lcrc::CRC_INIT, xorout = lcrc::CRC_XOROUT, fin4096 = 0;
   uint32_t poly = 0, x4096 = 0;  // this mode's polynomial and x^(8*4096) mod P (k_ranges' chunk shift)
@@ -434,8 +436,13 @@ static int batch_uniform_impl(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint
   const uint32_t mflags = ctx->flags & LCRC_FLAG_MASK;
   if (length == 4096 && stride == 4096) {
     // single pass: k_windows folds each 4 KiB block and writes the final CRC
+    // kernel-carried timing (lcrc_timer_kernels), as in lcrc_batch_uniform_queue
+    hipEvent_t ts = ctx->tk_start ? ctx->t0 : nullptr, te = ctx->tk_stop ? ctx->t1 : nullptr;
     HIPCHK(lcrc_launch_windows(true, ctx->grid_a, base, (uint64_t)n * 4096, ctx->d_tab, out_crc, n, ctx->fin4096,
-                               mflags, expected, out_mismatch, st));
+                               mflags, expected, out_mismatch, st, ts, te));
+    if (ts) ctx->tk_any = true;
+    if (te) ctx->tk_end = true;
+    ctx->tk_start = false;
     return LCRC_OK;
   }
   const uint64_t span = (uint64_t)(n - 1) * stride + length;
@@ -513,6 +520,7 @@ int lcrc_batch_uniform_queue(lcrc_ctx* ctx, const lcrc_ujob* jobs, size_t njobs,
       HIPCHK(lcrc_launch_windows_queue(ctx->grid_a, q, m, ctx->d_tab, ctx->fin4096, ctx->flags & LCRC_FLAG_MASK, st,
                                        ts, te));
       if (ts) ctx->tk_any = true;
+      if (te) ctx->tk_end = true;
       ctx->tk_start = false;
     }
   }
@@ -1314,8 +1322,8 @@ int lcrc_timer_start(lcrc_ctx* ctx) {
 int lcrc_timer_stop(lcrc_ctx* ctx, float* ms) {
   if (!ctx || !ms) return LCRC_EINVAL;
   if (ctx->tk_stop) {  // kernel-carried: the events are the first and last launches' own start and end
-    const bool any = ctx->tk_any;
-    ctx->tk_start = ctx->tk_stop = ctx->tk_any = false;
+    const bool any = ctx->tk_any && ctx->tk_end;
+    ctx->tk_start = ctx->tk_stop = ctx->tk_any = ctx->tk_end = false;
     if (!any) return LCRC_EINVAL;
   } else {
     HIPCHK(hipEventRecord(ctx->t1, ctx->stream));
@@ -1326,15 +1334,30 @@ int lcrc_timer_stop(lcrc_ctx* ctx, float* ms) {
 }
 // Fast-path launches carry the timer's events themselves (hipExtLaunchKernelGGL): edge 0 -- the next launch
 // records t0 at its start; edge 1 -- the launches from the next one on record t1 at their end (the last one
-// wins). No marker packet between launches, no host latency before the first kernel. Ended by lcrc_timer_stop.
+// wins); edge 2 -- disarm. No marker packet between launches, no host latency before the first kernel. Ended by
+// lcrc_timer_stop.
 int lcrc_timer_kernels(lcrc_ctx* ctx, int edge) {
-  if (!ctx || edge < 0 || edge > 1) return LCRC_EINVAL;
-  if (edge == 0) {
+  if (!ctx || edge < 0 || edge > 2) return LCRC_EINVAL;
+  if (edge == 2) {  // disarm
+    ctx->tk_start = ctx->tk_stop = ctx->tk_any = ctx->tk_end = false;
+  } else if (edge == 0) {
     ctx->tk_start = true;
     ctx->tk_any = false;
   } else {
     ctx->tk_stop = true;
+    ctx->tk_end = false;
   }
+  return LCRC_OK;
+}
+// Kernel-carried timing over several contexts (one stream each, same device): from `first`'s start event to
+// `last`'s stop event. The caller arms edge 0 on the context of the first timed launch and edge 1 on every
+// context before its last timed launch, then takes the largest span over the contexts. Waits for `last`'s
+// stop event; the timers stay armed until lcrc_timer_stop (or lcrc_timer_kernels) resets them.
+int lcrc_timer_span(lcrc_ctx* first, lcrc_ctx* last, float* ms) {
+  if (!first || !last || !ms || first->device != last->device) return LCRC_EINVAL;
+  if (!first->tk_any || !last->tk_stop || !last->tk_end) return LCRC_EINVAL;
+  HIPCHK(hipEventSynchronize(last->t1));
+  HIPCHK(hipEventElapsedTime(ms, first->t0, last->t1));
   return LCRC_OK;
 }
 

@@ -2927,15 +2927,20 @@ double lcrc_probe_clock_mhz(int nwg) {
 }
 #endif
 
+// t_start / t_stop (nullable, final mode): events recorded by the dispatch itself, as in lcrc_launch_windows_queue
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
                                uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
-                               const uint32_t* expected, uint32_t* mismatch, hipStream_t st) {
+                               const uint32_t* expected, uint32_t* mismatch, hipStream_t st, hipEvent_t t_start,
+                               hipEvent_t t_stop) {
   const uint64_t nreg = (span + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
   if (nreg == 0) return hipSuccess;
   grid *= lcrc_dev::A_WG_PER_CU;  // `grid` = CUs
   uint64_t need = (nreg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
   int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
-  if (final_mode)
+  if (final_mode && (t_start || t_stop))
+    hipExtLaunchKernelGGL(lcrc_dev::k_windows<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, t_start, t_stop, 0,
+                          base, span, nreg, gtab, out, nblk, fin, flags, expected, mismatch);
+  else if (final_mode)
     hipLaunchKernelGGL(lcrc_dev::k_windows<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg, gtab,
                        out, nblk, fin, flags, expected, mismatch);
   else

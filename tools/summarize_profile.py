@@ -88,8 +88,8 @@ def main(outdir, rnd, config, mode):
                 kernel_events = "carried by the launches" in line["roofline"].get("timing", "")
                 timed = ts[-(nl + 1):] if len(ts) > nl else []
                 span = None
-                if kernel_events and len(ts) >= nl:  # first launch's start to the last one's end
-                    span = (ts[-1][1] - ts[-nl][0]) / 1e3 / nl
+                if kernel_events and len(ts) >= nl:  # first launch's start to the latest end (several streams)
+                    span = (max(e for _, e in ts[-nl:]) - ts[-nl][0]) / 1e3 / nl
                 elif timed:
                     span = (timed[-1][1] - timed[0][1]) / 1e3 / nl
                 if span:
@@ -119,6 +119,10 @@ def main(outdir, rnd, config, mode):
                        "hbm_write_bytes_per_launch": t["hbm_write_bytes_per_launch"],
                        "source": f"profiles/{tag}_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
                                  "FETCH_SIZE KiB x1024 x2 per the gfx950 correction)"}, f, indent=1)
+    if summary.get("bench_line", {}).get("streams", 1) > 1 and "kernel" in summary:
+        summary["overlap_note"] = ("launches rotate over several streams and run concurrently (two workgroups per CU, "
+                                   "one of each launch): a launch's own duration (avg_us, frac) spans its overlap with "
+                                   "its neighbours; the rate of the stream of launches is trace_launch_us")
     print(json.dumps(summary, indent=1))
 
 
