@@ -50,6 +50,7 @@ METRIC = "GiB/s CRC32C over device-resident 4 KiB blocks; % of HBM3E read BW"
 PEAK_GBS = 8000.0  # MI355X HBM3E peak, GB/s (MI355X_MICROARCH.md chip table, spec)
 NBUF = 4
 QMAX = 32  # batches per queued launch (MAX_QJOBS in lcrc_kernels.hip)
+MIXED_QUEUE = 1  # mixed config: steps per lcrc_batch_queue submission (1: one lcrc_batch per step)
 
 
 def parse(argv=None):
@@ -64,10 +65,12 @@ def parse(argv=None):
     p.add_argument("--table-sync", action="store_true",
                    help="table config: time the synchronous lcrc_table_scan (results to pinned host memory)")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
-    p.add_argument("--queue", type=int, default=1,
+    p.add_argument("--queue", type=int, default=None,
                    help="fixed config: 1 (default): one lcrc_batch_uniform launch per step; Q > 1: steps per "
                         "lcrc_batch_uniform_queue submission (<= 32 per launch, launches balanced); 0: all timed "
-                        "steps in one queued submission")
+                        "steps in one queued submission. mixed config: Q > 1: steps per "
+                        "lcrc_batch_queue submission on one engine; 1 (default): one lcrc_batch per step, rotated over the "
+                        "engines")
     p.add_argument("--streams", type=int, default=0,
                    help="engines (context + HIP stream) the submissions rotate over (0: 1 queued, 2 per-step)")
     p.add_argument("--blocks", type=int, default=65536, help="fixed config: 4 KiB blocks per batch")
@@ -361,10 +364,28 @@ def workload_mixed(m, synth, engs, rank, device, args):
     for e in engs:
         e.reserve(total)
 
-    def run(first, count):
-        for i in range(first, first + count):
-            k = i % len(engs)
-            engs[k].batch(bufs[i % 2], total, dd, len(sizes), outs[k])
+    q = args.queue
+    if q == 1:  # one lcrc_batch per step, rotated over the engines
+        def run(first, count):
+            for i in range(first, first + count):
+                k = i % len(engs)
+                engs[k].batch(bufs[i % 2], total, dd, len(sizes), outs[k])
+        launches = None
+        sub = f"one lcrc_batch per step, rotated over {len(engs)} streams"
+    else:  # lcrc_batch_queue: q steps per submission, the two passes pipelined across them (window pass of
+        # step i+1 beside the range pass of step i)
+        qouts = [m.DeviceBuffer(4 * len(sizes), device) for _ in range(2)]
+
+        def run(first, count):
+            subs = []
+            for g, (i0, n) in enumerate(groups(first, count, q)):
+                k = g % len(engs)
+                arr = m.gjobs([(bufs[i % 2], total, dd, len(sizes), qouts[i % 2]) for i in range(i0, i0 + n)])
+                subs.append((lambda e=engs[k], a=arr: e.batch_queue(a), n, n, k))
+            return subs
+        run.prepares = True
+        launches = lambda count: count  # noqa: E731  (one window pass per step)
+        sub = f"lcrc_batch_queue of {q} steps per submission ({len(engs)} stream(s) + the context's side stream)"
 
     def crcs():
         engs[0].batch(bufs[0], total, dd, len(sizes), outs[0])
@@ -372,8 +393,8 @@ def workload_mixed(m, synth, engs, rank, device, args):
         return outs[0].download(np.uint32, len(sizes))
 
     cfg = {"workload": "SSTable file, block sizes 256 B-64 KiB zipf(1.1) (BASELINE configs[2])",
-           "blocks": int(len(sizes)), "file_bytes": int(total), "mean_block": float(sizes.mean())}
-    return Workload(run, int(lens.sum()), cfg, None, ("ranges", data, offs, lens), crcs)
+           "blocks": int(len(sizes)), "file_bytes": int(total), "mean_block": float(sizes.mean()), "submission": sub}
+    return Workload(run, int(lens.sum()), cfg, launches, ("ranges", data, offs, lens), crcs)
 
 
 def workload_wal(m, synth, engs, rank, device, args):
@@ -644,7 +665,9 @@ def main(argv=None):
     synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
     mode = m.MODE_C if args.mode == "c" else m.MODE_REF
     flags = m.FLAG_MASK if mode == m.MODE_C else 0
-    queued = args.config == "fixed" and not args.host_resident and args.queue != 1
+    if args.queue is None:
+        args.queue = MIXED_QUEUE if args.config == "mixed" else 1
+    queued = args.config in ("fixed", "mixed") and not args.host_resident and args.queue != 1
     nstreams = args.streams or (1 if queued else 2)
     if args.engine == "host":
         engs = []

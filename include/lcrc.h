@@ -168,6 +168,25 @@ typedef struct lcrc_ujob {
 int lcrc_batch_uniform_queue(lcrc_ctx* ctx, const lcrc_ujob* jobs, size_t njobs, uint32_t length, uint64_t stride,
                              void* stream);
 
+/* One batch of a general queue (lcrc_batch_queue): exactly the arguments of one lcrc_batch call. */
+typedef struct lcrc_gjob {
+  const uint8_t* base;    /* device */
+  uint64_t base_len;
+  const lcrc_desc* descs; /* device, n descriptors */
+  uint64_t n;
+  uint32_t* out_crc;      /* device, n words */
+  uint32_t* out_mismatch; /* device, nullable, ceil(n/32) words, zeroed by the call */
+} lcrc_gjob;
+
+/* A queue of independent descriptor batches (jobs: HOST array of njobs), each exactly as one
+ * lcrc_batch(ctx, jobs[k].base, jobs[k].base_len, jobs[k].descs, jobs[k].n, ...) call -- e.g. every SSTable
+ * of a compaction's output, or the files a recovery verifies. The general path's two passes are pipelined
+ * across the batches: the window pass of batch k+1 streams while the range pass of batch k finishes beside
+ * it on a second stream of the context, so consecutive window passes run back to back instead of waiting
+ * for each batch's latency-bound second pass. Enqueued on `stream` (the forked work joins it before the
+ * call's end), graph-capturable, nothing synchronized. */
+int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* stream);
+
 /* Same as lcrc_batch_uniform but base / expected / out_crc / out_mismatch are HOST pointers. Data is
  * staged through pinned buffers in chunks of chunk_bytes (0 = default) with H2D copies overlapping
  * the kernels. Synchronous. */

@@ -75,6 +75,11 @@ class _UJob(ctypes.Structure):
                 ("out_crc", ctypes.c_void_p), ("out_mismatch", ctypes.c_void_p)]
 
 
+class _GJob(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("base_len", ctypes.c_uint64), ("descs", ctypes.c_void_p),
+                ("n", ctypes.c_uint64), ("out_crc", ctypes.c_void_p), ("out_mismatch", ctypes.c_void_p)]
+
+
 class _Hasher(ctypes.Structure):
     _fields_ = [("state", ctypes.c_uint32), ("mode", ctypes.c_int32), ("amount", ctypes.c_uint64)]
 
@@ -86,7 +91,7 @@ ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
-    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
+    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
     "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_tb_create", "lcrc_tb_destroy", "lcrc_tb_add", "lcrc_tb_flush", "lcrc_tb_finish", "lcrc_tb_size",
@@ -136,6 +141,7 @@ def lib():
     sig("lcrc_batch_covered", i32, vp, vp, u64, vp, sz, u64, vp, vp, vp)
     sig("lcrc_batch_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, vp)
     sig("lcrc_batch_uniform_queue", i32, vp, ctypes.POINTER(_UJob), sz, u32, u64, vp)
+    sig("lcrc_batch_queue", i32, vp, ctypes.POINTER(_GJob), sz, vp)
     sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
     sig("lcrc_wal_scan", i32, vp, vp, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp)
     sig("lcrc_wal_scan_async", i32, vp, vp, u64, vp, sz, vp, vp)
@@ -421,6 +427,13 @@ class Engine:
         _check(lib().lcrc_batch_uniform_queue(self.ctx, arr.arr, arr.n, int(length), int(stride), stream),
                "lcrc_batch_uniform_queue")
 
+    def batch_queue(self, jobs, stream=None):
+        """lcrc_batch_queue: jobs = [(base, base_len, descs, n, out_crc[, out_mismatch])] (or the array gjobs()
+        made of them), each one lcrc_batch batch; the window pass of each batch streams while the previous
+        batch's range pass finishes beside it."""
+        arr = jobs if isinstance(jobs, GJobs) else gjobs(jobs)
+        _check(lib().lcrc_batch_queue(self.ctx, arr.arr, arr.n, stream), "lcrc_batch_queue")
+
     def batch_host_uniform(self, base, n, length, stride, expected=None, chunk_bytes=0):
         """Host-resident input (numpy / PinnedBuffer). Returns (crc array, mismatch bitmap)."""
         bp, _nb, keep = (base.ptr, base.nbytes, base) if isinstance(base, PinnedBuffer) else _buf(base)
@@ -613,6 +626,22 @@ class UJobs:
 
 def ujobs(jobs):
     return UJobs(jobs)
+
+
+class GJobs:
+    """A prepared lcrc_gjob array (lcrc_batch_queue's jobs, built once, submitted any number of times)."""
+
+    def __init__(self, jobs):
+        self.n = len(jobs)
+        self.arr = (_GJob * max(1, self.n))()
+        self.keep = list(jobs)
+        for k, j in enumerate(jobs):
+            mm = j[5] if len(j) > 5 else None
+            self.arr[k] = _GJob(_ptr(j[0]), int(j[1]), _ptr(j[2]), int(j[3]), _ptr(j[4]), _ptr(mm))
+
+
+def gjobs(jobs):
+    return GJobs(jobs)
 
 
 def unpack_bits(words, n):

@@ -142,6 +142,9 @@ struct lcrc_ctx {
   int general = 0;  // general path: 0 auto (k_ranges for uniform one-chunk layouts), 1 k_ranges, 2 k_windows + k_blocks
   int grid_a = 256, grid_b = 1024;
   DevBuf<uint32_t> win;       // window partials for the general path
+  DevBuf<uint32_t> win2;      // lcrc_batch_queue: the second window buffer (batches alternate)
+  hipStream_t side = nullptr;  // lcrc_batch_queue: the range passes, beside the next batch's window pass
+  hipEvent_t q_fork = nullptr, q_join = nullptr, q_w[2] = {nullptr, nullptr}, q_b[2] = {nullptr, nullptr};
   DevBuf<uint8_t> chunk[2];   // host-resident pipeline staging
   DevBuf<uint32_t> hexp[2];   // expected values per chunk
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
@@ -294,6 +297,10 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
     if ((e = hipEventCreateWithFlags(&ctx->ev_copied[i], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming)) != hipSuccess)
       return bail(fail_hip(e, "hipEventCreate"));
+  if ((e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking)) != hipSuccess)
+    return bail(fail_hip(e, "hipStreamCreate"));
+  for (hipEvent_t* ev : {&ctx->q_fork, &ctx->q_join, &ctx->q_w[0], &ctx->q_w[1], &ctx->q_b[0], &ctx->q_b[1]})
+    if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bail(fail_hip(e, "hipEventCreate"));
   if ((e = hipHostMalloc(&ctx->h_count, 8 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
     return bail(fail_hip(e, "hipHostMalloc"));
   if ((e = hipHostMalloc(&ctx->ts_host, sizeof(lcrc_tscan_dev), hipHostMallocDefault)) != hipSuccess)
@@ -317,7 +324,11 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   ctx->win.release();
+  ctx->win2.release();
+  for (hipEvent_t ev : {ctx->q_fork, ctx->q_join, ctx->q_w[0], ctx->q_w[1], ctx->q_b[0], ctx->q_b[1]})
+    if (ev) (void)hipEventDestroy(ev);
   for (int i = 0; i < 2; ++i) {
     ctx->chunk[i].release();
     ctx->hexp[i].release();
@@ -357,6 +368,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   if (ctx->t1) (void)hipEventDestroy(ctx->t1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   delete ctx;
   return LCRC_OK;
 }
@@ -375,9 +387,14 @@ int lcrc_ctx_reserve(lcrc_ctx* ctx, uint64_t max_span) {
   if (!ctx) return LCRC_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
-  return ctx->win.ensure(window_words(max_span));
+  if ((rc = ctx->win.ensure(window_words(max_span)))) return rc;
+  return ctx->win2.ensure(window_words(max_span));  // lcrc_batch_queue's second window buffer
 }
 
+#ifndef LCRC_BATCH_WG_PER_CU
+#define LCRC_BATCH_WG_PER_CU 2  // 16 waves per CU: a full 32-wave grid cut config 3 k_blocks alone 22.0 -> 18.0 us but
+                                // crowded a concurrent batch on another stream (2-stream wall 4.1-4.3K -> 3.8K GiB/s)
+#endif
 int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
                uint32_t* out_crc, uint32_t* out_mismatch, void* stream) {
   if (!ctx || (n && (!descs || !out_crc || !base))) return LCRC_EINVAL;
@@ -400,13 +417,61 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
                                st));
     win = ctx->win.p;
   }
-#ifndef LCRC_BATCH_WG_PER_CU
-#define LCRC_BATCH_WG_PER_CU 2  // 16 waves per CU: a full 32-wave grid cut config 3 k_blocks alone 22.0 -> 18.0 us but
-                                // crowded a concurrent batch on another stream (2-stream wall 4.1-4.3K -> 3.8K GiB/s)
-#endif
   HIPCHK(lcrc_launch_blocks(false, std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU), base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
                             ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK, out_crc,
                             out_mismatch, nullptr, nullptr, st));
+  return LCRC_OK;
+}
+
+// The general path over a queue of batches, its two passes pipelined across them:
+//   stream:  W_0 -> W_1 -> W_2 (after R_0) -> ...        (window passes back to back on the HBM stream)
+//   side:    R_0 (after W_0) -> R_1 (after W_1) -> ...    (each range pass beside the next window pass)
+// Batches alternate between two window buffers, so W_k waits only for R_{k-2}, the last reader of its buffer.
+// The side stream first waits for everything enqueued on `stream` before the call, and `stream` waits for
+// the last range pass before anything enqueued after it: a fork and a join, so the call behaves as its
+// batches would one after another on `stream` (and captures into a graph as two branches).
+// (Two contexts on two streams each running W then R per batch fall into lockstep: both window passes share
+// the HBM stream, then both range passes leave it idle.)
+int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* stream) {
+  if (!ctx || (njobs && !jobs)) return LCRC_EINVAL;
+  for (size_t k = 0; k < njobs; ++k)
+    if (jobs[k].n && (!jobs[k].descs || !jobs[k].out_crc || !jobs[k].base)) return LCRC_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  const bool direct = (ctx->flags & LCRC_FLAG_DIRECT) != 0;
+  if (direct || ctx->general == 1 || njobs < 2) {  // one pass per batch (or nothing to pipeline)
+    for (size_t k = 0; k < njobs; ++k)
+      if ((rc = lcrc_batch(ctx, jobs[k].base, jobs[k].base_len, jobs[k].descs, jobs[k].n, jobs[k].out_crc,
+                           jobs[k].out_mismatch, st)))
+        return rc;
+    return LCRC_OK;
+  }
+  uint64_t span = 0;
+  for (size_t k = 0; k < njobs; ++k) span = std::max(span, jobs[k].base_len);
+  if ((rc = ctx->win.ensure(window_words(span))) || (rc = ctx->win2.ensure(window_words(span)))) return rc;
+  uint32_t* wins[2] = {ctx->win.p, ctx->win2.p};
+  const int grid_b = std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU);
+  HIPCHK(hipEventRecord(ctx->q_fork, st));
+  HIPCHK(hipStreamWaitEvent(ctx->side, ctx->q_fork, 0));
+  for (size_t k = 0; k < njobs; ++k) {
+    const lcrc_gjob& j = jobs[k];
+    const int b = (int)(k & 1);
+    if (k >= 2) HIPCHK(hipStreamWaitEvent(st, ctx->q_b[b], 0));  // R_{k-2} has read this window buffer
+    if (j.n && j.base_len)
+      HIPCHK(lcrc_launch_windows(false, ctx->grid_a, j.base, j.base_len, ctx->d_tab, wins[b], 0, 0, 0, nullptr,
+                                 nullptr, st));
+    HIPCHK(hipEventRecord(ctx->q_w[b], st));
+    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->q_w[b], 0));
+    if (j.out_mismatch && j.n)
+      HIPCHK(hipMemsetAsync(j.out_mismatch, 0, ((j.n + 31) / 32) * sizeof(uint32_t), ctx->side));
+    HIPCHK(lcrc_launch_blocks(false, grid_b, j.base, j.base_len, (const lcrc_desc_dev*)j.descs, j.n, 0, 0, nullptr,
+                              j.base_len ? wins[b] : nullptr, ctx->d_tab, ctx->init, ctx->xorout,
+                              ctx->flags & LCRC_FLAG_MASK, j.out_crc, j.out_mismatch, nullptr, nullptr, ctx->side));
+    HIPCHK(hipEventRecord(ctx->q_b[b], ctx->side));
+  }
+  HIPCHK(hipEventRecord(ctx->q_join, ctx->side));
+  HIPCHK(hipStreamWaitEvent(st, ctx->q_join, 0));
   return LCRC_OK;
 }
 

@@ -625,7 +625,8 @@ __device__ __forceinline__ void build_tables(uint32_t* L, const uint32_t* __rest
 __device__ unsigned long long lcrc_dbg_clock[4096];   // k_windows per workgroup: shader and real clock
 __device__ unsigned long long lcrc_dbg_stamp[4096 * 8];  // k_windows per wave: entry, tables ready, first half,
                                                         // end, table source loaded, staged, HW_ID, XCC_ID
-__device__ unsigned long long lcrc_dbg_bstamp[8192 * 4];  // k_blocks per wave: entry, tables, first range, end
+__device__ unsigned long long lcrc_dbg_bstamp[8192 * 8];  // k_blocks per wave: entry, tables, the ends of the
+                                                         // first 5 iterations, end
 #endif
 
 // Where k_windows' regions come from. WinOne: one contiguous span (a batch, a file). WinQueue: a queue of
@@ -1104,7 +1105,8 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
   __shared__ __attribute__((aligned(16))) uint32_t L[B_LDS_DWORDS];
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long b_entry = __builtin_amdgcn_s_memrealtime();
-  unsigned long long b_first = 0;
+  unsigned long long b_it[5] = {0, 0, 0, 0, 0};
+  uint32_t b_nit = 0;
 #endif
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
   const uint32_t lane = __lane_id();
@@ -1112,36 +1114,26 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
   const uint64_t wave = (uint64_t)blockIdx.x * (B_THREADS / 64) + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * (B_THREADS / 64);
   const bool use_win = win != nullptr;
-  // descriptors are loaded one iteration ahead of their use (the first one before the table fill)
+  // descriptors are loaded one iteration ahead of their use (the first one before the table fill); the
+  // raw words are kept and checked only when the iteration that uses them starts, so the load is not
+  // waited for where it is issued.
   // a range outside [0, base_len) is never read: it becomes empty, CRC 0, and is flagged as a mismatch
-  auto load_desc = [&](uint64_t i, uint64_t& s, uint32_t& len, int32_t& xrel, bool& oob) {
-    s = 0;
-    len = 0;
-    xrel = LCRC_NO_EXPECT_DEV;
-    oob = false;
+  auto load_desc = [&](uint64_t i, lcrc_desc_dev& d) {
+    d.offset = 0;
+    d.length = 0;
+    d.expect_rel = LCRC_NO_EXPECT_DEV;
     if (i < n) {
       if (UNIFORM) {
-        s = i * ustride;
-        len = ulen;
+        d.offset = i * ustride;
+        d.length = ulen;
       } else {
-        const lcrc_desc_dev d = descs[i];
-        s = d.offset;
-        len = d.length;
-        xrel = d.expect_rel;
-        if (s > base_len || len > base_len - s) {
-          oob = true;
-          s = 0;
-          len = 0;
-        }
+        d = descs[i];
       }
     }
   };
-  uint64_t s_nx;
-  uint32_t len_nx;
-  int32_t xrel_nx;
-  bool oob_nx;
+  lcrc_desc_dev d_nx;
 #ifdef LCRC_KB_TREE4
-  load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx, oob_nx);
+  load_desc(wave * 4 + row, d_nx);
   for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS) {
     const uint32_t w = 4 * i;  // slice | Z4096 | the 4-way tree shifts
     const uint32_t src = w < 1024 ? TAB_SLICE + w : w < 2048 ? TAB_Z4096 + (w - 1024) : TAB_KB4 + (w - 2048);
@@ -1157,7 +1149,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       const uint32_t i = threadIdx.x + k * B_THREADS;
       if (i < B_LDS_DWORDS / 4) t[k] = ((const u32x4*)gtab)[i];
     }
-    load_desc(wave * 4 + row, s_nx, len_nx, xrel_nx, oob_nx);  // the first descriptor in the same round trip
+    load_desc(wave * 4 + row, d_nx);  // the first descriptor in the same round trip
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const uint32_t i = threadIdx.x + k * B_THREADS;
@@ -1170,14 +1162,17 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
   const unsigned long long b_tab = __builtin_amdgcn_s_memrealtime();
 #endif
 
+#if defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 1  // ablation: table fill only
+  if (n) return;
+#endif
   for (uint64_t i0 = wave * 4; i0 < n; i0 += nwaves * 4) {
     const uint64_t i = i0 + row;
     const bool valid = i < n;
-    const uint64_t s = s_nx;
-    const uint32_t len = len_nx;
-    const int32_t xrel = xrel_nx;
-    const bool oob = oob_nx;
-    load_desc(i + nwaves * 4, s_nx, len_nx, xrel_nx, oob_nx);
+    const bool oob = !UNIFORM && (d_nx.offset > base_len || (uint64_t)d_nx.length > base_len - d_nx.offset);
+    const uint64_t s = oob ? 0 : d_nx.offset;
+    const uint32_t len = oob ? 0u : d_nx.length;
+    const int32_t xrel = d_nx.expect_rel;
+    load_desc(i + nwaves * 4, d_nx);
     const uint64_t e = s + len;
     // the expected value, loaded with the data (bytewise: any alignment, and checked against the buffer)
     uint32_t expv = 0;
@@ -1204,8 +1199,11 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       const uint32_t rr32 = rounds;
       // lane g's window value of round q is wv[16 q] (the slots before the head are padding)
       const uint32_t* wv = win + ws + g - npad;
-      const uint32_t rmax = max(max(__builtin_amdgcn_readlane(rr32, 0), __builtin_amdgcn_readlane(rr32, 16)),
+      uint32_t rmax = max(max(__builtin_amdgcn_readlane(rr32, 0), __builtin_amdgcn_readlane(rr32, 16)),
                                 max(__builtin_amdgcn_readlane(rr32, 32), __builtin_amdgcn_readlane(rr32, 48)));
+#if defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 3  // ablation: no window fold (wrong CRCs)
+      if (n) rmax = 0;
+#endif
 
       // every load this range needs first: head and tail pieces, the first batch of window values
       const RowPiece ph = row_load(base, s, head_end, g);
@@ -1214,7 +1212,11 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int j = 0; j < B_BATCH; ++j) vals[j] = ((uint32_t)j < rounds && 16u * j + g > npad) ? wv[16 * j] : 0u;
 
+#if defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 2  // ablation: no head/tail walks (wrong CRCs)
+      const uint32_t head = ph.w[0] ^ ph.w[1] ^ pt.w[2];
+#else
       const uint32_t head = row_walk(L, ph, s == head_end, init, g, lane);
+#endif
       uint32_t a = 0;
       for (uint32_t q0 = 0; q0 < rmax; q0 += B_BATCH) {
         if (q0) {
@@ -1242,7 +1244,9 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       const uint32_t mid = row_bcast0(a, lane);
       acc = single ? head : mid;
       // tail: the partial last window, walked from the folded value
+#if !(defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 2)
       acc = row_walk(L, pt, ta == e, acc, g, lane);
+#endif
     } else {
       // direct: walk the whole range in 256 B chunks (sparse batches)
       uint32_t nch = (uint32_t)(((uint64_t)len + 255) >> 8);
@@ -1280,16 +1284,16 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       }
     }
 #ifdef LCRC_PROBE_CLOCK
-    if (!b_first) b_first = __builtin_amdgcn_s_memrealtime();
+    if (b_nit < 5) b_it[b_nit++] = __builtin_amdgcn_s_memrealtime();
 #endif
   }
 #ifdef LCRC_PROBE_CLOCK
   const uint64_t gw = (uint64_t)blockIdx.x * (B_THREADS / 64) + (threadIdx.x >> 6);
   if (lane == 0 && gw < 8192) {
-    lcrc_dbg_bstamp[gw * 4 + 0] = b_entry;
-    lcrc_dbg_bstamp[gw * 4 + 1] = b_tab;
-    lcrc_dbg_bstamp[gw * 4 + 2] = b_first;
-    lcrc_dbg_bstamp[gw * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    lcrc_dbg_bstamp[gw * 8 + 0] = b_entry;
+    lcrc_dbg_bstamp[gw * 8 + 1] = b_tab;
+    for (int k = 0; k < 5; ++k) lcrc_dbg_bstamp[gw * 8 + 2 + k] = b_it[k];
+    lcrc_dbg_bstamp[gw * 8 + 7] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
@@ -2908,7 +2912,7 @@ int lcrc_probe_stamps(unsigned long long* dst) {
 }
 
 int lcrc_probe_bstamps(unsigned long long* dst) {
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(lcrc_dev::lcrc_dbg_bstamp), sizeof(unsigned long long) * 8192 * 4) ==
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(lcrc_dev::lcrc_dbg_bstamp), sizeof(unsigned long long) * 8192 * 8) ==
                  hipSuccess ? 0 : -1;
 }
 

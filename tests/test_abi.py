@@ -36,6 +36,9 @@ def test_kernel_image_is_gfx950(lcrc):
 def test_struct_layouts(lcrc):
     assert lcrc.DESC_DTYPE.itemsize == 16
     assert lcrc.WAL_REC_DTYPE.itemsize == 24
+    import ctypes
+    assert ctypes.sizeof(lcrc._GJob) == 48 and lcrc._GJob.out_mismatch.offset == 40  # lcrc_gjob
+    assert ctypes.sizeof(lcrc._UJob) == 40  # lcrc_ujob
 
 
 @pytest.mark.parametrize("n", [0, 1, 3, 7, 8, 9, 16, 100, 4096, 100003])
@@ -82,6 +85,7 @@ def test_batched_api_fails_loudly_without_device(lcrc):
     with pytest.raises(lcrc.NoDeviceError):
         lcrc.Engine(0, lcrc.MODE_C)
     assert lcrc.lib().lcrc_batch(None, None, 0, None, 0, None, None, None) == lcrc.EINVAL
+    assert lcrc.lib().lcrc_batch_queue(None, None, 0, None) == lcrc.EINVAL
 
 
 def test_scalar_extend_every_length_and_register(lcrc, orc):

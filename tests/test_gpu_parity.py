@@ -590,3 +590,88 @@ def test_sparse_verify_in_a_large_file(lcrc, orc):
     print(f"sparse verify: 100 x 4,097 B in a 1 GiB buffer: {us:.1f} us per call")
     assert us < 60.0
     eng.close()
+
+
+@pytest.mark.parametrize("path", ["auto", "ranges"])
+def test_general_queue_matches_batches(lcrc, orc, path, monkeypatch):
+    """lcrc_batch_queue: 7 independent descriptor batches (different file sizes, an empty batch, a batch of
+    zero-length file, expected values with injected mismatches, out-of-bounds descriptors) in one call, the
+    window pass of each batch beside the previous batch's range pass on the context's second stream: the CRCs
+    and mismatch bits of 7 separate lcrc_batch calls and of the oracle; then the same queue captured in a HIP
+    graph (a fork and a join) and replayed twice."""
+    if path != "auto":
+        monkeypatch.setenv("LCRC_GENERAL", path)
+    rng = np.random.default_rng(0x9E)
+    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
+    jobs, want, keep = [], [], []
+    for k, size in enumerate([3 << 20, 1 << 20, 5 << 20, 0, 2 << 20, 777_777, 4 << 20]):
+        data = rng.integers(0, 256, max(size, 1), dtype=np.uint8)[:size]
+        n = 0 if k == 1 else int(rng.integers(1, 900))
+        lens = rng.integers(0, 70000, n).astype(np.uint32)
+        offs = np.array([int(rng.integers(0, max(1, size - int(L) - 4))) for L in lens], np.uint64)
+        if size == 0:
+            lens[:] = 0
+            offs[:] = 0
+        rel = (lens.astype(np.int64) if size else np.full(n, lcrc.NO_EXPECT, np.int64)).astype(np.int32)
+        ok = (offs + lens.astype(np.uint64) + 4 <= size) if size else np.zeros(n, bool)
+        crc = np.array([orc.mask(int(c)) for c in orc.crc_ranges(data.tobytes(), offs, lens, 1)], np.uint32) if n \
+            else np.zeros(0, np.uint32)
+        f = data.copy()
+        good = np.zeros(n, bool)
+        for i in range(n):  # store the expected value after each range unless a later range overwrote it
+            if ok[i] and rng.random() < 0.8:
+                f[int(offs[i] + lens[i]):int(offs[i] + lens[i]) + 4] = np.frombuffer(int(crc[i]).to_bytes(4, "little"),
+                                                                                       np.uint8)
+        if n > 3 and size:  # two out-of-bounds descriptors
+            offs[1], lens[1] = size + 3, 1
+            offs[2], lens[2] = size - 2, 9
+        inb = offs + lens.astype(np.uint64) <= size
+        want_crc = np.zeros(n, np.uint32)
+        if inb.any():
+            want_crc[inb] = [orc.mask(int(c)) for c in orc.crc_ranges(f.tobytes(), offs[inb], lens[inb], 1)]
+        for i in range(n):
+            slot = int(offs[i]) + int(rel[i])
+            good[i] = bool(inb[i]) and rel[i] != lcrc.NO_EXPECT and 0 <= slot and slot + 4 <= size and \
+                int.from_bytes(f[slot:slot + 4].tobytes(), "little") == int(want_crc[i])
+        want_mm = ~good if size else np.zeros(n, bool)
+        want_mm[~inb] = True
+        d = np.zeros(n, lcrc.DESC_DTYPE)
+        d["offset"], d["length"], d["expect_rel"] = offs, lens, rel
+        base = lcrc.DeviceBuffer.from_host(f if size else np.zeros(1, np.uint8))
+        dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8) if n else np.zeros(16, np.uint8))
+        out = lcrc.DeviceBuffer(max(4, 4 * n))
+        mm = lcrc.DeviceBuffer(max(4, 4 * ((n + 31) // 32)))
+        keep += [base, dd, out, mm]
+        jobs.append((base, size, dd, n, out, mm))
+        want.append((want_crc, want_mm))
+
+    def check():
+        for (base, size, dd, n, out, mm), (wc, wm) in zip(jobs, want):
+            got = out.download(np.uint32, n)
+            assert np.array_equal(got, wc), np.nonzero(got != wc)[0][:10]
+            assert lcrc.unpack_bits(mm.download(np.uint32, (n + 31) // 32), n).tolist() == wm.tolist()
+
+    # separate lcrc_batch calls first, then the queue
+    for base, size, dd, n, out, mm in jobs:
+        eng.batch(base, size, dd, n, out, mm)
+    eng.sync()
+    check()
+    for j in jobs:
+        j[4].zero()
+        j[5].upload(np.full(max(1, (j[3] + 31) // 32), 0xFFFFFFFF, np.uint32))
+    eng.batch_queue(jobs)
+    eng.sync()
+    check()
+    eng.reserve(5 << 20)
+    arr = lcrc.gjobs(jobs)
+    g = eng.graph_capture(lambda: eng.batch_queue(arr))
+    try:
+        for _ in range(2):
+            for j in jobs:
+                j[4].zero()
+            eng.graph_launch(g)
+            eng.sync()
+            check()
+    finally:
+        eng.graph_destroy(g)
+    eng.close()

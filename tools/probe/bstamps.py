@@ -25,13 +25,22 @@ for i in range(10):
 eng.sync()
 eng.batch(buf, total, dd, len(sizes), out)
 eng.sync()
-st = (ctypes.c_ulonglong * (8192 * 4))()
+st = (ctypes.c_ulonglong * (8192 * 8))()
 m.lib().lcrc_probe_bstamps(st)
-a = np.frombuffer(st, dtype=np.uint64).reshape(8192, 4).astype(np.int64)
+a = np.frombuffer(st, dtype=np.uint64).reshape(8192, 8).astype(np.int64)
 a = a[a[:, 0] != 0]
 t0 = a[:, 0].min()
 r = (a - t0) / 100.0
 print(f"k_blocks: ranges {len(sizes)}, waves {len(a)}")
-for k, name in enumerate(["entry", "tables", "first", "end"]):
+for k, name in enumerate(["entry", "tables", "it1", "it2", "it3", "it4", "it5", "end"]):
     col = r[:, k][a[:, k] != 0]
     print(f"  {name:7s} " + " ".join(f"{x:7.2f}" for x in np.percentile(col, [0, 10, 50, 90, 100])))
+# per-iteration durations (each row's range: loads, head walk, fold, tail walk, store)
+prev = a[:, 1]
+for k in range(5):
+    cur = a[:, 2 + k]
+    ok = cur != 0
+    if ok.any():
+        d = (cur[ok] - prev[ok]) / 100.0
+        print(f"  iter {k + 1} waves {ok.sum():5d} us " + " ".join(f"{x:6.2f}" for x in np.percentile(d, [10, 50, 90])))
+    prev = np.where(ok, cur, prev)
