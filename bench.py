@@ -51,6 +51,7 @@ PEAK_GBS = 8000.0  # MI355X HBM3E peak, GB/s (MI355X_MICROARCH.md chip table, sp
 NBUF = 4
 QMAX = 32  # batches per queued launch (MAX_QJOBS in lcrc_kernels.hip)
 MIXED_QUEUE = 1  # mixed config: steps per lcrc_batch_queue submission (1: one lcrc_batch per step)
+WAL_QUEUE = 1  # wal config: scans per lcrc_wal_scan_queue submission (1: one lcrc_wal_scan_async per step)
 
 
 def parse(argv=None):
@@ -431,15 +432,34 @@ def workload_wal(m, synth, engs, rank, device, args):
     if (first["status"] != 0).any():
         raise RuntimeError("wal bench: a freshly written log has a record flagged as corrupt")
 
-    def run(first_, count):  # records and their count stay on the device
-        for i in range(first_, first_ + count):
-            k = i % len(engs)
-            engs[k].wal_scan_async(dev, len(data), recs[k], maxr, counts[k])
+    q = args.queue
+    if q == 1:
+        def run(first_, count):  # records and their count stay on the device
+            for i in range(first_, first_ + count):
+                k = i % len(engs)
+                engs[k].wal_scan_async(dev, len(data), recs[k], maxr, counts[k])
+        launches = None
+        sub = f"one lcrc_wal_scan_async per step, rotated over {len(engs)} streams"
+    else:  # lcrc_wal_scan_queue: q scans per submission (header walks of all first, window passes back to back)
+        qrecs = [m.DeviceBuffer(maxr * m.WAL_REC_DTYPE.itemsize, device) for _ in range(q)]
+        qcounts = [m.DeviceBuffer(8, device) for _ in range(q)]
+
+        def run(first_, count):
+            subs = []
+            for g, (i0, n) in enumerate(groups(first_, count, q)):
+                k = g % len(engs)
+                arr = m.wjobs([(dev, len(data), qrecs[j], maxr, qcounts[j]) for j in range(n)])
+                subs.append((lambda e=engs[k], a=arr: e.wal_scan_queue(a), n, n, k))
+            return subs
+        run.prepares = True
+        launches = lambda count: count  # noqa: E731  (one window pass per step)
+        sub = f"lcrc_wal_scan_queue of {q} scans per submission ({len(engs)} stream(s) + the context's side stream)"
 
     cfg = {"workload": "WAL: 32 KiB log blocks, records n~U[1,2^k), k~U[1,16] (BASELINE configs[3])",
-           "file_bytes": int(len(data)), "records": int(len(first)), "bytes_counted": "sum(1+len)"}
+           "file_bytes": int(len(data)), "records": int(len(first)), "bytes_counted": "sum(1+len)",
+           "submission": sub}
     sample = ("ranges_raw", data, h + 6, first["length"].astype(np.uint64) + 1)
-    return Workload(run, covered, cfg, None, sample, lambda: first["crc"].copy())
+    return Workload(run, covered, cfg, launches, sample, lambda: first["crc"].copy())
 
 
 def workload_table(m, synth, engs, rank, device, args):
@@ -666,8 +686,8 @@ def main(argv=None):
     mode = m.MODE_C if args.mode == "c" else m.MODE_REF
     flags = m.FLAG_MASK if mode == m.MODE_C else 0
     if args.queue is None:
-        args.queue = MIXED_QUEUE if args.config == "mixed" else 1
-    queued = args.config in ("fixed", "mixed") and not args.host_resident and args.queue != 1
+        args.queue = {"mixed": MIXED_QUEUE, "wal": WAL_QUEUE}.get(args.config, 1)
+    queued = args.config in ("fixed", "mixed", "wal") and not args.host_resident and args.queue != 1
     nstreams = args.streams or (1 if queued else 2)
     if args.engine == "host":
         engs = []

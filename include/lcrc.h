@@ -24,10 +24,12 @@
  *                                          few blocks of a file, table.rs:114-146): cost ~ the blocks read
  *   lcrc_batch_uniform_queue            <- the same for a queue of independent batches (e.g. every table of
  *                                          a compaction's output), submitted as one launch per 32 batches
+ *   lcrc_batch_queue                    <- lcrc_batch for a queue of independent descriptor batches
  *   lcrc_batch_host_uniform             <- the same starting and ending in host memory (pinned H2D,
  *                                          kernel, D2H, double-buffered)
  *   lcrc_wal_scan / lcrc_wal_scan_async <- the header parse + CRC verify of (2) for every physical record
  *                                          of a device-resident log file, 32 KiB block by block
+ *   lcrc_wal_scan_queue                 <- the same for several log files in one submission (recovery, scrub)
  *   lcrc_tb_* + lcrc_batch_seal         <- TableBuilder (table.rs:344-529) with the trailers sealed in batch
  *   lcrc_table_scan[_async]             <- Table::open with paranoid_checks (table.rs:39-103) followed by
  *                                          read_block_from_file(verify_checksum) (format.rs:146-171) of
@@ -180,11 +182,10 @@ typedef struct lcrc_gjob {
 
 /* A queue of independent descriptor batches (jobs: HOST array of njobs), each exactly as one
  * lcrc_batch(ctx, jobs[k].base, jobs[k].base_len, jobs[k].descs, jobs[k].n, ...) call -- e.g. every SSTable
- * of a compaction's output, or the files a recovery verifies. The general path's two passes are pipelined
- * across the batches: the window pass of batch k+1 streams while the range pass of batch k finishes beside
- * it on a second stream of the context, so consecutive window passes run back to back instead of waiting
- * for each batch's latency-bound second pass. Enqueued on `stream` (the forked work joins it before the
- * call's end), graph-capturable, nothing synchronized. */
+ * of a compaction's output, or the files a recovery verifies. The batches alternate over two streams of the
+ * context, so two batches' window passes share the HBM stream while their latency-bound range passes overlap.
+ * Enqueued on `stream` (the forked work joins it before the call's end), graph-capturable (after
+ * lcrc_ctx_reserve), nothing synchronized. */
 int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* stream);
 
 /* Same as lcrc_batch_uniform but base / expected / out_crc / out_mismatch are HOST pointers. Data is
@@ -203,6 +204,22 @@ int lcrc_wal_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wa
  * *n_recs (DEVICE or pinned host memory) by the last kernel. Records past max_recs are not written. */
 int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs,
                         size_t max_recs, uint64_t* n_recs, void* stream);
+
+/* One log of a queued WAL scan (lcrc_wal_scan_queue): the arguments of one lcrc_wal_scan_async call. */
+typedef struct lcrc_wjob {
+  const uint8_t* file;   /* device */
+  uint64_t file_len;
+  lcrc_wal_rec* recs;    /* device, max_recs records */
+  uint64_t max_recs;
+  uint64_t* n_recs;      /* device or pinned host: the record count */
+} lcrc_wjob;
+
+/* Several logs scanned in one submission, each exactly as one lcrc_wal_scan_async call (jobs: HOST array) --
+ * e.g. every log file a recovery or a scrub verifies. The header walks of all the logs run first, in one
+ * launch, while the HBM stream is idle; then the logs alternate over two streams of the context as in
+ * lcrc_batch_queue. Enqueued on `stream`, nothing is synchronized, graph-capturable after a first call of the
+ * same shape (per-log workspaces are allocated on first use). */
+int lcrc_wal_scan_queue(lcrc_ctx* ctx, const lcrc_wjob* jobs, size_t njobs, void* stream);
 
 /* One block of an SSTable located by lcrc_table_scan (host struct, 24 B). */
 typedef struct lcrc_tblk {

@@ -80,6 +80,11 @@ class _GJob(ctypes.Structure):
                 ("n", ctypes.c_uint64), ("out_crc", ctypes.c_void_p), ("out_mismatch", ctypes.c_void_p)]
 
 
+class _WJob(ctypes.Structure):
+    _fields_ = [("file", ctypes.c_void_p), ("file_len", ctypes.c_uint64), ("recs", ctypes.c_void_p),
+                ("max_recs", ctypes.c_uint64), ("n_recs", ctypes.c_void_p)]
+
+
 class _Hasher(ctypes.Structure):
     _fields_ = [("state", ctypes.c_uint32), ("mode", ctypes.c_int32), ("amount", ctypes.c_uint64)]
 
@@ -91,7 +96,7 @@ ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
-    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async",
+    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
     "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_tb_create", "lcrc_tb_destroy", "lcrc_tb_add", "lcrc_tb_flush", "lcrc_tb_finish", "lcrc_tb_size",
@@ -142,6 +147,7 @@ def lib():
     sig("lcrc_batch_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, vp)
     sig("lcrc_batch_uniform_queue", i32, vp, ctypes.POINTER(_UJob), sz, u32, u64, vp)
     sig("lcrc_batch_queue", i32, vp, ctypes.POINTER(_GJob), sz, vp)
+    sig("lcrc_wal_scan_queue", i32, vp, ctypes.POINTER(_WJob), sz, vp)
     sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
     sig("lcrc_wal_scan", i32, vp, vp, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp)
     sig("lcrc_wal_scan_async", i32, vp, vp, u64, vp, sz, vp, vp)
@@ -451,6 +457,13 @@ class Engine:
         _check(lib().lcrc_wal_scan_async(self.ctx, _ptr(file_dev), int(file_len), _ptr(recs_dev), int(max_recs),
                                          _ptr(count_dev), stream), "lcrc_wal_scan_async")
 
+    def wal_scan_queue(self, jobs, stream=None):
+        """lcrc_wal_scan_queue: jobs = [(file_dev, file_len, recs_dev, max_recs, count_dev)] (or the array wjobs()
+        made of them), each one lcrc_wal_scan_async; the header walks of all the logs first, then the window
+        passes back to back with each log's range pass beside the next one."""
+        arr = jobs if isinstance(jobs, WJobs) else wjobs(jobs)
+        _check(lib().lcrc_wal_scan_queue(self.ctx, arr.arr, arr.n, stream), "lcrc_wal_scan_queue")
+
     def wal_scan_device(self, file_dev, file_len, recs_dev, max_recs):
         """lcrc_wal_scan leaving the records on the device (recs_dev); returns the record count."""
         n = ctypes.c_size_t(0)
@@ -642,6 +655,21 @@ class GJobs:
 
 def gjobs(jobs):
     return GJobs(jobs)
+
+
+class WJobs:
+    """A prepared lcrc_wjob array (lcrc_wal_scan_queue's logs, built once, submitted any number of times)."""
+
+    def __init__(self, jobs):
+        self.n = len(jobs)
+        self.arr = (_WJob * max(1, self.n))()
+        self.keep = list(jobs)
+        for k, j in enumerate(jobs):
+            self.arr[k] = _WJob(_ptr(j[0]), int(j[1]), _ptr(j[2]), int(j[3]), _ptr(j[4]))
+
+
+def wjobs(jobs):
+    return WJobs(jobs)
 
 
 def unpack_bits(words, n):

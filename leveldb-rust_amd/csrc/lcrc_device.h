@@ -64,6 +64,22 @@ struct lcrc_qjob_host {
   uint64_t nblk;
 };
 
+// One log of a queued WAL scan as the launcher receives it (its workspace and outputs).
+struct lcrc_wjob_dev_host {
+  const uint8_t* file;
+  uint64_t file_len, nblocks;
+  uint32_t* counts;
+  uint2* slots;
+  uint8_t* stops;
+  uint32_t* local;
+  uint64_t* part;
+  lcrc_wal_rec_dev* recs;
+  lcrc_desc_dev* descs;
+  uint64_t max_recs;
+  uint64_t* n_total;
+  uint64_t* n_out;
+};
+
 // State of an asynchronous whole-table scan (lcrc_table_scan_async), in device memory.
 struct lcrc_tscan_dev {
   uint32_t status;  // LCRC_TSCAN_* of include/lcrc.h: 0 ok, 1 corrupt (`code`), 2 host walk needed, 3 capacity

@@ -1106,6 +1106,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long b_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long b_it[5] = {0, 0, 0, 0, 0};
+  unsigned long long b_ph[4] = {0, 0, 0, 0};  // first iteration: loads landed, head walked, folded, tail walked
   uint32_t b_nit = 0;
 #endif
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
@@ -1212,10 +1213,22 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int j = 0; j < B_BATCH; ++j) vals[j] = ((uint32_t)j < rounds && 16u * j + g > npad) ? wv[16 * j] : 0u;
 
+#ifdef LCRC_PROBE_PHASES
+      if (b_nit == 0) {
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        b_ph[0] = __builtin_amdgcn_s_memrealtime();
+      }
+#endif
 #if defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 2  // ablation: no head/tail walks (wrong CRCs)
       const uint32_t head = ph.w[0] ^ ph.w[1] ^ pt.w[2];
 #else
       const uint32_t head = row_walk(L, ph, s == head_end, init, g, lane);
+#endif
+#ifdef LCRC_PROBE_PHASES
+      if (b_nit == 0) {
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::"v"(head) : "memory");
+        b_ph[1] = __builtin_amdgcn_s_memrealtime();
+      }
 #endif
       uint32_t a = 0;
       for (uint32_t q0 = 0; q0 < rmax; q0 += B_BATCH) {
@@ -1242,10 +1255,22 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       }
 #endif
       const uint32_t mid = row_bcast0(a, lane);
+#ifdef LCRC_PROBE_PHASES
+      if (b_nit == 0) {
+        __asm__ volatile("" ::"v"(mid));
+        b_ph[2] = __builtin_amdgcn_s_memrealtime();
+      }
+#endif
       acc = single ? head : mid;
       // tail: the partial last window, walked from the folded value
 #if !(defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 2)
       acc = row_walk(L, pt, ta == e, acc, g, lane);
+#endif
+#ifdef LCRC_PROBE_PHASES
+      if (b_nit == 0) {
+        __asm__ volatile("" ::"v"(acc));
+        b_ph[3] = __builtin_amdgcn_s_memrealtime();
+      }
 #endif
     } else {
       // direct: walk the whole range in 256 B chunks (sparse batches)
@@ -1293,6 +1318,9 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
     lcrc_dbg_bstamp[gw * 8 + 0] = b_entry;
     lcrc_dbg_bstamp[gw * 8 + 1] = b_tab;
     for (int k = 0; k < 5; ++k) lcrc_dbg_bstamp[gw * 8 + 2 + k] = b_it[k];
+#ifdef LCRC_PROBE_PHASES
+    for (int k = 0; k < 4; ++k) lcrc_dbg_bstamp[gw * 8 + 3 + k] = b_ph[k];  // over it2..it5
+#endif
     lcrc_dbg_bstamp[gw * 8 + 7] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
@@ -1663,12 +1691,13 @@ constexpr uint32_t WAL_PARTB = 64;  // blocks per parse workgroup (= per part to
 #endif
 
 template <uint32_t WIN>
-__global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                  uint64_t nblocks, uint32_t* __restrict__ counts,
-                                                  uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                                  uint32_t* __restrict__ local, uint64_t* __restrict__ part) {
+__device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file, uint64_t file_len,
+                                               uint64_t nblocks, uint32_t* __restrict__ counts,
+                                               uint2* __restrict__ slots, uint8_t* __restrict__ stops,
+                                               uint32_t* __restrict__ local, uint64_t* __restrict__ part,
+                                               uint32_t bx) {
   __shared__ u32x4 wwin[WIN ? 64 * (WIN / 16) : 1];
-  const uint64_t b = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint64_t b = (uint64_t)bx * 64 + threadIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint8_t* blk = file + b * 32768ull;
   const uint64_t rem = b < nblocks ? file_len - b * 32768ull : 0;
@@ -1747,7 +1776,42 @@ __global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ fi
     stops[b] = (uint8_t)stop;
     local[b] = inc - nrec;
   }
-  if (lane == 63) part[blockIdx.x] = inc;
+  if (lane == 63) part[bx] = inc;
+}
+
+template <uint32_t WIN>
+__global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                  uint64_t nblocks, uint32_t* __restrict__ counts,
+                                                  uint2* __restrict__ slots, uint8_t* __restrict__ stops,
+                                                  uint32_t* __restrict__ local, uint64_t* __restrict__ part) {
+  wal_parse_body<WIN>(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x);
+}
+
+// several logs in one launch (lcrc_wal_scan_queue): log blockIdx.y, its parse workgroups blockIdx.x
+struct WalJobDev {
+  const uint8_t* file;
+  uint64_t file_len, nblocks;
+  uint32_t* counts;
+  uint2* slots;
+  uint8_t* stops;
+  uint32_t* local;
+  uint64_t* part;
+  lcrc_wal_rec_dev* recs;
+  lcrc_desc_dev* descs;
+  uint64_t max_recs;
+  uint64_t* n_total;
+  uint64_t* n_out;
+};
+constexpr int MAX_WJOBS = 16;  // logs per launch (kernel-argument space: 16 x 104 B)
+struct WalJobsArg {
+  WalJobDev j[MAX_WJOBS];
+};
+
+template <uint32_t WIN>
+__global__ void __launch_bounds__(64) k_wal_parse_q(const WalJobsArg jobs) {
+  const WalJobDev& J = jobs.j[blockIdx.y];
+  if ((uint64_t)blockIdx.x * WAL_PARTB >= J.nblocks) return;  // past this log's blocks (workgroup-uniform)
+  wal_parse_body<WIN>(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
 }
 
 __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcrc_desc_dev* __restrict__ descs,
@@ -1773,24 +1837,25 @@ __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcr
 // of the last slot re-walks a block that has more records than slots. first(b) = the parse workgroups'
 // totals before b's workgroup (summed by each emit workgroup) + local[b]. Workgroup 0 also writes the total
 // record count to n_total (device) and n_out (device or pinned host memory).
-__global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ file, uint64_t nblocks,
-                                                  const uint32_t* __restrict__ counts,
-                                                  const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
-                                                  const uint32_t* __restrict__ local,
-                                                  const uint64_t* __restrict__ part,
-                                                  lcrc_wal_rec_dev* __restrict__ recs,
-                                                  lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
-                                                  uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out) {
+__device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, uint64_t nblocks,
+                                              const uint32_t* __restrict__ counts,
+                                              const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
+                                              const uint32_t* __restrict__ local,
+                                              const uint64_t* __restrict__ part,
+                                              lcrc_wal_rec_dev* __restrict__ recs,
+                                              lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
+                                              uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
+                                              uint32_t bx) {
   __shared__ uint64_t red[256];
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t g = (uint64_t)bx * blockDim.x + threadIdx.x;
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
   const uint64_t nparts = (nblocks + WAL_PARTB - 1) / WAL_PARTB;
   // sum of the parse workgroups' totals before this workgroup's blocks (all of them for workgroup 0's
   // total); 256 / WAL_SLOTS divides WAL_PARTB, so one parse workgroup covers every block here
   static_assert(WAL_PARTB % (256 / WAL_SLOTS) == 0, "an emit workgroup's blocks lie in one part");
-  const uint64_t upto = blockIdx.x == 0 ? nparts : ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / WAL_PARTB;
-  const uint64_t mine = ((uint64_t)blockIdx.x * 256 / WAL_SLOTS) / WAL_PARTB;
+  const uint64_t upto = bx == 0 ? nparts : ((uint64_t)bx * 256 / WAL_SLOTS) / WAL_PARTB;
+  const uint64_t mine = ((uint64_t)bx * 256 / WAL_SLOTS) / WAL_PARTB;
   uint64_t acc = 0, accm = 0;
   for (uint64_t w = threadIdx.x; w < upto; w += 256) {
     acc += part[w];
@@ -1811,7 +1876,7 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
     __syncthreads();
   }
   const uint64_t base = red[0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bx == 0 && threadIdx.x == 0) {
     *n_total = total_upto;
     if (n_out) *n_out = total_upto;
   }
@@ -1833,6 +1898,25 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
       if (oj < max_recs) wal_put(recs, descs, oj, b * 32768ull + at, length, type, j + 1 == cnt, stops[b]);
     }
   }
+}
+
+__global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ file, uint64_t nblocks,
+                                                  const uint32_t* __restrict__ counts,
+                                                  const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
+                                                  const uint32_t* __restrict__ local,
+                                                  const uint64_t* __restrict__ part,
+                                                  lcrc_wal_rec_dev* __restrict__ recs,
+                                                  lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
+                                                  uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out) {
+  wal_emit_body(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
+  const WalJobDev& J = jobs.j[blockIdx.y];
+  // past this log's (block, slot) threads: workgroup 0 always runs (it writes the total)
+  if (blockIdx.x && (uint64_t)blockIdx.x * 256 >= J.nblocks * WAL_SLOTS) return;
+  wal_emit_body(J.file, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, J.recs, J.descs, J.max_recs, J.n_total,
+                J.n_out, blockIdx.x);
 }
 
 
@@ -3089,6 +3173,26 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
   const uint64_t g = (nt + 255) / 256;
   hipLaunchKernelGGL(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
                      stops, local, part, recs, descs, max_recs, n_total, n_out);
+  return hipGetLastError();
+}
+
+// several logs' header walks and record emits, two launches (lcrc_wal_scan_queue); m <= MAX_WJOBS
+hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t m, hipStream_t st) {
+  using lcrc_dev::WalJobsArg;
+  if (m == 0) return hipSuccess;
+  if (m > (uint32_t)lcrc_dev::MAX_WJOBS) return hipErrorInvalidValue;
+  WalJobsArg a;
+  memset(&a, 0, sizeof(a));
+  uint64_t gp = 1, ge = 1;
+  for (uint32_t k = 0; k < m; ++k) {
+    const lcrc_wjob_dev_host& j = jobs[k];
+    a.j[k] = lcrc_dev::WalJobDev{j.file, j.file_len, j.nblocks, j.counts, j.slots, j.stops, j.local, j.part,
+                                 j.recs, j.descs, j.max_recs, j.n_total, j.n_out};
+    gp = std::max<uint64_t>(gp, (j.nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB);
+    ge = std::max<uint64_t>(ge, (j.nblocks * lcrc_dev::WAL_SLOTS + 255) / 256);
+  }
+  hipLaunchKernelGGL(lcrc_dev::k_wal_parse_q<LCRC_WAL_WIN>, dim3((unsigned)gp, m), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(lcrc_dev::k_wal_emit_q, dim3((unsigned)ge, m), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

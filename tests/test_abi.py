@@ -39,6 +39,7 @@ def test_struct_layouts(lcrc):
     import ctypes
     assert ctypes.sizeof(lcrc._GJob) == 48 and lcrc._GJob.out_mismatch.offset == 40  # lcrc_gjob
     assert ctypes.sizeof(lcrc._UJob) == 40  # lcrc_ujob
+    assert ctypes.sizeof(lcrc._WJob) == 40 and lcrc._WJob.n_recs.offset == 32  # lcrc_wjob
 
 
 @pytest.mark.parametrize("n", [0, 1, 3, 7, 8, 9, 16, 100, 4096, 100003])
@@ -86,6 +87,7 @@ def test_batched_api_fails_loudly_without_device(lcrc):
         lcrc.Engine(0, lcrc.MODE_C)
     assert lcrc.lib().lcrc_batch(None, None, 0, None, 0, None, None, None) == lcrc.EINVAL
     assert lcrc.lib().lcrc_batch_queue(None, None, 0, None) == lcrc.EINVAL
+    assert lcrc.lib().lcrc_wal_scan_queue(None, None, 0, None) == lcrc.EINVAL
 
 
 def test_scalar_extend_every_length_and_register(lcrc, orc):

@@ -675,3 +675,60 @@ def test_general_queue_matches_batches(lcrc, orc, path, monkeypatch):
     finally:
         eng.graph_destroy(g)
     eng.close()
+
+
+def test_wal_scan_queue_matches_single_scans(lcrc, orc, engines):
+    """lcrc_wal_scan_queue: 5 logs (different sizes, one empty, one with corrupted records, one whose last block
+    is partial, one with max_recs 0) in one submission -- header walks in one launch, records in one more, window
+    passes back to back, range passes on the side stream -- give exactly the records, verdicts and counts of 5
+    separate lcrc_wal_scan_async calls; then the queue again in a HIP graph."""
+    rng = np.random.default_rng(0xA11)
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    logs = []
+    for k, nrec in enumerate([300, 0, 900, 40, 200]):
+        recs = [rng.integers(0, 256, int(rng.integers(0, 1 << int(rng.integers(1, 16)))), dtype=np.uint8).tobytes()
+                for _ in range(nrec)]
+        log = bytearray(orc.log_write(recs))
+        if k == 2:
+            for pos in rng.integers(0, len(log), 6):
+                log[int(pos)] ^= 0x5A
+        if k == 3:
+            log = log[:len(log) - 1000] if len(log) > 5000 else log
+        logs.append(bytes(log))
+    jobs, want = [], []
+    for k, log in enumerate(logs):
+        dev = lcrc.DeviceBuffer.from_host(np.frombuffer(log, np.uint8) if log else np.zeros(1, np.uint8))
+        cap = 0 if k == 4 else len(log) // 7 + 1
+        rd = lcrc.DeviceBuffer(max(1, cap) * lcrc.WAL_REC_DTYPE.itemsize)
+        cnt = lcrc.DeviceBuffer(8)
+        eng.wal_scan_async(dev, len(log), rd, cap, cnt)
+        eng.sync()
+        n = int(cnt.download(np.uint64, 1)[0])
+        want.append((n, rd.download(lcrc.WAL_REC_DTYPE, min(n, cap)).tobytes() if cap else b""))
+        jobs.append((dev, len(log), rd, cap, cnt))
+
+    def check():
+        for (dev, flen, rd, cap, cnt), (n, recs) in zip(jobs, want):
+            assert int(cnt.download(np.uint64, 1)[0]) == n
+            if cap:
+                assert rd.download(lcrc.WAL_REC_DTYPE, min(n, cap)).tobytes() == recs
+
+    for j in jobs:
+        j[2].zero()
+        j[4].zero()
+    eng.wal_scan_queue(jobs)
+    eng.sync()
+    check()
+    arr = lcrc.wjobs(jobs)
+    g = eng.graph_capture(lambda: eng.wal_scan_queue(arr))
+    try:
+        for _ in range(2):
+            for j in jobs:
+                j[2].zero()
+                j[4].zero()
+            eng.graph_launch(g)
+            eng.sync()
+            check()
+    finally:
+        eng.graph_destroy(g)
+    eng.close()

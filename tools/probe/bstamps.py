@@ -44,3 +44,14 @@ for k in range(5):
         d = (cur[ok] - prev[ok]) / 100.0
         print(f"  iter {k + 1} waves {ok.sum():5d} us " + " ".join(f"{x:6.2f}" for x in np.percentile(d, [10, 50, 90])))
     prev = np.where(ok, cur, prev)
+if os.environ.get("PHASES"):
+    # LCRC_PROBE_PHASES build: first iteration's phase ends in columns 3..6 (loads, head, fold, tail), 2 = end
+    ph = a[:, 3:7]
+    ok = (ph != 0).all(1)
+    prev = a[ok, 1]
+    for k, name in enumerate(["loads", "head walk", "fold", "tail walk"]):
+        d = (ph[ok, k] - prev) / 100.0
+        print(f"  phase {name:10s} us " + " ".join(f"{x:6.2f}" for x in np.percentile(d, [10, 50, 90])))
+        prev = ph[ok, k]
+    d = (a[ok, 2] - prev) / 100.0
+    print(f"  phase {'store':10s} us " + " ".join(f"{x:6.2f}" for x in np.percentile(d, [10, 50, 90])))
