@@ -28,7 +28,7 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* gtab, uint32_t x4096, uint32_t poly,
                               uint32_t init, uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
-                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st);
+                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st, uint32_t rows_per_wg = 32);
 hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
                                      uint32_t fin, uint32_t flags, hipStream_t st, hipEvent_t t_start,
                                      hipEvent_t t_stop);
@@ -436,12 +436,13 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
   int rc = set_device(ctx);
   if (rc) return rc;
   hipStream_t st = pick_stream(ctx, stream);
-  if (out_mismatch && n) HIPCHK(hipMemsetAsync(out_mismatch, 0, ((n + 31) / 32) * sizeof(uint32_t), st));
   if (n == 0) return LCRC_OK;
+  // no fill of out_mismatch: every range sets or clears its own bit (LCRC_KFLAG_SETCLR)
+  const uint32_t kflags = (ctx->flags & LCRC_FLAG_MASK) | LCRC_KFLAG_SETCLR;
   const bool direct = (ctx->flags & LCRC_FLAG_DIRECT) != 0;
   if (!direct && ctx->general == 1) {
     HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr,
-                              ctx->d_tab, ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
+                              ctx->d_tab, ctx->x4096, ctx->poly, ctx->init, ctx->xorout, kflags,
                               out_crc, out_mismatch, nullptr, nullptr, st));
     return LCRC_OK;
   }
@@ -453,7 +454,7 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
     win = ctx->win.p;
   }
   HIPCHK(lcrc_launch_blocks(false, std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU), base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
-                            ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK, out_crc,
+                            ctx->d_tab, ctx->init, ctx->xorout, kflags, out_crc,
                             out_mismatch, nullptr, nullptr, st));
   return LCRC_OK;
 }
@@ -494,13 +495,13 @@ int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* s
   for (size_t k = 0; k < njobs; ++k) {
     const lcrc_gjob& j = jobs[k];
     const int b = (int)(k & 1);
-    if (j.out_mismatch && j.n) HIPCHK(hipMemsetAsync(j.out_mismatch, 0, ((j.n + 31) / 32) * sizeof(uint32_t), lane[b]));
     if (j.n && j.base_len)
       HIPCHK(lcrc_launch_windows(false, ctx->grid_a, j.base, j.base_len, ctx->d_tab, wins[b], 0, 0, 0, nullptr,
                                  nullptr, lane[b]));
     HIPCHK(lcrc_launch_blocks(false, grid_b, j.base, j.base_len, (const lcrc_desc_dev*)j.descs, j.n, 0, 0, nullptr,
                               j.base_len ? wins[b] : nullptr, ctx->d_tab, ctx->init, ctx->xorout,
-                              ctx->flags & LCRC_FLAG_MASK, j.out_crc, j.out_mismatch, nullptr, nullptr, lane[b]));
+                              (ctx->flags & LCRC_FLAG_MASK) | LCRC_KFLAG_SETCLR, j.out_crc, j.out_mismatch, nullptr,
+                              nullptr, lane[b]));
   }
   return lanes_join(ctx, st);
 }
@@ -514,11 +515,13 @@ int lcrc_batch_covered(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, co
   int rc = set_device(ctx);
   if (rc) return rc;
   hipStream_t st = pick_stream(ctx, stream);
-  if (out_mismatch && n) HIPCHK(hipMemsetAsync(out_mismatch, 0, ((n + 31) / 32) * sizeof(uint32_t), st));
   if (n == 0) return LCRC_OK;
+  // a few ranges: one wave's four rows per workgroup, so the walks spread over the CUs instead of sharing a
+  // few CUs' VALU and LDS eight waves apiece
   HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr,
-                            ctx->d_tab, ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
-                            out_crc, out_mismatch, nullptr, nullptr, st));
+                            ctx->d_tab, ctx->x4096, ctx->poly, ctx->init, ctx->xorout,
+                            (ctx->flags & LCRC_FLAG_MASK) | LCRC_KFLAG_SETCLR, out_crc, out_mismatch, nullptr, nullptr,
+                            st, 4));
   return LCRC_OK;
 }
 

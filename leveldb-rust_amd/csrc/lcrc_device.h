@@ -9,6 +9,9 @@
 #ifndef LCRC_FLAG_MASK
 #define LCRC_FLAG_MASK 0x1u
 #endif
+// kernel-only flag (k_blocks, k_ranges): the mismatch bitmap was NOT zeroed before the launch -- every range
+// sets or clears its own bit, and the last range clears the bits past n in the last word (no fill kernel)
+#define LCRC_KFLAG_SETCLR 0x100u
 
 // Per-mode constant table image (uint32 words), uploaded once per context.
 enum : int {

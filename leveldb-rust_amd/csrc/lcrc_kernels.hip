@@ -1090,6 +1090,21 @@ __device__ __forceinline__ uint32_t load_le32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// range i's mismatch bit. Zeroed bitmap: set the bad ones. LCRC_KFLAG_SETCLR (no fill before the launch):
+// every range sets or clears its own bit, and range n - 1 also clears the bits past it in the last word
+// (one thread's atomics to one word stay in order).
+__device__ __forceinline__ void mismatch_bit(uint32_t* __restrict__ mm, uint64_t i, uint64_t n, bool bad,
+                                             uint32_t flags) {
+  const uint32_t bit = 1u << (i & 31);
+  if (!(flags & LCRC_KFLAG_SETCLR)) {
+    if (bad) atomicOr(&mm[i >> 5], bit);
+    return;
+  }
+  if (bad) atomicOr(&mm[i >> 5], bit);
+  else atomicAnd(&mm[i >> 5], ~bit);
+  if (i + 1 == n && bit != 0x80000000u) atomicAnd(&mm[i >> 5], (bit << 1) - 1u);
+}
+
 // waves_per_eu(8): 64 VGPRs and few enough SGPRs for 8 waves per SIMD (at 97 SGPRs only 6 fit, so a
 // quarter of the 4 x 512-thread workgroups per CU started only when others had finished)
 template <bool UNIFORM>
@@ -1302,7 +1317,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       } else if (xrel != LCRC_NO_EXPECT_DEV) {
         bad = bad || !exp_ok || expv != crc;
       }
-      if (bad && mismatch) atomicOr(&mismatch[i >> 5], 1u << (i & 31));
+      if (mismatch) mismatch_bit(mismatch, i, n, bad, flags);
       if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
         recs[i].crc = crc;
         recs[i].status = bad ? 1 : 0;
@@ -1389,16 +1404,46 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
   const uint32_t* __restrict__ xch = inv + 4097;  // x^(8 * 4096 * k) mod P, k < R_KMAX
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan, async table scan)
   if (blockIdx.x >= n) return;  // a grid sized by a bound: no range is dealt to this workgroup
+  // A row's first range is its own ticket (the row index), and rows claim no shared chunk before they have
+  // taken it: its descriptor is loaded, and then its first chunk, while the LDS image is built.
+  const uint32_t row_wg = tid >> 4;
+  const uint64_t i_first = blockIdx.x + (uint64_t)row_wg * gridDim.x;
+  lcrc_desc_dev d_first{0, 0, LCRC_NO_EXPECT_DEV};
+  if (!UNIFORM && i_first < n) d_first = descs[i_first];
+  bool fresh = true, pre = true;
+  const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
+  u32x4 va[8], vb[8];
+  {
+    // the first chunk's start and limit exactly as the loop derives them below
+    uint64_t s0 = UNIFORM ? i_first * ustride : d_first.offset;
+    uint32_t len0 = UNIFORM ? ulen : d_first.length;
+    if (!UNIFORM && (s0 > base_len || len0 > base_len - s0)) s0 = len0 = 0;
+    const uint32_t d40 = (uint32_t)(s0 & 3);
+    const uint32_t span0 = len0 + d40;
+    const bool ovf0 = span0 > 4096 && span0 <= 4096 + R_OVF;
+    const uint64_t ce0 = ovf0 ? s0 - d40 + 4096 : s0 + len0;
+    const uint64_t lim = i_first < n ? (ce0 < base_len ? ce0 : base_len) : 0;
+    const uint64_t csl = i_first < n ? s0 - d40 : 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t B = readlane64(csl, 16 * (j >> 1)) + 2048u * (j & 1);
+      const uint64_t lq = readlane64(lim, 16 * (j >> 1));
+      const uint32_t nrec = lq > B ? (lq - B < 2048 ? (uint32_t)(lq - B) : 2048u) : 0u;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(base + (nrec ? B : 0)), (short)0, (int)nrec, 0x00020000);
+      va[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_a, 0, LCRC_LOAD_AUX);
+      vb[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_b, 0, LCRC_LOAD_AUX);
+    }
+  }
   build_tables(L, gtab, wv, lane);
   if (tid < R_SLOTS) sl_gen[tid] = 0;
   if (tid == 0) {
-    ticket = 0;
+    ticket = A_THREADS / 16;
     work_mask = 0;
     free_mask = ~0u >> (32 - R_SLOTS);
   }
   lds_barrier();
   const Rot R = make_rot(lane);
-  const uint32_t voff_a = 256u * (lane & 7) + 16u * (lane >> 3), voff_b = voff_a + 128;
   const __amdgpu_buffer_rsrc_t no_rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0, 0x00020000);
   // per-row state, uniform within the 16-lane row. mode 0: looking for work, 1: a private range (chunks
   // walked in order by this row), 2: one chunk of shared range `sl`.
@@ -1412,7 +1457,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
     // 1. rows without work claim a chunk of a shared range ...
     const bool need = mode == 0 && !done;
     uint32_t got = R_SLOTS, gc = 0;
-    if (need && g == 0) {
+    if (need && !fresh && g == 0) {
       uint32_t m = *(volatile uint32_t*)&work_mask;
       while (m) {
         const uint32_t s = __builtin_ctz(m);
@@ -1442,8 +1487,10 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
     // ... or take the next range
     const bool need2 = need && got >= R_SLOTS;
     uint32_t v = 0;
-    if (need2 && g == 0) v = atomicAdd(&ticket, 1u);
-    v = row_bcast0(v, lane);
+    const bool use_first = need2 && fresh;
+    if (need2 && !fresh && g == 0) v = atomicAdd(&ticket, 1u);
+    v = use_first ? row_wg : row_bcast0(v, lane);
+    if (need2) fresh = false;
     if (need2) {
       const uint64_t i = blockIdx.x + (uint64_t)v * gridDim.x;
       if (i >= n) {
@@ -1457,7 +1504,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
           s = i * ustride;
           len = ulen;
         } else {
-          const lcrc_desc_dev d = descs[i];
+          const lcrc_desc_dev d = use_first ? d_first : descs[i];
           s = d.offset;
           len = d.length;
           xrel = d.expect_rel;
@@ -1555,7 +1602,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
     // 2. the rows' chunks; bytes past the range (or the buffer) end read as zeros
     const uint64_t lim = act ? (ce < base_len ? ce : base_len) : 0;
     const uint64_t csl = act ? cs : 0;
-    u32x4 va[8], vb[8];
+    if (!pre)  // (the first iteration's chunks were loaded before the tables)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint64_t B = readlane64(csl, 16 * (j >> 1)) + 2048u * (j & 1);
@@ -1580,6 +1627,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
         }
       }
     }
+    pre = false;
     const uint32_t x = walk_half<false, false, false>(L, R, va, 0u, no_rs, voff_a);
     uint32_t p = walk_half<false>(L, R, vb, x, no_rs, voff_b);
     p = tree_level<0>(L, R, p, lane);
@@ -1625,7 +1673,9 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
     if (shr) mode = 0;
     // 4. finish: register = acc * x^(-8 pad) ^ walk(0, V)
     if (__builtin_amdgcn_ballot_w64(fin && g == 0)) {
-      uint32_t raw = gf_mul(padinv, acc, poly);
+      uint32_t raw = acc;
+      // x^0 (reflected: bit 31) when the range fills its chunks exactly or runs on past one full chunk
+      if (__builtin_amdgcn_ballot_w64(fin && g == 0 && padinv != 0x80000000u)) raw = gf_mul(padinv, acc, poly);
       // slice table T_t at LDS byte 256 * entry + 32 * t (set S0, replica 0)
       if (ovf) {  // walk on over the dwords and bytes past the full chunk
         for (uint32_t k = 0; k < ovn; ++k) {
@@ -1645,7 +1695,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
         if (oob) crc = 0;
         out[rng] = crc;
         const bool bad = oob || (has_exp && (!exp_ok || expv != crc));
-        if (bad && mismatch) atomicOr(&mismatch[rng >> 5], 1u << (rng & 31));
+        if (mismatch) mismatch_bit(mismatch, rng, n, bad, flags);
         if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
           recs[rng].crc = crc;
           recs[rng].status = bad ? 1 : 0;
@@ -3143,10 +3193,10 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
                               const uint32_t* uexp, const uint32_t* gtab, uint32_t x4096, uint32_t poly,
                               uint32_t init, uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
-                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st) {
+                              const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st, uint32_t rows_per_wg) {
   if (n == 0) return hipSuccess;
   grid *= lcrc_dev::R_WG_PER_CU;
-  const uint64_t per_wg = lcrc_dev::A_THREADS / 16;  // rows per workgroup
+  const uint64_t per_wg = rows_per_wg;  // ranges dealt per workgroup in the first round (32 rows: all of them)
   const uint64_t need = (n + per_wg - 1) / per_wg;
   const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   const uint32_t* inv = gtab + TAB_INV;

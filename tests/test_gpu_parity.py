@@ -433,6 +433,46 @@ def test_out_of_bounds_descriptors(lcrc, orc, path, monkeypatch):
     eng.close()
 
 
+@pytest.mark.parametrize("path", ["ranges", "blocks", "covered", "direct"])
+def test_mismatch_bitmap_not_prefilled(lcrc, orc, path, monkeypatch):
+    """lcrc_batch / lcrc_batch_covered fill no bitmap before the kernel: every range sets or clears its own
+    bit and the last range clears the bits past n. A bitmap full of ones comes back exact (bad ranges only,
+    zero past n) and the word after it is untouched, twice in a row."""
+    if path in ("ranges", "blocks"):
+        monkeypatch.setenv("LCRC_GENERAL", path)
+    rng = np.random.default_rng(77)
+    for n in (77, 64, 1):
+        # ranges back to back, each followed by its 4-byte expected slot; ~70 % hold the right CRC
+        lens = rng.integers(1, 9000, n).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens.astype(np.uint64) + 4)[:-1] + 3  # unaligned starts
+        host = np.frombuffer(bytes(orc.splitmix_bytes(0xB17 + n, int(offs[-1]) + int(lens[-1]) + 8)), np.uint8).copy()
+        want_crc = orc.crc_ranges(host.tobytes(), offs, lens, 1)
+        want_bad = rng.random(n) < 0.3
+        for o, L, c, b in zip(offs, lens, want_crc, want_bad):
+            v = int(c) ^ (1 if b else 0)
+            host[int(o) + int(L):int(o) + int(L) + 4] = np.frombuffer(v.to_bytes(4, "little"), np.uint8)
+        d = np.zeros(n, lcrc.DESC_DTYPE)
+        d["offset"], d["length"], d["expect_rel"] = offs, lens, lens.astype(np.int64)
+        eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_DIRECT if path == "direct" else 0)
+        base = lcrc.DeviceBuffer.from_host(host)
+        dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8))
+        words = (n + 31) // 32
+        out, mm = lcrc.DeviceBuffer(4 * n), lcrc.DeviceBuffer(4 * (words + 1))
+        for _ in range(2):
+            mm.upload(np.full(words + 1, 0xFFFFFFFF, np.uint32).view(np.uint8))
+            eng.batch(base, len(host), dd, n, out, mm, covered=int(lens.sum()) if path == "covered" else None)
+            eng.sync()
+            assert np.array_equal(out.download(np.uint32, n), want_crc)
+            got = mm.download(np.uint32, words + 1)
+            assert got[words] == 0xFFFFFFFF
+            want_words = np.zeros(words, np.uint32)
+            for i in np.nonzero(want_bad)[0]:
+                want_words[i >> 5] |= np.uint32(1 << (i & 31))
+            assert np.array_equal(got[:words], want_words), (n, got[:words], want_words)
+        eng.close()
+
+
 # ---- round 2: BASELINE configs[2] at full size, the queue API, unaligned bases, large logs ------------------
 @pytest.mark.parametrize("path", ["blocks", "ranges"])
 def test_config3_mixed_sstable_full_size(lcrc, orc, synth, path, monkeypatch):
