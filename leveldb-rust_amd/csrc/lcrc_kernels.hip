@@ -1260,15 +1260,19 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
           if (q < rounds) a = zl(L, KL_Z4096, a) ^ (16u * q + g == npad ? head : vals[j]);
         }
       }
+      // (a wave whose four ranges each lie in one window -- short WAL records -- skips the row tree and
+      // the tail walk: both are wave-uniform decisions)
+      if (rmax) {
 #ifdef LCRC_KB_TREE4
-      a = row_join4(L, a, g, KL_WA, KL_WB);
+        a = row_join4(L, a, g, KL_WA, KL_WB);
 #else
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const uint32_t pn = row_down(a, m);
-        if ((g & ((2u << m) - 1)) == 0) a = zl(L, TAB_ZWIN + m * 1024, a) ^ pn;
-      }
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t pn = row_down(a, m);
+          if ((g & ((2u << m) - 1)) == 0) a = zl(L, TAB_ZWIN + m * 1024, a) ^ pn;
+        }
 #endif
+      }
       const uint32_t mid = row_bcast0(a, lane);
 #ifdef LCRC_PROBE_PHASES
       if (b_nit == 0) {
@@ -1279,7 +1283,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       acc = single ? head : mid;
       // tail: the partial last window, walked from the folded value
 #if !(defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 2)
-      acc = row_walk(L, pt, ta == e, acc, g, lane);
+      if (__builtin_amdgcn_ballot_w64(ta != e)) acc = row_walk(L, pt, ta == e, acc, g, lane);
 #endif
 #ifdef LCRC_PROBE_PHASES
       if (b_nit == 0) {
