@@ -53,7 +53,7 @@ hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint6
                               uint32_t xorout, uint32_t flags, uint32_t* out, uint32_t* mismatch,
                               const uint64_t* n_dev, lcrc_wal_rec_dev* recs, hipStream_t st);
 hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
-                                 uint2* slots, uint8_t* stops, uint32_t* local, uint64_t* part,
+                                 uint2* slots, uint8_t* stops, uint64_t* local, uint64_t* part,
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t m, hipStream_t st);
@@ -709,21 +709,23 @@ int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32
 int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs, size_t max_recs,
                         uint64_t* n_recs, void* stream) {
   if (!ctx || !n_recs || (file_len && !file) || (max_recs && !recs)) return LCRC_EINVAL;
+  if (file_len >= LCRC_WAL_MAX_FILE) return LCRC_EINVAL;  // record indices and counts are 32-bit on the device
   int rc = set_device(ctx);
   if (rc) return rc;
   hipStream_t st = pick_stream(ctx, stream);
   const uint64_t nblocks = (file_len + 32767) / 32768;
-  // wal_offsets: [0] the total, then per block the in-workgroup offset (u32) and per 64 blocks a total
+  // wal_offsets: [0] the total, then per block the in-workgroup offsets and per 64 blocks the totals, as packed
+  // (records | one-window records << 32) counts
   if ((rc = ctx->wal_counts.ensure(nblocks + 1)) || (rc = ctx->wal_slots.ensure(nblocks * 64 + 1)) ||
       (rc = ctx->wal_stops.ensure(nblocks + 1)) ||
-      (rc = ctx->wal_offsets.ensure(1 + (nblocks + 1) / 2 + (nblocks + 63) / 64 + 1)))
+      (rc = ctx->wal_offsets.ensure(1 + nblocks + (nblocks + 63) / 64 + 1)))
     return rc;
   if (max_recs && ((rc = ctx->wal_descs.ensure(max_recs)) || (rc = ctx->wal_crcs.ensure(max_recs)) ||
                    (rc = ctx->win.ensure(window_words(file_len)))))
     return rc;
   uint64_t* n_total = ctx->wal_offsets.p;
-  uint32_t* local = (uint32_t*)(ctx->wal_offsets.p + 1);
-  uint64_t* part = ctx->wal_offsets.p + 1 + (nblocks + 1) / 2;
+  uint64_t* local = ctx->wal_offsets.p + 1;
+  uint64_t* part = ctx->wal_offsets.p + 1 + nblocks;
   // One stream: the header walk, the records at their file-order positions, the window pass over the whole
   // file, then one k_blocks over all records (the log format stores the raw crc: no mask) that also stores
   // each record's crc and verdict. (Run beside the window pass on a second stream the latency-bound header
@@ -757,7 +759,8 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
 int lcrc_wal_scan_queue(lcrc_ctx* ctx, const lcrc_wjob* jobs, size_t njobs, void* stream) {
   if (!ctx || (njobs && !jobs)) return LCRC_EINVAL;
   for (size_t k = 0; k < njobs; ++k)
-    if (!jobs[k].n_recs || (jobs[k].file_len && !jobs[k].file) || (jobs[k].max_recs && !jobs[k].recs))
+    if (!jobs[k].n_recs || (jobs[k].file_len && !jobs[k].file) || (jobs[k].max_recs && !jobs[k].recs) ||
+        jobs[k].file_len >= LCRC_WAL_MAX_FILE)
       return LCRC_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
@@ -780,13 +783,13 @@ int lcrc_wal_scan_queue(lcrc_ctx* ctx, const lcrc_wjob* jobs, size_t njobs, void
       const uint64_t nblocks = (j.file_len + 32767) / 32768;
       if ((rc = w.counts.ensure(nblocks + 1)) || (rc = w.slots.ensure(nblocks * 64 + 1)) ||
           (rc = w.stops.ensure(nblocks + 1)) ||
-          (rc = w.offsets.ensure(1 + (nblocks + 1) / 2 + (nblocks + 63) / 64 + 1)))
+          (rc = w.offsets.ensure(1 + nblocks + (nblocks + 63) / 64 + 1)))
         return rc;
       if (j.max_recs && ((rc = w.descs.ensure(j.max_recs)) || (rc = w.crcs.ensure(j.max_recs)) ||
                          (rc = w.win.ensure(window_words(j.file_len)))))
         return rc;
       h[k] = lcrc_wjob_dev_host{j.file, j.file_len, nblocks, w.counts.p, w.slots.p, w.stops.p,
-                                (uint32_t*)(w.offsets.p + 1), w.offsets.p + 1 + (nblocks + 1) / 2,
+                                w.offsets.p + 1, w.offsets.p + 1 + nblocks,
                                 (lcrc_wal_rec_dev*)j.recs, w.descs.p, j.max_recs, w.offsets.p, j.n_recs};
     }
     HIPCHK(lcrc_launch_wal_parse_queue(h, m, st));

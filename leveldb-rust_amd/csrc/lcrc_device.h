@@ -57,6 +57,7 @@ struct lcrc_wal_rec_dev {  // == lcrc_wal_rec
 #define LCRC_WAL_STOP_TRAILER_DEV 0
 #define LCRC_WAL_STOP_BAD_LENGTH_DEV 1
 #define LCRC_WAL_STOP_ZERO_DEV 2
+#define LCRC_WAL_MAX_FILE (1ull << 34)  // WAL scans: files below 16 GiB (record indices fit 32 bits)
 
 // One batch of a queued uniform launch as the launcher receives it (lcrc_ujob minus the layout fields).
 struct lcrc_qjob_host {
@@ -74,7 +75,7 @@ struct lcrc_wjob_dev_host {
   uint32_t* counts;
   uint2* slots;
   uint8_t* stops;
-  uint32_t* local;
+  uint64_t* local;
   uint64_t* part;
   lcrc_wal_rec_dev* recs;
   lcrc_desc_dev* descs;

@@ -1187,7 +1187,9 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
     const bool oob = !UNIFORM && (d_nx.offset > base_len || (uint64_t)d_nx.length > base_len - d_nx.offset);
     const uint64_t s = oob ? 0 : d_nx.offset;
     const uint32_t len = oob ? 0u : d_nx.length;
-    const int32_t xrel = d_nx.expect_rel;
+    // WAL scan (recs): the descriptor carries the record's file-order index, its expected CRC is at -6
+    const uint64_t ridx = recs ? (uint64_t)(uint32_t)d_nx.expect_rel : i;
+    const int32_t xrel = recs ? -6 : d_nx.expect_rel;
     load_desc(i + nwaves * 4, d_nx);
     const uint64_t e = s + len;
     // the expected value, loaded with the data (bytewise: any alignment, and checked against the buffer)
@@ -1323,8 +1325,8 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       }
       if (mismatch) mismatch_bit(mismatch, i, n, bad, flags);
       if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
-        recs[i].crc = crc;
-        recs[i].status = bad ? 1 : 0;
+        recs[ridx].crc = crc;
+        recs[ridx].status = bad ? 1 : 0;
       }
     }
 #ifdef LCRC_PROBE_CLOCK
@@ -1503,6 +1505,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
         uint64_t s;
         uint32_t len;
         int32_t xrel = LCRC_NO_EXPECT_DEV;
+        uint64_t i_rec = i;  // the output slot (WAL scan: the record's file-order index)
         oob = false;
         if (UNIFORM) {
           s = i * ustride;
@@ -1511,14 +1514,15 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
           const lcrc_desc_dev d = use_first ? d_first : descs[i];
           s = d.offset;
           len = d.length;
-          xrel = d.expect_rel;
+          xrel = recs ? -6 : d.expect_rel;  // WAL scan: the record's file-order index, its CRC at -6
+          if (recs) i_rec = (uint32_t)d.expect_rel;
           if (s > base_len || len > base_len - s) {  // never read: empty, CRC 0, flagged as a mismatch
             oob = true;
             s = 0;
             len = 0;
           }
         }
-        rng = i;
+        rng = i_rec;
         d4 = (uint32_t)(s & 3);  // chunks start on the dword at or below s: aligned loads
         cs = s - d4;
         e = s + len;
@@ -1577,7 +1581,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
           if (slot < R_SLOTS) {
             const uint32_t gen = (sl_gen[slot] + 1) & 0xFFFFu;
             sl_gen[slot] = gen;
-            sl_rng[slot] = (uint32_t)i;
+            sl_rng[slot] = (uint32_t)rng;  // the output slot (a WAL record: its file-order index)
             sl_cs0[slot] = cs;
             sl_e[slot] = e;
             sl_padinv[slot] = padinv;
@@ -1744,11 +1748,19 @@ constexpr uint32_t WAL_PARTB = 64;  // blocks per parse workgroup (= per part to
 #define LCRC_WAL_WIN 0
 #endif
 
+// The WAL scan orders its record descriptors for k_blocks with the records whose covered bytes
+// [h + 6, h + 7 + len) lie in one 256 B window of the file first (about half of the reference's random-read
+// length mix): waves of them alone take the head walk only (k_blocks skips the row tree and the tail walk).
+__device__ __forceinline__ uint32_t wal_single(uint64_t b, uint32_t at, uint32_t length) {
+  const uint64_t s = b * 32768ull + at + 6;
+  return (s >> 8) == ((s + length) >> 8) ? 1u : 0u;  // last covered byte s + length
+}
+
 template <uint32_t WIN>
 __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file, uint64_t file_len,
                                                uint64_t nblocks, uint32_t* __restrict__ counts,
                                                uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                               uint32_t* __restrict__ local, uint64_t* __restrict__ part,
+                                               uint64_t* __restrict__ local, uint64_t* __restrict__ part,
                                                uint32_t bx) {
   __shared__ u32x4 wwin[WIN ? 64 * (WIN / 16) : 1];
   const uint64_t b = (uint64_t)bx * 64 + threadIdx.x;
@@ -1756,7 +1768,7 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
   const uint8_t* blk = file + b * 32768ull;
   const uint64_t rem = b < nblocks ? file_len - b * 32768ull : 0;
   const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
-  uint32_t consumed = 0, nrec = 0, stop = LCRC_WAL_STOP_TRAILER_DEV;
+  uint32_t consumed = 0, nrec = 0, nsingle = 0, stop = LCRC_WAL_STOP_TRAILER_DEV;
   if constexpr (WIN == 0) {
     while (cap - consumed >= 7) {
       uint32_t length, type;
@@ -1769,8 +1781,10 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
         stop = LCRC_WAL_STOP_ZERO_DEV;
         break;
       }
-      if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type);
+      const uint32_t one = wal_single(b, consumed, length);
+      if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | (one << 8));
       ++nrec;
+      nsingle += one;
       consumed += 7 + length;
     }
   } else {
@@ -1808,8 +1822,10 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
           more = false;
           break;
         }
-        if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type);
+        const uint32_t one = wal_single(b, consumed, length);
+        if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | (one << 8));
         ++nrec;
+        nsingle += one;
         consumed += 7 + length;
         if (cap - consumed < 7) {
           more = false;
@@ -1818,17 +1834,18 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
       } while (consumed + 7 <= wlo + WIN);
     }
   }
-  // wave exclusive scan by shuffles
-  uint32_t inc = nrec;
+  // wave exclusive scan by shuffles of (records | one-window records << 32)
+  const uint64_t mine = (uint64_t)nrec | ((uint64_t)nsingle << 32);
+  uint64_t inc = mine;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(inc, d, 64);
+    const uint64_t v = __shfl_up(inc, d, 64);
     if (lane >= (uint32_t)d) inc += v;
   }
   if (b < nblocks) {
     counts[b] = nrec;
     stops[b] = (uint8_t)stop;
-    local[b] = inc - nrec;
+    local[b] = inc - mine;
   }
   if (lane == 63) part[bx] = inc;
 }
@@ -1837,7 +1854,7 @@ template <uint32_t WIN>
 __global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
                                                   uint64_t nblocks, uint32_t* __restrict__ counts,
                                                   uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                                  uint32_t* __restrict__ local, uint64_t* __restrict__ part) {
+                                                  uint64_t* __restrict__ local, uint64_t* __restrict__ part) {
   wal_parse_body<WIN>(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x);
 }
 
@@ -1848,7 +1865,7 @@ struct WalJobDev {
   uint32_t* counts;
   uint2* slots;
   uint8_t* stops;
-  uint32_t* local;
+  uint64_t* local;
   uint64_t* part;
   lcrc_wal_rec_dev* recs;
   lcrc_desc_dev* descs;
@@ -1868,33 +1885,42 @@ __global__ void __launch_bounds__(64) k_wal_parse_q(const WalJobsArg jobs) {
   wal_parse_body<WIN>(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
 }
 
+// record o (file order) and its verify descriptor at position pos of k_blocks' order. The descriptor's
+// expect_rel carries o (the expected CRC of a WAL record is always at -6: k_blocks and k_ranges read it there
+// and store the crc and verdict in recs[o]).
 __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcrc_desc_dev* __restrict__ descs,
-                                        uint64_t o, uint64_t header, uint32_t length, uint32_t type, bool last,
-                                        uint32_t stop) {
-  lcrc_wal_rec_dev rr;
-  rr.header = header;
-  rr.length = length;
-  rr.type = (uint8_t)type;
-  rr.status = 0;
-  rr.block_end = last ? 1 : 0;
-  rr.crc = 0;
-  rr.stop = last ? stop : 0;
-  recs[o] = rr;
-  lcrc_desc_dev d;
-  d.offset = header + 6;
-  d.length = 1 + length;
-  d.expect_rel = -6;
-  descs[o] = d;
+                                        uint64_t o, uint64_t pos, uint64_t max_recs, uint64_t header, uint32_t length,
+                                        uint32_t type, bool last, uint32_t stop) {
+  if (o < max_recs) {
+    lcrc_wal_rec_dev rr;
+    rr.header = header;
+    rr.length = length;
+    rr.type = (uint8_t)type;
+    rr.status = 0;
+    rr.block_end = last ? 1 : 0;
+    rr.crc = 0;
+    rr.stop = last ? stop : 0;
+    recs[o] = rr;
+  }
+  if (pos < max_recs) {
+    lcrc_desc_dev d;
+    d.offset = header + 6;
+    d.length = 1 + length;
+    d.expect_rel = (int32_t)(uint32_t)o;
+    descs[pos] = d;
+  }
 }
 
-// one thread per (block, slot): records in file order at first(b) + i (those below max_recs); the thread
-// of the last slot re-walks a block that has more records than slots. first(b) = the parse workgroups'
-// totals before b's workgroup (summed by each emit workgroup) + local[b]. Workgroup 0 also writes the total
+// one thread per (block, slot), one wave per block: records in file order at first(b) + i (those below
+// max_recs); the thread of the last slot re-walks a block that has more records than slots. Packed counts
+// (records | one-window records << 32): first(b) = the parse workgroups' totals before b's workgroup (summed
+// by each emit workgroup) + local[b]. Descriptors: the one-window records first, then the others, each in file
+// order (both only when every record fits max_recs; else in file order). Workgroup 0 also writes the total
 // record count to n_total (device) and n_out (device or pinned host memory).
 __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, uint64_t nblocks,
                                               const uint32_t* __restrict__ counts,
                                               const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
-                                              const uint32_t* __restrict__ local,
+                                              const uint64_t* __restrict__ local,
                                               const uint64_t* __restrict__ part,
                                               lcrc_wal_rec_dev* __restrict__ recs,
                                               lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
@@ -1905,15 +1931,16 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
   const uint64_t nparts = (nblocks + WAL_PARTB - 1) / WAL_PARTB;
-  // sum of the parse workgroups' totals before this workgroup's blocks (all of them for workgroup 0's
-  // total); 256 / WAL_SLOTS divides WAL_PARTB, so one parse workgroup covers every block here
+  // the totals of all parse workgroups, and of those before this workgroup's blocks; 256 / WAL_SLOTS divides
+  // WAL_PARTB, so one parse workgroup covers every block here
   static_assert(WAL_PARTB % (256 / WAL_SLOTS) == 0, "an emit workgroup's blocks lie in one part");
-  const uint64_t upto = bx == 0 ? nparts : ((uint64_t)bx * 256 / WAL_SLOTS) / WAL_PARTB;
+  static_assert(WAL_SLOTS == 64, "one wave per block");
   const uint64_t mine = ((uint64_t)bx * 256 / WAL_SLOTS) / WAL_PARTB;
   uint64_t acc = 0, accm = 0;
-  for (uint64_t w = threadIdx.x; w < upto; w += 256) {
-    acc += part[w];
-    if (w < mine) accm += part[w];
+  for (uint64_t w = threadIdx.x; w < nparts; w += 256) {
+    const uint64_t v = part[w];
+    acc += v;
+    if (w < mine) accm += v;
   }
   red[threadIdx.x] = acc;
   __syncthreads();
@@ -1921,7 +1948,7 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
     if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
     __syncthreads();
   }
-  const uint64_t total_upto = red[0];
+  const uint64_t total = red[0];
   __syncthreads();
   red[threadIdx.x] = accm;
   __syncthreads();
@@ -1929,27 +1956,42 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
     if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
     __syncthreads();
   }
-  const uint64_t base = red[0];
+  const uint64_t before = red[0];
+  const uint64_t tot_r = (uint32_t)total, tot_s = total >> 32;
   if (bx == 0 && threadIdx.x == 0) {
-    *n_total = total_upto;
-    if (n_out) *n_out = total_upto;
+    *n_total = tot_r;
+    if (n_out) *n_out = tot_r;
   }
-  if (b >= nblocks || max_recs == 0) return;
+  if (b >= nblocks || max_recs == 0) return;  // wave-uniform
+  const bool split = tot_r <= max_recs;
   const uint32_t cnt = counts[b];
+  const uint64_t loc = local[b];
+  const uint64_t first = (uint32_t)before + (uint32_t)loc;           // file order
+  const uint64_t first_s = (before >> 32) + (loc >> 32);             // one-window records before b
+  const uint64_t first_m = tot_s + first - first_s;                  // the others, after every one-window one
+  uint2 sl = make_uint2(0, 0);
+  if (i < cnt) sl = slots[g];
+  const uint32_t one = (sl.y >> 8) & 1u;
+  const uint64_t ones = __builtin_amdgcn_ballot_w64(i < cnt && one);
+  const uint32_t rank_s = __builtin_popcountll(ones & ((1ull << i) - 1));
   if (i >= cnt) return;
-  const uint64_t first = base + local[b];
-  const uint64_t o = first + i;
-  const uint2 sl = slots[g];
   uint32_t at = sl.x & 0xFFFFu, length = sl.x >> 16;
-  if (o < max_recs) wal_put(recs, descs, o, b * 32768ull + at, length, sl.y, i + 1 == cnt, stops[b]);
+  const uint64_t o = first + i;
+  uint64_t pos = !split ? o : one ? first_s + rank_s : first_m + (i - rank_s);
+  wal_put(recs, descs, o, pos, max_recs, b * 32768ull + at, length, sl.y & 0xFFu, i + 1 == cnt, stops[b]);
   if (i == WAL_SLOTS - 1 && cnt > WAL_SLOTS) {
     const uint8_t* blk = file + b * 32768ull;
+    uint64_t ns = __builtin_popcountll(ones), nm = WAL_SLOTS - ns;
     for (uint32_t j = WAL_SLOTS; j < cnt; ++j) {  // the parse already validated every header up to cnt
       at += 7 + length;
       uint32_t type;
       wal_header(blk, at, length, type);
+      const uint32_t one_j = wal_single(b, at, length);
       const uint64_t oj = first + j;
-      if (oj < max_recs) wal_put(recs, descs, oj, b * 32768ull + at, length, type, j + 1 == cnt, stops[b]);
+      pos = !split ? oj : one_j ? first_s + ns : first_m + nm;
+      ns += one_j;
+      nm += 1 - one_j;
+      wal_put(recs, descs, oj, pos, max_recs, b * 32768ull + at, length, type, j + 1 == cnt, stops[b]);
     }
   }
 }
@@ -1957,7 +1999,7 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
 __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ file, uint64_t nblocks,
                                                   const uint32_t* __restrict__ counts,
                                                   const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
-                                                  const uint32_t* __restrict__ local,
+                                                  const uint64_t* __restrict__ local,
                                                   const uint64_t* __restrict__ part,
                                                   lcrc_wal_rec_dev* __restrict__ recs,
                                                   lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
@@ -3216,7 +3258,7 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
 // n_total (device): the record count for k_blocks; n_out (device or pinned host, nullable): the same for
 // the caller
 hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_t nblocks, uint32_t* counts,
-                                 uint2* slots, uint8_t* stops, uint32_t* local, uint64_t* part,
+                                 uint2* slots, uint8_t* stops, uint64_t* local, uint64_t* part,
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st) {
   const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
