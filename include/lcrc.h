@@ -25,6 +25,7 @@
  *   lcrc_batch_uniform_queue            <- the same for a queue of independent batches (e.g. every table of
  *                                          a compaction's output), submitted as one launch per 32 batches
  *   lcrc_batch_queue                    <- lcrc_batch for a queue of independent descriptor batches
+ *   lcrc_batch_multi                    <- a host-resident descriptor batch sharded over several GPUs
  *   lcrc_batch_host_uniform             <- the same starting and ending in host memory (pinned H2D,
  *                                          kernel, D2H, double-buffered)
  *   lcrc_wal_scan / lcrc_wal_scan_async <- the header parse + CRC verify of (2) for every physical record
@@ -194,6 +195,15 @@ int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* s
 int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32_t length, uint64_t stride,
                             const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch,
                             size_t chunk_bytes);
+
+/* Several GPUs, one HOST-resident file (an mmap'd .ldb, a log buffer): the descriptor list (host) is cut into
+ * nctx contiguous shards of about equal covered bytes, on multiples of 32 descriptors; shard k runs on ctxs[k]
+ * (its own device, stream and host thread): the byte span its ranges and expected values read is copied H2D,
+ * its descriptors are rebased to the span, one lcrc_batch, CRCs and mismatch bits D2H into out_crc / out_mismatch
+ * (host, n and ceil(n/32) entries) at the shard's position. Same results as lcrc_batch over the whole file;
+ * no collective, the host concatenates. Several contexts may share a device. Synchronous. */
+int lcrc_batch_multi(lcrc_ctx* const* ctxs, int nctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs,
+                     size_t n, uint32_t* out_crc, uint32_t* out_mismatch);
 
 /* Parse and verify every physical record of a device-resident log file (file_len bytes, 32 KiB
  * blocks, layout of src/db/log.rs). Records are written in file order to recs (device, capacity

@@ -96,7 +96,7 @@ ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
-    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
+    "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_multi", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
     "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_tb_create", "lcrc_tb_destroy", "lcrc_tb_add", "lcrc_tb_flush", "lcrc_tb_finish", "lcrc_tb_size",
@@ -149,6 +149,7 @@ def lib():
     sig("lcrc_batch_queue", i32, vp, ctypes.POINTER(_GJob), sz, vp)
     sig("lcrc_wal_scan_queue", i32, vp, ctypes.POINTER(_WJob), sz, vp)
     sig("lcrc_batch_host_uniform", i32, vp, vp, sz, u32, u64, vp, vp, vp, sz)
+    sig("lcrc_batch_multi", i32, vp, ctypes.c_int, vp, u64, vp, sz, vp, vp)
     sig("lcrc_wal_scan", i32, vp, vp, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp)
     sig("lcrc_wal_scan_async", i32, vp, vp, u64, vp, sz, vp, vp)
     sig("lcrc_table_scan", i32, vp, vp, u64, cp, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp, sz)
@@ -622,6 +623,23 @@ class Engine:
         crcs = out.download(np.uint32, n)
         bits = mm.download(np.uint32, (n + 31) // 32)
         return crcs, unpack_bits(bits, n)
+
+
+def batch_multi(engines, data, offsets, lengths, expect_rel=None):
+    """lcrc_batch_multi: a host-resident file (numpy / bytes) and its descriptors sharded over the engines (one
+    per GPU, or several on one); returns (crc array, mismatch bool array) as lcrc_batch over the whole file."""
+    data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data)
+    n = len(offsets)
+    d = np.zeros(n, DESC_DTYPE)
+    d["offset"], d["length"] = offsets, lengths
+    d["expect_rel"] = NO_EXPECT if expect_rel is None else expect_rel
+    ctxs = (ctypes.c_void_p * len(engines))(*[e.ctx for e in engines])
+    out = np.empty(max(n, 1), np.uint32)
+    mm = np.empty(max((n + 31) // 32, 1), np.uint32)
+    _check(lib().lcrc_batch_multi(ctxs, len(engines), data.ctypes.data_as(ctypes.c_void_p), data.nbytes,
+                                  d.ctypes.data_as(ctypes.c_void_p), n, out.ctypes.data_as(ctypes.c_void_p),
+                                  mm.ctypes.data_as(ctypes.c_void_p)), "lcrc_batch_multi")
+    return out[:n], unpack_bits(mm, n)
 
 
 class UJobs:

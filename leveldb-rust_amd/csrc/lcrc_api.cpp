@@ -12,6 +12,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lcrc.h"
@@ -155,6 +156,11 @@ struct lcrc_ctx {
   DevBuf<uint64_t> wal_offsets;
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs;
+  // lcrc_batch_multi: this context's shard (the byte span its descriptors cover, the rebased descriptors,
+  // CRCs and mismatch words)
+  DevBuf<uint8_t> ms_data;
+  DevBuf<lcrc_desc_dev> ms_desc;
+  DevBuf<uint32_t> ms_out, ms_mm;
   // lcrc_wal_scan_queue: one workspace per log of a submission (header walk, records, window values)
   struct WalWs {
     DevBuf<uint32_t> counts;
@@ -353,6 +359,10 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->wal_offsets.release();
   ctx->wal_descs.release();
   ctx->wal_crcs.release();
+  ctx->ms_data.release();
+  ctx->ms_desc.release();
+  ctx->ms_out.release();
+  ctx->ms_mm.release();
   for (auto& w : ctx->wq)
     for (auto* d : {&w.counts, &w.crcs, &w.win}) d->release();
   for (auto& w : ctx->wq) {
@@ -704,6 +714,91 @@ int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32
   (void)hipFree(d_out);
   if (d_mm) (void)hipFree(d_mm);
   return result;
+}
+
+// One shard of lcrc_batch_multi on its context's device: the span [lo, hi) of the file its descriptors read
+// (ranges and expected values) goes H2D, the descriptors are rebased to it, one lcrc_batch, results D2H.
+static int multi_shard(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
+                       uint32_t* out_crc, uint32_t* out_mismatch) {
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  if (n == 0) return LCRC_OK;
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const lcrc_desc& d = descs[i];
+    if (d.offset > base_len) continue;  // never read: out of bounds in the shard too
+    lo = std::min<uint64_t>(lo, d.offset);
+    hi = std::max<uint64_t>(hi, std::min<uint64_t>(base_len, d.offset + d.length));
+    if (d.expect_rel != LCRC_NO_EXPECT) {
+      const int64_t xp = (int64_t)d.offset + d.expect_rel;
+      if (xp >= 0 && (uint64_t)xp + 4 <= base_len) {
+        lo = std::min<uint64_t>(lo, (uint64_t)xp);
+        hi = std::max<uint64_t>(hi, (uint64_t)xp + 4);
+      }
+    }
+  }
+  if (lo > hi) lo = hi = 0;
+  const uint64_t span = hi - lo;
+  std::vector<lcrc_desc_dev> rb(n);
+  for (size_t i = 0; i < n; ++i) {
+    // rebased: anything outside [lo, hi) stays outside [0, span) (a range past the file ends past the span, an
+    // offset past the file lies past it, an expected value outside the file falls outside the span)
+    rb[i].offset = descs[i].offset > base_len ? UINT64_MAX / 2 : descs[i].offset - lo;
+    rb[i].length = descs[i].length;
+    rb[i].expect_rel = descs[i].expect_rel;
+  }
+  const size_t words = (n + 31) / 32;
+  if ((rc = ctx->ms_data.ensure(std::max<uint64_t>(span, 1))) || (rc = ctx->ms_desc.ensure(n)) ||
+      (rc = ctx->ms_out.ensure(n)) || (rc = ctx->ms_mm.ensure(words)))
+    return rc;
+  hipStream_t st = ctx->stream;
+  if (span) HIPCHK(hipMemcpyAsync(ctx->ms_data.p, base + lo, span, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(ctx->ms_desc.p, rb.data(), n * sizeof(lcrc_desc_dev), hipMemcpyHostToDevice, st));
+  if ((rc = lcrc_batch(ctx, ctx->ms_data.p, span, (const lcrc_desc*)ctx->ms_desc.p, n, ctx->ms_out.p,
+                       out_mismatch ? ctx->ms_mm.p : nullptr, st)))
+    return rc;
+  HIPCHK(hipMemcpyAsync(out_crc, ctx->ms_out.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (out_mismatch) HIPCHK(hipMemcpyAsync(out_mismatch, ctx->ms_mm.p, words * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return LCRC_OK;
+}
+
+int lcrc_batch_multi(lcrc_ctx* const* ctxs, int nctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs,
+                     size_t n, uint32_t* out_crc, uint32_t* out_mismatch) {
+  if (!ctxs || nctx < 1 || (n && (!descs || !out_crc || !base))) return LCRC_EINVAL;
+  for (int k = 0; k < nctx; ++k)
+    if (!ctxs[k]) return LCRC_EINVAL;
+  if (n == 0) return LCRC_OK;
+  // contiguous shards of about equal covered bytes (+64 per descriptor for its fixed cost), cut on multiples of
+  // 32 descriptors so that no mismatch-bitmap word is shared by two shards
+  std::vector<size_t> cut(nctx + 1, n);
+  cut[0] = 0;
+  double total = 0;
+  for (size_t i = 0; i < n; ++i) total += (double)descs[i].length + 64.0;
+  double acc = 0;
+  int k = 1;
+  for (size_t i = 0; i < n && k < nctx; ++i) {
+    acc += (double)descs[i].length + 64.0;
+    while (k < nctx && acc >= total * k / nctx) {
+      cut[k] = std::min(n, (i + 1 + 31) / 32 * 32);
+      ++k;
+    }
+  }
+  for (int j = 1; j <= nctx; ++j) cut[j] = std::max(cut[j], cut[j - 1]);
+  std::vector<int> rcs(nctx, LCRC_OK);
+  std::vector<std::thread> th;
+  for (int j = 0; j < nctx; ++j) {
+    const size_t a = cut[j], b = cut[j + 1];
+    if (a == b) continue;
+    th.emplace_back([&, j, a, b] {
+      rcs[j] = multi_shard(ctxs[j], base, base_len, descs + a, b - a, out_crc + a,
+                           out_mismatch ? out_mismatch + a / 32 : nullptr);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r : rcs)
+    if (r) return r;
+  return LCRC_OK;
 }
 
 int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs, size_t max_recs,

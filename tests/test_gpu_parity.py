@@ -772,3 +772,39 @@ def test_wal_scan_queue_matches_single_scans(lcrc, orc, engines):
     finally:
         eng.graph_destroy(g)
     eng.close()
+
+
+@pytest.mark.parametrize("nctx", [1, 2, 3])
+def test_batch_multi_shards(lcrc, orc, synth, nctx):
+    """lcrc_batch_multi: a host-resident SSTable-layout file (BASELINE configs[2] sizes, 24 MiB)
+    with corrupted blocks, unsorted and out-of-bounds descriptors appended, sharded over 1-3 contexts (several
+    share the one GPU here; each shard has its own device buffer, stream and host thread) -- every CRC and
+    mismatch bit equals the oracle's and the single-context lcrc_batch's."""
+    sizes = synth.mixed_sizes(24 << 20, seed=synth.SEED_MIXED + 7)
+    offs, total = synth.sstable_layout(sizes)
+    f = np.frombuffer(bytes(orc.splitmix_bytes(0xABC, total)), np.uint8).copy()
+    lens = sizes.astype(np.uint32) + 1
+    crc = orc.crc_ranges(f.tobytes(), offs, lens, 1)
+    for k, (o, L) in enumerate(zip(offs, lens)):
+        v = int(crc[k]) ^ (1 if k % 97 == 5 else 0)
+        f[int(o) + int(L):int(o) + int(L) + 4] = np.frombuffer(v.to_bytes(4, "little"), np.uint8)
+    rng = np.random.default_rng(3)
+    extra = rng.permutation(len(offs))[:200]
+    offs2 = np.concatenate([offs, offs[extra], np.array([total - 3, total + 10, 2 ** 40], np.uint64)])
+    lens2 = np.concatenate([lens, lens[extra], np.array([100, 1, 5], np.uint32)])
+    xr = lens2.astype(np.int64)
+    engs = [lcrc.Engine(0, lcrc.MODE_C) for _ in range(nctx)]
+    got, bad = lcrc.batch_multi(engs, f, offs2, lens2, xr)
+    ok = (offs2 <= total) & (lens2.astype(np.uint64) <= total - np.minimum(offs2, total))
+    want = np.zeros(len(offs2), np.uint32)
+    want[ok] = orc.crc_ranges(f.tobytes(), offs2[ok], lens2[ok], 1)
+    assert np.array_equal(got, want)
+    stored = np.array([int.from_bytes(f[int(o) + int(L):int(o) + int(L) + 4].tobytes(), "little")
+                       if ok[k] and int(o) + int(L) + 4 <= total else -1
+                       for k, (o, L) in enumerate(zip(offs2, lens2))], np.int64)
+    assert np.array_equal(bad, ~ok | (stored != want.astype(np.int64)))
+    one, one_bad = engs[0].crc_ranges(f, offs2, lens2, expect_rel=xr)
+    assert np.array_equal(got, one) and np.array_equal(bad, one_bad)
+    for e in engs:
+        e.close()
+
