@@ -63,6 +63,8 @@ def parse(argv=None):
     p.add_argument("--marker-timer", action="store_true",
                    help="fixed config: time the roofline with event markers after the first submission instead of "
                         "events carried by the launches")
+    p.add_argument("--graph", action="store_true",
+                   help="table config: replay each scanner's scan from a HIP graph (one launch per step)")
     p.add_argument("--table-sync", action="store_true",
                    help="table config: time the synchronous lcrc_table_scan (results to pinned host memory)")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
@@ -503,16 +505,26 @@ def workload_table(m, synth, engs, rank, device, args):
         def run(first, count):  # synchronous: one device scan, results back on the host
             for i in range(first, first + count):
                 scanners[i % len(engs)].table_scan_into(dev, len(f), out)
+    elif args.graph:
+        # each scanner's whole scan (14 launches) captured once in a HIP graph and replayed per step
+        graphs = [e.graph_capture(lambda e=e, r=r: e.table_scan_async(dev, len(f), r[0], cap, r[1], r[2]))
+                  for e, r in zip(scanners, res)]
+
+        def run(first, count):
+            for i in range(first, first + count):
+                k = i % len(engs)
+                scanners[k].graph_launch(graphs[k])
     else:
         def run(first, count):  # device-only: enqueued, results, count and verdict stay on the device
             for i in range(first, first + count):
                 k = i % len(engs)
                 scanners[k].table_scan_async(dev, len(f), res[k][0], cap, res[k][1], res[k][2])
 
-    run.keep = (pinned, scanners, res)
+    run.keep = (pinned, scanners, res, dev)  # (a graph holds raw pointers: the file must outlive it)
     cfg = {"workload": "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)",
            "blocks": len(blocks), "file_bytes": int(len(f)), "crc": "crc-32/iso-hdlc (crc32fast), the reference's trailers",
-           "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else "lcrc_table_scan_async"}
+           "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else
+           "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async"}
     return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None,
                     per_step_sync=bool(args.table_sync), engines=scanners)
 
