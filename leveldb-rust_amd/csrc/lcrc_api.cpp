@@ -306,16 +306,15 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   ctx->grid_b = prop.multiProcessorCount * lcrc_blocks_per_cu();  // k_blocks: every resident workgroup
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return bail(fail_hip(e, "hipStreamCreate"));
-  if ((e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking)) != hipSuccess)
-    return bail(fail_hip(e, "hipStreamCreate"));
+  // (the copy stream of lcrc_batch_host_uniform is created on its first call, as the queue lanes)
   if ((e = hipEventCreate(&ctx->t0)) != hipSuccess || (e = hipEventCreate(&ctx->t1)) != hipSuccess)
     return bail(fail_hip(e, "hipEventCreate"));
   for (int i = 0; i < 2; ++i)
     if ((e = hipEventCreateWithFlags(&ctx->ev_copied[i], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming)) != hipSuccess)
       return bail(fail_hip(e, "hipEventCreate"));
-  for (hipStream_t* l : {&ctx->side, &ctx->side2})
-    if ((e = hipStreamCreateWithFlags(l, hipStreamNonBlocking)) != hipSuccess) return bail(fail_hip(e, "hipStreamCreate"));
+  // (the queue lanes' streams are created on first use, ensure_lanes: every stream a context creates takes one of
+  // the process's few hardware queues, and two contexts' main streams sharing one serialize)
   for (hipEvent_t* ev : {&ctx->q_fork, &ctx->q_join, &ctx->q_join2})
     if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bail(fail_hip(e, "hipEventCreate"));
   if ((e = hipHostMalloc(&ctx->h_count, 8 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
@@ -419,6 +418,15 @@ static size_t lcrc_wal_queue_max() { return 16; }  // MAX_WJOBS in lcrc_kernels.
 
 static uint64_t window_words(uint64_t span) { return ((span + 16383) / 16384) * 64; }
 
+// the two queue lanes (ctx->side, ctx->side2), created on the first queued call. Created with every context, four
+// streams per context made two contexts' main streams share a hardware queue (GPU_MAX_HW_QUEUES = 4 here): the
+// table bench's two scanners ran one after the other, 110 vs 86 us per scan.
+static int ensure_lanes(lcrc_ctx* ctx) {
+  for (hipStream_t* l : {&ctx->side, &ctx->side2})
+    if (!*l) HIPCHK(hipStreamCreateWithFlags(l, hipStreamNonBlocking));
+  return LCRC_OK;
+}
+
 // `st` waits for both queue lanes (ctx->side, ctx->side2)
 static int lanes_join(lcrc_ctx* ctx, hipStream_t st) {
   HIPCHK(hipEventRecord(ctx->q_join, ctx->side));
@@ -498,6 +506,7 @@ int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* s
   for (size_t k = 0; k < njobs; ++k) span = std::max(span, jobs[k].base_len);
   if ((rc = ctx->win.ensure(window_words(span))) || (rc = ctx->win2.ensure(window_words(span)))) return rc;
   uint32_t* wins[2] = {ctx->win.p, ctx->win2.p};
+  if ((rc = ensure_lanes(ctx))) return rc;
   hipStream_t lane[2] = {ctx->side, ctx->side2};
   const int grid_b = std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU);
   HIPCHK(hipEventRecord(ctx->q_fork, st));
@@ -642,6 +651,7 @@ int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32
   int rc = set_device(ctx);
   if (rc) return rc;
   if (n == 0) return LCRC_OK;
+  if (!ctx->copy_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
   if (chunk_bytes == 0) chunk_bytes = 64ull << 20;
   // blocks per chunk: a multiple of 32 so every chunk starts on a mismatch-bitmap word
   size_t bpc = std::max<size_t>(chunk_bytes / std::max<uint64_t>(stride, 1), 1);
@@ -887,6 +897,7 @@ int lcrc_wal_scan_queue(lcrc_ctx* ctx, const lcrc_wjob* jobs, size_t njobs, void
                                 w.offsets.p + 1, w.offsets.p + 1 + nblocks,
                                 (lcrc_wal_rec_dev*)j.recs, w.descs.p, j.max_recs, w.offsets.p, j.n_recs};
     }
+    if ((rc = ensure_lanes(ctx))) return rc;
     HIPCHK(lcrc_launch_wal_parse_queue(h, m, st));
     HIPCHK(hipEventRecord(ctx->q_fork, st));
     hipStream_t lane[2] = {ctx->side, ctx->side2};

@@ -1105,10 +1105,13 @@ __device__ __forceinline__ void mismatch_bit(uint32_t* __restrict__ mm, uint64_t
   if (i + 1 == n && bit != 0x80000000u) atomicAnd(&mm[i >> 5], (bit << 1) - 1u);
 }
 
+#ifndef LCRC_KB_WPE
+#define LCRC_KB_WPE 8  // k_blocks' waves per SIMD (register budget); measurement builds vary it
+#endif
 // waves_per_eu(8): 64 VGPRs and few enough SGPRs for 8 waves per SIMD (at 97 SGPRs only 6 fit, so a
 // quarter of the 4 x 512-thread workgroups per CU started only when others had finished)
 template <bool UNIFORM>
-__global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) k_blocks(const uint8_t* __restrict__ base, uint64_t base_len,
+__global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(LCRC_KB_WPE, 8))) k_blocks(const uint8_t* __restrict__ base, uint64_t base_len,
                                                      const lcrc_desc_dev* __restrict__ descs, uint64_t n,
                                                      uint64_t ustride, uint32_t ulen,
                                                      const uint32_t* __restrict__ uexp,
