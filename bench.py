@@ -484,7 +484,13 @@ def workload_table(m, synth, engs, rank, device, args):
     pinned = m.PinnedBuffer((len(blocks) + 8) * m.TBLK_DTYPE.itemsize)
     out = pinned.array.view(m.TBLK_DTYPE)
     out[:] = 0
-    scanners = [m.Engine(device, m.MODE_REF) for _ in engs]
+    # the scanners replace the stream engines (closed first): every stream of the process takes one of its few
+    # hardware queues (GPU_MAX_HW_QUEUES = 4), and two scanners whose streams share a queue run one after the other
+    # (measured: 110 us per scan on two streams, as on one; 86-88 us with the scanners' streams on distinct queues)
+    nscan = len(engs)
+    for e in engs:
+        e.close()
+    scanners = [m.Engine(device, m.MODE_REF) for _ in range(nscan)]
     got = scanners[0].table_scan_into(dev, len(f), out)
     if got != len(blocks) or (out["status"][:got] != 0).any():
         raise RuntimeError("table bench: the sealed table does not scan clean")
