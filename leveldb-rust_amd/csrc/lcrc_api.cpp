@@ -307,6 +307,10 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return bail(fail_hip(e, "hipStreamCreate"));
   // (the copy stream of lcrc_batch_host_uniform is created on its first call, as the queue lanes)
+#ifdef LCRC_EAGER_STREAMS  // measurement build: every stream at creation, as before round 2's last changes
+  for (hipStream_t* l : {&ctx->copy_stream, &ctx->side, &ctx->side2})
+    if ((e = hipStreamCreateWithFlags(l, hipStreamNonBlocking)) != hipSuccess) return bail(fail_hip(e, "hipStreamCreate"));
+#endif
   if ((e = hipEventCreate(&ctx->t0)) != hipSuccess || (e = hipEventCreate(&ctx->t1)) != hipSuccess)
     return bail(fail_hip(e, "hipEventCreate"));
   for (int i = 0; i < 2; ++i)
