@@ -1929,37 +1929,25 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
                                               lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
                                               uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
                                               uint32_t bx) {
-  __shared__ uint64_t red[256];
   const uint64_t g = (uint64_t)bx * blockDim.x + threadIdx.x;
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
   const uint64_t nparts = (nblocks + WAL_PARTB - 1) / WAL_PARTB;
-  // the totals of all parse workgroups, and of those before this workgroup's blocks; 256 / WAL_SLOTS divides
-  // WAL_PARTB, so one parse workgroup covers every block here
-  static_assert(WAL_PARTB % (256 / WAL_SLOTS) == 0, "an emit workgroup's blocks lie in one part");
+  // the totals of all parse workgroups, and of those before this wave's block: one wave per block (64 slots),
+  // each wave sums the parts itself (lane-strided loads and a butterfly: no barrier, no LDS)
   static_assert(WAL_SLOTS == 64, "one wave per block");
-  const uint64_t mine = ((uint64_t)bx * 256 / WAL_SLOTS) / WAL_PARTB;
-  uint64_t acc = 0, accm = 0;
-  for (uint64_t w = threadIdx.x; w < nparts; w += 256) {
+  const uint64_t mine = b / WAL_PARTB;
+  uint64_t total = 0, before = 0;
+  for (uint64_t w = i; w < nparts; w += 64) {
     const uint64_t v = part[w];
-    acc += v;
-    if (w < mine) accm += v;
+    total += v;
+    if (w < mine) before += v;
   }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (uint32_t d = 128; d; d >>= 1) {
-    if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
-    __syncthreads();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    total += __shfl_xor(total, d, 64);
+    before += __shfl_xor(before, d, 64);
   }
-  const uint64_t total = red[0];
-  __syncthreads();
-  red[threadIdx.x] = accm;
-  __syncthreads();
-  for (uint32_t d = 128; d; d >>= 1) {
-    if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
-    __syncthreads();
-  }
-  const uint64_t before = red[0];
   const uint64_t tot_r = (uint32_t)total, tot_s = total >> 32;
   if (bx == 0 && threadIdx.x == 0) {
     *n_total = tot_r;
