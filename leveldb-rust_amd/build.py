@@ -22,16 +22,19 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def source_hash():
-    """sha256 (16 hex digits) of every source and header the library is built from, and of this recipe. It is
-    compiled into lcrc_version(), so a library can be matched to the tree it claims to come from (smoke()
-    checks the loaded library against the tree it runs in)."""
+def source_hash(extra_flags=()):
+    """sha256 (16 hex digits) of every source and header the library is built from, of this recipe and of any
+    extra compile flags. It is compiled into lcrc_version(), so a library can be matched to the tree and the
+    flags it claims to come from: smoke() checks the loaded library against the tree it runs in with NO extra
+    flags, so a library built with any define of its own fails that check."""
     h = hashlib.sha256()
     for name in sorted(SOURCES + HEADERS) + [os.path.basename(__file__)]:
         path = __file__ if name == os.path.basename(__file__) else os.path.join(CSRC, name)
         h.update(name.encode() + b"\0")
         with open(path, "rb") as f:
             h.update(f.read())
+    for flag in extra_flags:
+        h.update(b"flag\0" + flag.encode() + b"\0")
     return h.hexdigest()[:16]
 
 
@@ -44,7 +47,13 @@ def _stale():
 
 
 def build(force=False, verbose=False, extra_flags=()):
-    if not force and not _stale():
+    """The in-tree library. Diagnostic builds (-DLCRC_PROBE_*: clock stamps) go to tools/probe/variants via
+    tools/probe/build_one.sh, never here."""
+    extra_flags = tuple(extra_flags)
+    bad = [f for f in extra_flags if f.replace(" ", "").startswith("-DLCRC_PROBE")]
+    if bad:
+        raise ValueError(f"build.py: {bad} are diagnostic flags; the in-tree library is built without them")
+    if not force and not extra_flags and not _stale():
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
@@ -52,7 +61,7 @@ def build(force=False, verbose=False, extra_flags=()):
     # stalling on every load issued before it; k_windows reads it one walk later instead
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-           "-Wall", "-Wno-unused-result", f'-DLCRC_SRC_HASH="{source_hash()}"', "-o", tmp] + list(extra_flags) + [os.path.join(CSRC, s) for s in SOURCES]
+           "-Wall", "-Wno-unused-result", f'-DLCRC_SRC_HASH="{source_hash(extra_flags)}"', "-o", tmp] + list(extra_flags) + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

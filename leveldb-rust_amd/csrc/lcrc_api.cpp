@@ -211,10 +211,6 @@ int upload_tables(int mode, uint32_t** d_tab) {
   for (int m = 0; m < 4; ++m) lcrc::make_shift_tables(poly, 256ull << m, tab.data() + TAB_ZWIN + m * 1024);
   lcrc::make_shift_tables(poly, 4096, tab.data() + TAB_Z4096);
   lcrc::make_shift_tables(poly, LCRC_TS_PIECE, tab.data() + TAB_Z64K);
-  {
-    const uint64_t kb4[12] = {16, 32, 48, 64, 128, 192, 256, 512, 768, 1024, 2048, 3072};
-    for (int t = 0; t < 12; ++t) lcrc::make_shift_tables(poly, kb4[t], tab.data() + TAB_KB4 + t * 1024);
-  }
   // k_windows builds its LDS image from columns (entries 1, 2, 4, .., 128) of the byte tables it uses
   for (int t = 0; t < 20; ++t) {
     const uint32_t src = t < 4 ? TAB_SLICE + t * 256                    // S0: T_p

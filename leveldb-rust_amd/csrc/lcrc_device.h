@@ -26,9 +26,7 @@ enum : int {
   TAB_SCOLS = 18600,  // the queued fast path's block shifts as columns: Z_{256 k}, k = 0..15, byte position q =
                       // 0..3 (table index 4 k + q, entry b = Z_{256 k}(b << 8 q)), 8 columns each
   TAB_Z64K = 19112,   // Z65536 (the async table scan joins the 64 KiB pieces of a long block)
-  TAB_KB4 = 20136,    // k_blocks' 4-way row trees: Z16, Z32, Z48 | Z64, Z128, Z192 | Z256, Z512, Z768 |
-                      // Z1024, Z2048, Z3072 (12 x 1024 words)
-  TAB_TOTAL = 32424,
+  TAB_TOTAL = 20136,
 };
 
 struct lcrc_desc_dev {  // == lcrc_desc

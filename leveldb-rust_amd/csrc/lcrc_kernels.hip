@@ -136,8 +136,7 @@ __device__ __forceinline__ uint32_t zlook(const void* L, uint32_t tab_byte_off, 
 // 8 lanes c and 8 registers j form an 8x8 matrix of pieces; transposing it leaves lane (k, c) with the
 // pieces 2048*c + 256*k + 128*h + 16*j', j' = 0..7: half h of window 8*c + k = l. The butterfly stages
 // run over lane bits 3..5:
-//   bit 3: v_mov_b32_dpp row_shr:8 / row_shl:8 with a bank_mask -- disabled banks keep `old`, so the DPP
-//          move is also the select (one instruction per register)
+//   bit 3: a DPP select (below)
 //   bit 4: v_permlane16_swap (odd rows of a <-> even rows of b), bit 5: v_permlane32_swap (one
 //          instruction per register pair)
 // Lane bit 3 (register pairs j, j + 1): per output one v_cndmask_b32 with a DPP source (row_shr:8 / row_shl:8
@@ -170,31 +169,19 @@ __device__ __forceinline__ void transpose_pair3(u32x4& a, u32x4& b) {
 
 template <int LB, int D = 1 << (LB - 3)>  // D: the register-index bit paired with lane bit LB
 __device__ __forceinline__ void transpose_stage(u32x4 (&v)[8]) {
-#ifndef LCRC_T3_MOVDPP
   if constexpr (LB == 3) {
+    static_assert(D == 1, "stage 3 pairs registers j, j + 1");
 #pragma unroll
     for (int j = 0; j < 8; j += 2) transpose_pair3(v[j], v[j + 1]);
     return;
   }
-#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (j & D) continue;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       uint32_t a = v[j][q], b = v[j + D][q];
-      if constexpr (LB == 3) {
-#ifndef LCRC_T3_MOVDPP
-        static_assert(D == 1, "stage 3 pairs registers j, j + 1");
-        continue;  // the whole register pair at once below (transpose_stage3)
-#else
-        // lanes 8..15 of each row (banks 2, 3) have bit 3 set
-        uint32_t na = (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)b, 0x118, 0xF, 0xC, false);
-        uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)a, 0x108, 0xF, 0x3, false);
-        v[j][q] = na;
-        v[j + D][q] = nb;
-#endif
-      } else if constexpr (LB == 4) {
+      if constexpr (LB == 4) {
         auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
         v[j][q] = r[0];
         v[j + D][q] = r[1];
@@ -215,55 +202,39 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t region_rsrc(const uint8_t* bas
                                                               uint64_t nreg) {
   uint32_t nrec = 0;
   uint64_t toff = 0;
-#ifdef LCRC_PROBE_NOLOAD  // ablation build: no memory traffic, loads return zeros
-  nreg = 0;
-#endif
   if (t < nreg) {
-#ifdef LCRC_PROBE_L2  // ablation build: every region aliases one of the first 32 (512 KiB, L2-resident)
-    toff = (t & 31) * (uint64_t)REGION;
-#else
     toff = t * (uint64_t)REGION;
-#endif
     const uint64_t rem = span - toff;
     nrec = rem < (uint64_t)REGION ? (uint32_t)rem : (uint32_t)REGION;
   }
   return __builtin_amdgcn_make_buffer_rsrc((void*)(base + toff), (short)0, (int)nrec, 0x00020000);
 }
 
-#ifdef LCRC_PROBE_LDSDATA  // ablation build: random data from an 8 KiB LDS tile, no VMEM at all
-__shared__ u32x4 lcrc_probe_tile[256];
-#define LCRC_REFILL(rs, off) (lcrc_probe_tile[((off) >> 4) & 255])
-#else
 #define LCRC_REFILL(rs, off) __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LCRC_LOAD_AUX)
-#endif
 
-// Load layouts of a 16 KiB region (half h = bytes [128 h, 128 h + 128) of every 256 B window). All read eight
-// whole 128 B lines (or sixteen 64 B halves) per instruction; they differ in which lane gets which 16 B piece,
-// i.e. in which transposes follow.
+// Load layouts of a 16 KiB region (half h = bytes [128 h, 128 h + 128) of every 256 B window). Both read eight
+// whole 128 B lines per instruction; they differ in which lane gets which 16 B piece, i.e. in which transposes
+// follow. (A third, L4 -- four lanes per 64 B half-line, a 4x4 transpose -- measured slower: the memory side lost
+// more than the VALU saved.)
 //  L8 (k_ranges): instruction j, lane l = 8c + k reads region byte 2048 j + 256 k + 128 h + 16 c; a transpose
 //      over lane bits 3, 4 (register bits 0, 1) and a lane-bit-5 chunk join (walk_half) leave lane l with half h
 //      of window l.
-//  L4: instruction j, lane l = 16b + a reads byte 256 (a + 16 (j & 3)) + 128 h + 16 ((j & 4) | b) -- the four
-//      lanes a, a+16, a+32, a+48 read one 64 B half-line; a 4x4 transpose (lane bits 4, 5 x register bits 0, 1).
 //  LX (k_windows, k_windows_q): piece c = c0 + 2 c1 + 4 c2 of a line goes to lane bit 4 (c0), 5 (c1) and 3 (c2):
 //      lane l = k + 8 c2 + 16 c0 + 32 c1 reads byte 2048 pi(j) + 256 k + 128 h + 16 c, pi swapping bits 0 and 2
 //      of j. The two permlane transposes (lane bits 4, 5 x register bits 0, 1; no DPP stage) leave lane l with
 //      the contiguous 64 B chunk c2 of windows W0 and W0 + 8; a row_ror:8 chunk join gives it window
 //      w(l) = (l & 15) | ((l >> 5) & 1) << 4 | ((l >> 4) & 1) << 5: its 4 KiB block's 16 windows stay in one DPP
 //      row, block (lane >> 4) with its two bits swapped.
-constexpr int LAY_L8 = 0, LAY_L4 = 1, LAY_LX = 2;
+constexpr int LAY_L8 = 0, LAY_LX = 2;
 template <int LAY>
 __device__ __forceinline__ uint32_t lane_voff(uint32_t lane, uint32_t h) {
-  if constexpr (LAY == LAY_L4) return 256u * (lane & 15) + 16u * ((lane >> 4) & 3) + 128u * h;
   if constexpr (LAY == LAY_LX)
     return 256u * (lane & 7) + 16u * (((lane >> 4) & 1) | (((lane >> 5) & 1) << 1) | (((lane >> 3) & 1) << 2)) + 128u * h;
   return 256u * (lane & 7) + 16u * (lane >> 3) + 128u * h;
 }
 template <int LAY>
 __device__ __forceinline__ constexpr uint32_t j_off(int j) {
-  return LAY == LAY_L4 ? 4096u * (j & 3) + 16u * (j & 4)
-         : LAY == LAY_LX ? 2048u * (((j & 1) << 2) | (j & 2) | ((j >> 2) & 1))
-                         : 2048u * j;
+  return LAY == LAY_LX ? 2048u * (((j & 1) << 2) | (j & 2) | ((j >> 2) & 1)) : 2048u * j;
 }
 // the window a lane holds after walk_half, and the block (of the region's four) its 16-lane row finishes
 template <int LAY>
@@ -275,10 +246,7 @@ __device__ __forceinline__ uint32_t block_of_row(uint32_t lane) {
   return window_of_lane<LAY>(lane) >> 4;
 }
 
-#ifndef LCRC_KW_LAYOUT
-#define LCRC_KW_LAYOUT 2
-#endif
-constexpr int KW_LAY = LCRC_KW_LAYOUT;  // k_windows' load layout (see lane_voff): 0 L8, 1 L4, 2 LX
+constexpr int KW_LAY = LAY_LX;  // k_windows' load layout (see lane_voff)
 
 template <int LAY = LAY_L8>
 __device__ __forceinline__ void load_half(u32x4 (&v)[8], __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
@@ -321,47 +289,25 @@ __device__ __forceinline__ void init_lx(uint32_t init, uint32_t& ia, uint32_t& i
 // returns walk(init, 128 B half of window l). As each register pair is consumed it is refilled from `rs`
 // (the same half of the next region), so every wave keeps between one and two half-tiles in flight.
 //
-// The transpose stops after lane bits 3 and 4 (LCRC_T5_FULL: all three): lane l then holds the 64 B chunk
-// l >> 5 of the half of windows (l & 31) (registers 0..3) and (l & 31) + 32 (registers 4..7), contiguous, so
-// the two chains walk them unchanged; one v_permlane32_swap of the two chain values (lane bit 5) then gives
-// every lane both chunks of its own window l, joined by Z64. The init register goes the other way: the chunk-0
-// lanes (l < 32) start window l from init[l] and window l + 32 from init[l + 32], the chunk-1 lanes from 0.
-// 16 permlane32 swaps per half become two.
-#ifndef LCRC_T5_FULL
-#define LCRC_T5_JOIN 1
-#else
-#define LCRC_T5_JOIN 0
-#endif
+// L8: the transpose stops after lane bits 3 and 4: lane l then holds the 64 B chunk l >> 5 of the half of windows
+// (l & 31) (registers 0..3) and (l & 31) + 32 (registers 4..7), contiguous, so the two chains walk them unchanged;
+// one v_permlane32_swap of the two chain values (lane bit 5) then gives every lane both chunks of its own window l,
+// joined by Z64. The init register goes the other way: the chunk-0 lanes (l < 32) start window l from init[l] and
+// window l + 32 from init[l + 32], the chunk-1 lanes from 0. 16 permlane32 swaps per half become two.
+// LX: lane bits 4, 5 x register bits 0, 1, then the row_ror:8 chunk join (join_lx).
 template <bool REFILL = true, int LAY = LAY_L8, bool INIT = true>
 __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4 (&v)[8], uint32_t init,
                                               __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
-  constexpr bool JOIN = LCRC_T5_JOIN && LAY == LAY_L8;
-#ifndef LCRC_PROBE_NOTRANSPOSE  // ablation build: walk the pieces as loaded (wrong CRCs, timing only)
-  if constexpr (LAY != LAY_L8) {  // L4, LX: lane bits 4, 5 x register bits 0, 1
+  constexpr bool JOIN = LAY == LAY_L8;
+  if constexpr (LAY == LAY_LX) {
     transpose_stage<4, 1>(v);
     transpose_stage<5, 2>(v);
   } else {
     transpose_stage<3>(v);
     transpose_stage<4>(v);
-    if constexpr (!JOIN) transpose_stage<5>(v);
   }
-#endif
-#ifdef LCRC_PROBE_NOWALK  // ablation build: fold the data with xor only
-  uint32_t p = init;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    p ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-    v[j] = LCRC_REFILL(rs, voff + j_off<LAY>(j));
-  }
-  return p;
-#else
   // two independent chains over the 64 B quarters (pieces 0..3 and 4..7); x carries the chain register
-  // already xored with its next data word. Pair (j, 4 + j) is refilled REFILL_DELAY step groups after it
-  // was consumed (0: at once).
-#ifndef LCRC_REFILL_DELAY
-#define LCRC_REFILL_DELAY 0
-#endif
-  constexpr int D = LCRC_REFILL_DELAY;
+  // already xored with its next data word. Pair (j, 4 + j) is refilled as soon as it is consumed.
   uint32_t ia = INIT ? init : 0u, ib = 0u;
   if constexpr (JOIN && INIT) {  // lanes < 32: init[l] and init[l + 32]; lanes >= 32: 0 and 0
     const auto r = __builtin_amdgcn_permlane32_swap(init, 0u, false, false);
@@ -380,9 +326,9 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     xb = step4x(L, R, xb, v[4 + j].w);
     xa = step4x(L, R, xa, j < 3 ? v[j + 1].x : 0u);
     xb = step4x(L, R, xb, j < 3 ? v[5 + j].x : 0u);
-    if (REFILL && j - D >= 0) {
-      v[j - D] = LCRC_REFILL(rs, voff + j_off<LAY>(j - D));
-      v[4 + j - D] = LCRC_REFILL(rs, voff + j_off<LAY>(4 + j - D));
+    if (REFILL) {
+      v[j] = LCRC_REFILL(rs, voff + j_off<LAY>(j));
+      v[4 + j] = LCRC_REFILL(rs, voff + j_off<LAY>(4 + j));
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the refill here: hipcc would otherwise sink it past the walk
   }
@@ -397,15 +343,7 @@ __device__ __forceinline__ uint32_t walk_half(const void* L, const Rot& R, u32x4
     xa = c0;
     xb = c1;
   }
-  const uint32_t res = zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two 64 B chunks
-#pragma unroll
-  for (int j = 4 - D; j < 4; ++j) {
-    if (!REFILL) break;
-    v[j] = LCRC_REFILL(rs, voff + j_off<LAY>(j));
-    v[4 + j] = LCRC_REFILL(rs, voff + j_off<LAY>(4 + j));
-  }
-  return res;
-#endif
+  return zrot<SET_S1>(L, R, xa) ^ xb;  // Z64 join of the two 64 B chunks
 }
 
 // one level of the block tree inside a 16-lane DPP row: lane g (g % 2^(M+1) == 0) <-
@@ -484,19 +422,12 @@ struct Share {
 
 __device__ __forceinline__ Share make_share(uint64_t nreg) {
   Share sh;
-#ifndef LCRC_REGION_CONTIG
   // regions dealt round-robin over the workgroups: at any moment the whole chip streams one contiguous
   // stretch of the buffer (memory skeleton: 39.9 us per 256 MiB against 41.4-42.0 with a contiguous
   // range per workgroup, tools/probe/probe_skel.hip). No ticket count: a 64-bit division in the prologue.
   sh.lo = blockIdx.x;
   sh.step = gridDim.x;
   sh.end = nreg;
-#else
-  const uint64_t per = (nreg + gridDim.x - 1) / gridDim.x;
-  sh.lo = (uint64_t)blockIdx.x * per;
-  sh.step = 1;
-  sh.end = sh.lo + per < nreg ? sh.lo + per : nreg;
-#endif
   return sh;
 }
 
@@ -752,14 +683,6 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   const unsigned long long s_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long s_first = 0;
 #endif
-#ifdef LCRC_PROBE_LDSDATA
-  for (uint32_t i = tid; i < 256; i += A_THREADS) {
-    uint32_t h = i * 0x9E3779B9u + blockIdx.x * 0x85EBCA6Bu;
-    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
-    lcrc_probe_tile[i] = u32x4{h, h * 0x27D4EB2Fu, h ^ 0x165667B1u, h * 0x94D049BBu};
-  }
-  __syncthreads();
-#endif
 
   // Prologue. The first region of wave w is region w of the share (static), so its HBM loads go out at
   // once; the tables are then built while they are in flight. Nothing in the build waits behind them: the
@@ -772,7 +695,6 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   if (SHIFT) scols = load_shift_cols(gtab, lane);  // issued before the region loads: returns first
   SliceCols slc;
   if (SHIFT) slc = load_slice_cols(gtab, wv);  // scalar: the build then waits on nothing but these
-#ifndef LCRC_DEEP
   uint64_t t = share.region(wv);
   uint32_t ht;
   u32x4 va[8], vb[8];
@@ -784,42 +706,15 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
     load_half<KW_LAY>(vb, rs0, voff_b);
     __builtin_amdgcn_sched_barrier(0);
   }
-#else
-  // deep pipeline: two regions (four half-tiles, 128 VGPRs) in flight per wave; the first two regions of
-  // wave w are static (w and w + waves), tickets start after them
-  constexpr uint32_t NW = A_THREADS / 64;
-  uint64_t t = share.region(wv), t1 = share.region(wv + NW);
-  uint32_t ht = src.find(t, 0), h1 = src.find(t1, ht);
-  u32x4 va[8], vb[8], vc[8], vd[8];
-  {
-    const __amdgpu_buffer_rsrc_t rs0 = src.rsrc(t, ht);
-    const __amdgpu_buffer_rsrc_t rs1 = src.rsrc(t1, h1);
-    __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_LAY>(va, rs0, voff_a);
-    __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_LAY>(vb, rs0, voff_b);
-    __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_LAY>(vc, rs1, voff_a);
-    __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_LAY>(vd, rs1, voff_b);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_src = __builtin_amdgcn_s_memrealtime();
 #endif
-#ifndef LCRC_PROBE_NOTABLES  // ablation build: no LDS image (wrong CRCs, timing only)
   build_tables<!SHIFT>(L, gtab, wv, lane, SHIFT ? &slc : nullptr);
   if (SHIFT) build_shift_tables(L, scols, wv, lane);
-#endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_staged = __builtin_amdgcn_s_memrealtime();
 #endif
-#ifndef LCRC_DEEP
   if (tid == 0) wg_ticket = A_THREADS / 64;  // tickets 0 .. waves-1 were the static first regions
-#else
-  if (tid == 0) wg_ticket = 2 * NW;
-#endif
   lds_barrier();
   const Rot R = make_rot(lane);
   const Rot SR = SHIFT ? make_shift_rot(lane) : R;
@@ -827,7 +722,6 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
   const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
-#ifndef LCRC_DEEP
   uint64_t tn = take_region(&wg_ticket, share, lane);
   uint32_t hn = src.find(tn, ht);
   // tn = the region the refills load (ticket taken after the prologue or in the previous iteration);
@@ -852,40 +746,6 @@ __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __r
     tn = tnn;
     hn = src.find(tnn, hn);
   }
-#else
-  // va/vb: region t, vc/vd: region t1; walking a half refills it with the same half of the region two
-  // ahead (t2 for va/vb, t3 for vc/vd): a refill has three half-walks to arrive instead of one
-  uint64_t t2 = take_region(&wg_ticket, share, lane);
-  uint32_t h2 = src.find(t2, h1);
-  while (t != NO_REGION) {
-    {
-      const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t2, h2);
-      const uint32_t ev = expect_of<FINAL>(src, t, ht, lane);
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t x = walk_half<true, KW_LAY, false>(L, R, va, 0u, rsn, voff_a);
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t p = walk_half<true, KW_LAY>(L, R, vb, x, rsn, voff_b);
-      finish_region<FINAL, SHIFT>(L, R, SR, p, t, ht, lane, src, fin, flags, ev);
-    }
-    const uint64_t t3 = take_region(&wg_ticket, share, lane);
-    const uint32_t h3 = src.find(t3, h2);
-    if (t1 != NO_REGION) {
-      const __amdgpu_buffer_rsrc_t rsn = src.rsrc(t3, h3);
-      const uint32_t ev = expect_of<FINAL>(src, t1, h1, lane);
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t x = walk_half<true, KW_LAY, false>(L, R, vc, 0u, rsn, voff_a);
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t p = walk_half<true, KW_LAY>(L, R, vd, x, rsn, voff_b);
-      finish_region<FINAL, SHIFT>(L, R, SR, p, t1, h1, lane, src, fin, flags, ev);
-    }
-    t = t2;
-    ht = h2;
-    t1 = t3;
-    h1 = h3;
-    t2 = take_region(&wg_ticket, share, lane);
-    h2 = src.find(t2, h3);
-  }
-#endif
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0 && blockIdx.x < 1024) {
@@ -926,15 +786,9 @@ __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, co
   WinQueue src{jobs.j, jobs.n, jobs.nreg, jobs.j[0].base, jobs.j[0].nblk, jobs.j[1].reg0};
   __asm__ volatile("" ::"s"(src.nj), "s"(src.nreg), "s"(src.b0), "s"(src.n0), "s"(src.r1), "s"(gtab), "s"(fin),
                    "s"(flags), "s"(gridDim.x));
-#ifndef LCRC_Q_TREE
   __shared__ __attribute__((aligned(16))) uint32_t L[AQ_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
   windows_body<true, true>(src, gtab, fin, flags, L, &wg_ticket);
-#else  // ablation: the block tree of the single-batch kernel
-  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
-  __shared__ uint32_t wg_ticket;
-  windows_body<true, false>(src, gtab, fin, flags, L, &wg_ticket);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -946,35 +800,24 @@ __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, co
 // ---------------------------------------------------------------------------------------------------
 constexpr int B_THREADS = 512;
 // k_blocks' LDS image (40 KiB): slice tables T0..T3, the binary row-tree shifts Z16..Z128 and Z256..Z2048, Z4096.
-// LCRC_KB_TREE4 (measured slower, kept for reference): a 56 KiB image with 4-way two-level row trees -- lane g
-// shifted by Z_{16 (3 - g % 4)}, four lanes xored by DPP, lane 4 k shifted by Z_{64 (3 - k)}, four xored: 8
-// lookups instead of 16, but config 3 3,957 vs 4,640 GiB/s, WAL 2,600 vs 3,148 (lane-dependent table bases
-// conflict in the banks, and only two workgroups fit a CU).
-#ifdef LCRC_KB_TREE4
-constexpr int KL_Z4096 = 1024, KL_PA = 2048, KL_PB = 5120, KL_WA = 8192, KL_WB = 11264;
-constexpr int B_LDS_DWORDS = 14336;
-#else
+// (4-way two-level row trees -- 8 lookups instead of 16, a 56 KiB image -- measured slower: config 3 3,957 vs
+// 4,640 GiB/s, WAL 2,600 vs 3,148; lane-dependent table bases conflict in the banks and only two workgroups fit
+// a CU.)
 constexpr int KL_Z4096 = TAB_Z4096;
 constexpr int B_LDS_DWORDS = TAB_COLS;  // slice and shift tables (not the column block)
-#endif
 constexpr int B_BATCH = 8;  // window values per lane loaded ahead of the fold
 
-#ifdef LCRC_PROBE_BLOCKS_NOCONFLICT  // ablation build: every k_blocks lookup reads entry r & 0x3 (wrong CRCs)
-#define KB_IDX(x) ((x) & 3u)
-#else
-#define KB_IDX(x) (x)
-#endif
 __device__ __forceinline__ uint32_t byte_step(const uint32_t* L, uint32_t r, uint32_t b) {
-  return (r >> 8) ^ L[TAB_SLICE + KB_IDX((r ^ b) & 0xff)];
+  return (r >> 8) ^ L[TAB_SLICE + ((r ^ b) & 0xff)];
 }
 __device__ __forceinline__ uint32_t step4(const uint32_t* L, uint32_t r, uint32_t w) {
   uint32_t x = r ^ w;
-  return L[TAB_SLICE + 768 + KB_IDX(x & 0xff)] ^ L[TAB_SLICE + 512 + KB_IDX((x >> 8) & 0xff)] ^
-         L[TAB_SLICE + 256 + KB_IDX((x >> 16) & 0xff)] ^ L[TAB_SLICE + KB_IDX(x >> 24)];
+  return L[TAB_SLICE + 768 + (x & 0xff)] ^ L[TAB_SLICE + 512 + ((x >> 8) & 0xff)] ^
+         L[TAB_SLICE + 256 + ((x >> 16) & 0xff)] ^ L[TAB_SLICE + (x >> 24)];
 }
 __device__ __forceinline__ uint32_t zl(const uint32_t* L, int off, uint32_t r) {
-  return L[off + KB_IDX(r & 0xff)] ^ L[off + 256 + KB_IDX((r >> 8) & 0xff)] ^
-         L[off + 512 + KB_IDX((r >> 16) & 0xff)] ^ L[off + 768 + KB_IDX(r >> 24)];
+  return L[off + (r & 0xff)] ^ L[off + 256 + ((r >> 8) & 0xff)] ^ L[off + 512 + ((r >> 16) & 0xff)] ^
+         L[off + 768 + (r >> 24)];
 }
 
 // Lane g's share of a row walk over [a, e) (0 <= e - a <= 256): the 16 B piece ending at
@@ -1033,19 +876,6 @@ __device__ __forceinline__ uint32_t row_bcast0(uint32_t v, uint32_t lane) {
   return lane < 32 ? (lane < 16 ? r0 : r1) : (lane < 48 ? r2 : r3);
 }
 
-#ifdef LCRC_KB_TREE4
-// Σ_g Z_{u (15 - g)}(v_g) over a 16-lane row into lane 0 (u = 16 for pieces, 256 for windows): tables at tA
-// (Z_u, Z_2u, Z_3u) and tB (Z_4u, Z_8u, Z_12u)
-__device__ __forceinline__ uint32_t row_join4(const uint32_t* L, uint32_t v, uint32_t g, int tA, int tB) {
-  if ((g & 3) != 3) v = zl(L, tA + (int)(2 - (g & 3)) * 1024, v);
-  v ^= row_down(v, 0);
-  v ^= row_down(v, 1);  // lane 4 k: the four shifted values of its group
-  if ((g & 3) == 0 && (g >> 2) != 3) v = zl(L, tB + (int)(2 - (g >> 2)) * 1024, v);
-  v ^= row_down(v, 2);
-  v ^= row_down(v, 3);  // lane 0: all sixteen
-  return v;
-}
-#endif
 
 // walk(R0, base[a, e)) from the row's loaded pieces, returned to every lane of the row; a == e -> R0.
 // Must be called by all 64 lanes (contains cross-lane ops).
@@ -1072,16 +902,12 @@ __device__ uint32_t row_walk(const uint32_t* L, const RowPiece& p, bool empty_ra
   cv = step4(L, cv, wq[1]);
   cv = step4(L, cv, wq[2]);
   cv = step4(L, cv, wq[3]) ^ rh;
-#ifdef LCRC_KB_TREE4
-  cv = row_join4(L, cv, g, KL_PA, KL_PB);
-#else
   // row tree: level m joins lane g with g + 2^m, shifting the left part by 16*2^m bytes
 #pragma unroll
   for (int m = 0; m < 4; ++m) {  // only the combining lanes look up (exec-masked: fewer bank conflicts)
     const uint32_t pn = row_down(cv, m);
     if ((g & ((2u << m) - 1)) == 0) cv = zl(L, TAB_ZPIECE + m * 1024, cv) ^ pn;
   }
-#endif
   const uint32_t res = row_bcast0(cv, lane);
   return empty_range ? R0 : res;
 }
@@ -1151,14 +977,6 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
     }
   };
   lcrc_desc_dev d_nx;
-#ifdef LCRC_KB_TREE4
-  load_desc(wave * 4 + row, d_nx);
-  for (uint32_t i = threadIdx.x; i < B_LDS_DWORDS / 4; i += B_THREADS) {
-    const uint32_t w = 4 * i;  // slice | Z4096 | the 4-way tree shifts
-    const uint32_t src = w < 1024 ? TAB_SLICE + w : w < 2048 ? TAB_Z4096 + (w - 1024) : TAB_KB4 + (w - 2048);
-    ((u32x4*)L)[i] = *(const u32x4*)(gtab + src);
-  }
-#else
   {
     // every load first, then every store: one L2 round trip for the image instead of one per 8 KiB
     constexpr int PER = (B_LDS_DWORDS / 4 + B_THREADS - 1) / B_THREADS;
@@ -1175,15 +993,11 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       if (i < B_LDS_DWORDS / 4) ((u32x4*)L)[i] = t[k];
     }
   }
-#endif
   __syncthreads();
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long b_tab = __builtin_amdgcn_s_memrealtime();
 #endif
 
-#if defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 1  // ablation: table fill only
-  if (n) return;
-#endif
   for (uint64_t i0 = wave * 4; i0 < n; i0 += nwaves * 4) {
     const uint64_t i = i0 + row;
     const bool valid = i < n;
@@ -1222,9 +1036,6 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       const uint32_t* wv = win + ws + g - npad;
       uint32_t rmax = max(max(__builtin_amdgcn_readlane(rr32, 0), __builtin_amdgcn_readlane(rr32, 16)),
                                 max(__builtin_amdgcn_readlane(rr32, 32), __builtin_amdgcn_readlane(rr32, 48)));
-#if defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 3  // ablation: no window fold (wrong CRCs)
-      if (n) rmax = 0;
-#endif
 
       // every load this range needs first: head and tail pieces, the first batch of window values
       const RowPiece ph = row_load(base, s, head_end, g);
@@ -1239,11 +1050,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
         b_ph[0] = __builtin_amdgcn_s_memrealtime();
       }
 #endif
-#if defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 2  // ablation: no head/tail walks (wrong CRCs)
-      const uint32_t head = ph.w[0] ^ ph.w[1] ^ pt.w[2];
-#else
       const uint32_t head = row_walk(L, ph, s == head_end, init, g, lane);
-#endif
 #ifdef LCRC_PROBE_PHASES
       if (b_nit == 0) {
         __asm__ volatile("s_waitcnt lgkmcnt(0)" ::"v"(head) : "memory");
@@ -1268,15 +1075,11 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
       // (a wave whose four ranges each lie in one window -- short WAL records -- skips the row tree and
       // the tail walk: both are wave-uniform decisions)
       if (rmax) {
-#ifdef LCRC_KB_TREE4
-        a = row_join4(L, a, g, KL_WA, KL_WB);
-#else
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const uint32_t pn = row_down(a, m);
           if ((g & ((2u << m) - 1)) == 0) a = zl(L, TAB_ZWIN + m * 1024, a) ^ pn;
         }
-#endif
       }
       const uint32_t mid = row_bcast0(a, lane);
 #ifdef LCRC_PROBE_PHASES
@@ -1287,9 +1090,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
 #endif
       acc = single ? head : mid;
       // tail: the partial last window, walked from the folded value
-#if !(defined(LCRC_PROBE_KB) && LCRC_PROBE_KB == 2)
       if (__builtin_amdgcn_ballot_w64(ta != e)) acc = row_walk(L, pt, ta == e, acc, g, lane);
-#endif
 #ifdef LCRC_PROBE_PHASES
       if (b_nit == 0) {
         __asm__ volatile("" ::"v"(acc));
@@ -2275,9 +2076,6 @@ __device__ __forceinline__ uint32_t small_mod(uint32_t x, uint32_t a) {
 
 __device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, uint8_t* o, uint32_t ulen,
                                    uint32_t lane) {
-#if defined(LCRC_SN_PROBE) && LCRC_SN_PROBE == 1
-  return true;  // probe: frame overhead only
-#endif
   uint32_t w0 = 0;  // bytes written before this window
   for (uint32_t base = q; base < qe;) {
     const uint32_t i = base + lane;  // candidate start (reads stay inside the staging's slack)
@@ -2325,9 +2123,6 @@ __device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, u
       const uint32_t ew = (uint32_t)__builtin_amdgcn_readlane((int)pw, j);
       const uint32_t ea = (uint32_t)__builtin_amdgcn_readlane((int)pa, j);
       const uint32_t eo = ew & 0xFFFFu, eln = (ew >> 16) + 1;
-#if defined(LCRC_SN_PROBE) && LCRC_SN_PROBE == 2
-      if (eln) continue;  // probe: parse only
-#endif
       if (ea & 0x80000000u) {
         const uint32_t a = ea & 0x7FFFFFFFu;
         for (uint32_t k = lane; k < eln; k += 64) o[eo + k] = in[a + k];

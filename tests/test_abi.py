@@ -109,3 +109,27 @@ def test_library_built_from_this_tree(lcrc):
     and it is this tree's (smoke() makes the same check on the GPU box)."""
     import __graft_entry__ as entry
     assert f"src {entry.source_hash()}" in lcrc.lib().lcrc_version().decode()
+
+
+def test_build_refuses_diagnostic_flags_and_hashes_flags():
+    """The in-tree library is never a diagnostic build: build.py refuses -DLCRC_PROBE_* for it, and any extra
+    compile flag changes the source hash compiled into lcrc_version(), so a library built with a define of its
+    own fails the provenance check above and smoke()'s."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("lcrc_build_t", os.path.join(ROOT, "leveldb-rust_amd", "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    with pytest.raises(ValueError):
+        b.build(extra_flags=["-DLCRC_PROBE_CLOCK"])
+    with pytest.raises(ValueError):
+        b.build(extra_flags=["-DLCRC_PROBE_PHASES=1"])
+    assert b.source_hash(["-DLCRC_A_WGCU=2"]) != b.source_hash()
+    assert b.source_hash(()) == b.source_hash()
+
+
+def test_product_kernels_carry_no_wrong_crc_ablation():
+    """Only clock-stamp diagnostics (which cannot change a CRC) remain behind LCRC_PROBE_* in the shipped
+    kernel source."""
+    with open(os.path.join(ROOT, "leveldb-rust_amd", "csrc", "lcrc_kernels.hip")) as f:
+        src = f.read()
+    assert set(re.findall(r"LCRC_PROBE_\w+", src)) <= {"LCRC_PROBE_CLOCK", "LCRC_PROBE_PHASES"}
