@@ -227,6 +227,22 @@ def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
     return dist.max(elapsed), elapsed, gpu_ms, cov_launches, cov_steps
 
 
+def single_launches(w, eng, count=12):
+    """Per-launch duration of ONE batch handed over alone (a reader verifying one batch): each launch carries its
+    own start and end events (lcrc_timer_kernels edges 0 and 1 on the same launch) and runs with the GPU idle
+    before and after it (the previous launch's end event waited for). Returns sorted durations in us."""
+    us = []
+    for i in range(count + 2):
+        eng.timer_kernels(0)
+        eng.timer_kernels(1)
+        w.single(i)
+        ms = eng.timer_stop()
+        if i >= 2:  # the first two warm the path (code object, clocks)
+            us.append(ms * 1e3)
+    eng.timer_kernels(2)
+    return sorted(us)
+
+
 def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
     """Whole-job throughput: every rank processed bytes_per_step * steps in at most elapsed_max."""
     return bytes_per_step * steps * world / elapsed_max / 2 ** 30
@@ -270,6 +286,7 @@ class Workload:
         self.per_step_sync = per_step_sync
         self.engines = engines  # the engines the steps run on, when not the bench's own
         self.kernel_events = kernel_events  # the launches can carry the roofline's events (queued fast path)
+        self.single = None  # single(i): one launch of the dominant kernel, for the alone-on-the-GPU figure
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -314,8 +331,11 @@ def workload_fixed(m, synth, engs, rank, device, args):
 
     cfg = {"workload": f"{nblk // 1024}K x 4 KiB blocks, device-resident (BASELINE configs[1])", "blocks": nblk,
            "block_bytes": blen, "batches_rotated": NBUF, "layout": "back-to-back", "submission": sub}
-    return Workload(run, nblk * blen, cfg, launches, ("uniform", host[0], nblk, blen), crcs,
-                    kernel_events=not args.marker_timer)
+    w = Workload(run, nblk * blen, cfg, launches, ("uniform", host[0], nblk, blen), crcs,
+                 kernel_events=not args.marker_timer)
+    if q == 1:  # one batch handed over alone: the launch with nothing before or after it on the GPU
+        w.single = lambda i: engs[0].batch_uniform(bufs[i % NBUF], nblk, blen, blen, outs[0][i % NBUF])
+    return w
 
 
 def workload_fixed_host(m, synth, rank, args):
@@ -700,6 +720,10 @@ def main(argv=None):
     rank, world = dist.rank, dist.world
     device = dist.local_rank
     m = entry.load()
+    if os.environ.get("LCRC_RANK_DEVICE_MOD") == "1" and args.engine == "device":
+        # test-only: rank r on device r % device_count, so that N device-bound ranks can share a 1-GPU box
+        # (tests/test_multi_rank_gpu.py); the driver's N-GPU runs never set it (rank r = device LOCAL_RANK)
+        device = dist.local_rank % max(1, m.device_count())
     synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
     mode = m.MODE_C if args.mode == "c" else m.MODE_REF
     flags = m.FLAG_MASK if mode == m.MODE_C else 0
@@ -730,11 +754,20 @@ def main(argv=None):
     elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, timers,
                                                                       kernel_events=w.kernel_events)
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
-    rows = dist.gather([rank, device, elapsed, fp])
-    per_gpu = [{"rank": int(r[0]), "device": int(r[1]),
-                "gib_s": round(w.nbytes * args.steps / r[2] / 2 ** 30, 2),
-                "pct_hbm": round(100.0 * w.nbytes * args.steps / r[2] / (PEAK_GBS * 1e9), 2),
-                "crc_xor": f"{int(r[3]):08x}"} for r in rows]
+    # this rank's per-launch figure of the dominant kernel (its own HIP events; -1 when not timed on the GPU)
+    launch_us = gpu_ms * 1e3 / cov_launches if (timers and gpu_ms and cov_launches) else -1.0
+    bytes_per_launch = w.nbytes * cov_steps / cov_launches if cov_launches else 0
+    rows = dist.gather([rank, device, elapsed, fp, launch_us])
+    per_gpu = []
+    for r in rows:
+        row = {"rank": int(r[0]), "device": int(r[1]),
+               "gib_s": round(w.nbytes * args.steps / r[2] / 2 ** 30, 2),
+               "pct_hbm": round(100.0 * w.nbytes * args.steps / r[2] / (PEAK_GBS * 1e9), 2),
+               "crc_xor": f"{int(r[3]):08x}"}
+        if r[4] > 0:
+            row["launch_us"] = round(r[4], 2)
+            row["frac"] = round(bytes_per_launch / (r[4] * 1e-6) / 1e9 / PEAK_GBS, 4)
+        per_gpu.append(row)
 
     result = {
         "metric": METRIC,
@@ -779,6 +812,16 @@ def main(argv=None):
                        "step of the whole pipeline, not one kernel's duration"),
             "profile": load_profile(args.config, args.mode),
         }
+        if w.single is not None and engs:
+            one = single_launches(w, engs[0])
+            med = one[len(one) // 2]
+            result["roofline"]["frac_single_launch"] = round(bytes_per_launch / (med * 1e-6) / 1e9 / PEAK_GBS, 4)
+            result["roofline"]["single_launch"] = {
+                "launch_us_median": round(med, 2), "launch_us_min": round(one[0], 2),
+                "launch_us_max": round(one[-1], 2), "launches": len(one),
+                "frac_best": round(bytes_per_launch / (one[0] * 1e-6) / 1e9 / PEAK_GBS, 4),
+                "timing": "one lcrc_batch_uniform launch alone on the GPU (the previous one's end waited for), its "
+                          "own start and end events; median over the launches (after the timed region)"}
     else:
         result["roofline"] = None
     if (rank == 0 and world == 1 and not args.no_cpu_baseline and w.sample is not None

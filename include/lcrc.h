@@ -124,6 +124,11 @@ typedef struct lcrc_wal_rec {
 #define LCRC_WAL_STOP_ZERO 2       /* type == 0 && length == 0 (zero fill) */
 #define LCRC_WAL_STOP_MISMATCH 3   /* checksum mismatch: the reader drops the rest of the block */
 
+/* Contexts and streams. A context owns per-call device workspace (window values, WAL and table-scan state,
+ * the shard buffers of lcrc_batch_multi). Calls on ONE context must therefore be stream-ordered: issue them
+ * on one stream (or order the streams with events); two calls of one context in flight on two unordered
+ * streams race on that workspace. For concurrent streams use one context per stream (bench.py does: one
+ * context per engine). Different contexts never share workspace. */
 int lcrc_device_count(int* n);
 int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags);
 int lcrc_ctx_destroy(lcrc_ctx* ctx);
@@ -196,12 +201,14 @@ int lcrc_batch_host_uniform(lcrc_ctx* ctx, const uint8_t* base, size_t n, uint32
                             const uint32_t* expected, uint32_t* out_crc, uint32_t* out_mismatch,
                             size_t chunk_bytes);
 
-/* Several GPUs, one HOST-resident file (an mmap'd .ldb, a log buffer): the descriptor list (host) is cut into
- * nctx contiguous shards of about equal covered bytes, on multiples of 32 descriptors; shard k runs on ctxs[k]
- * (its own device, stream and host thread): the byte span its ranges and expected values read is copied H2D,
- * its descriptors are rebased to the span, one lcrc_batch, CRCs and mismatch bits D2H into out_crc / out_mismatch
- * (host, n and ceil(n/32) entries) at the shard's position. Same results as lcrc_batch over the whole file;
- * no collective, the host concatenates. Several contexts may share a device. Synchronous. */
+/* Several GPUs, one HOST-resident file (an mmap'd .ldb, a log buffer): the descriptor list (host), taken in
+ * offset order, is cut into nctx contiguous shards of about equal covered bytes; shard k runs on ctxs[k] (its
+ * own device, stream and host thread): the byte span its ranges and expected values read is copied H2D, its
+ * descriptors are rebased to the span, one lcrc_batch, CRCs and mismatch bits D2H into out_crc / out_mismatch
+ * (host, n and ceil(n/32) entries) at the descriptors' own positions (a list out of offset order is sorted on
+ * the host and the results scattered back, so no shard copies more than its own span). Same results as
+ * lcrc_batch over the whole file; no collective, the host concatenates. Several contexts may
+ * share a device. Synchronous; on an error, lcrc_last_error() names the failing shard. */
 int lcrc_batch_multi(lcrc_ctx* const* ctxs, int nctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs,
                      size_t n, uint32_t* out_crc, uint32_t* out_mismatch);
 
@@ -345,8 +352,9 @@ int lcrc_timer_stop(lcrc_ctx* ctx, float* ms);
 int lcrc_timer_span(lcrc_ctx* first, lcrc_ctx* last, float* ms);
 
 /* HIP graphs of the context's own stream: lcrc_graph_begin starts capturing the calls made on the context
- * with stream NULL (they must allocate nothing: reserve first), lcrc_graph_end instantiates them as one
- * replayable graph; lcrc_graph_launch replays it on the context stream. */
+ * with stream NULL (they must allocate nothing: reserve first; the queued calls' two side streams are created
+ * by lcrc_graph_begin itself, so even a first queued call can be captured), lcrc_graph_end instantiates them as
+ * one replayable graph; lcrc_graph_launch replays it on the context stream. */
 int lcrc_graph_begin(lcrc_ctx* ctx);
 int lcrc_graph_end(lcrc_ctx* ctx, void** graph_exec);
 int lcrc_graph_launch(lcrc_ctx* ctx, void* graph_exec);

@@ -779,35 +779,75 @@ int lcrc_batch_multi(lcrc_ctx* const* ctxs, int nctx, const uint8_t* base, uint6
   for (int k = 0; k < nctx; ++k)
     if (!ctxs[k]) return LCRC_EINVAL;
   if (n == 0) return LCRC_OK;
-  // contiguous shards of about equal covered bytes (+64 per descriptor for its fixed cost), cut on multiples of
-  // 32 descriptors so that no mismatch-bitmap word is shared by two shards
+  // Shards are contiguous in OFFSET order, so that each one copies only the span its own ranges cover (a
+  // descriptor list out of file order would otherwise give every shard nearly the whole file). Already sorted
+  // lists keep their order; otherwise the results are scattered back to the caller's positions.
+  std::vector<size_t> order(n);
+  for (size_t i = 0; i < n; ++i) order[i] = i;
+  bool sorted = true;
+  for (size_t i = 1; i < n && sorted; ++i) sorted = descs[i - 1].offset <= descs[i].offset;
+  if (!sorted)
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return descs[a].offset < descs[b].offset; });
+  std::vector<lcrc_desc> sd;
+  if (!sorted) {
+    sd.resize(n);
+    for (size_t i = 0; i < n; ++i) sd[i] = descs[order[i]];
+  }
+  const lcrc_desc* D = sorted ? descs : sd.data();
+  // about equal covered bytes per shard (+64 per descriptor for its fixed cost); in place (sorted) the cuts fall on
+  // multiples of 32 descriptors so that no mismatch-bitmap word is shared by two shards
   std::vector<size_t> cut(nctx + 1, n);
   cut[0] = 0;
   double total = 0;
-  for (size_t i = 0; i < n; ++i) total += (double)descs[i].length + 64.0;
+  for (size_t i = 0; i < n; ++i) total += (double)D[i].length + 64.0;
   double acc = 0;
   int k = 1;
   for (size_t i = 0; i < n && k < nctx; ++i) {
-    acc += (double)descs[i].length + 64.0;
+    acc += (double)D[i].length + 64.0;
     while (k < nctx && acc >= total * k / nctx) {
-      cut[k] = std::min(n, (i + 1 + 31) / 32 * 32);
+      cut[k] = sorted ? std::min(n, (i + 1 + 31) / 32 * 32) : i + 1;
       ++k;
     }
   }
   for (int j = 1; j <= nctx; ++j) cut[j] = std::max(cut[j], cut[j - 1]);
+  // out of order: each shard writes its own result arrays, scattered afterwards
+  std::vector<uint32_t> scrc(sorted ? 0 : n), smm(sorted || !out_mismatch ? 0 : (n + 31) / 32 + nctx);
   std::vector<int> rcs(nctx, LCRC_OK);
+  std::vector<std::string> errs(nctx);  // each worker's lcrc_last_error (thread-local there)
   std::vector<std::thread> th;
   for (int j = 0; j < nctx; ++j) {
     const size_t a = cut[j], b = cut[j + 1];
     if (a == b) continue;
     th.emplace_back([&, j, a, b] {
-      rcs[j] = multi_shard(ctxs[j], base, base_len, descs + a, b - a, out_crc + a,
-                           out_mismatch ? out_mismatch + a / 32 : nullptr);
+      uint32_t* oc = sorted ? out_crc + a : scrc.data() + a;
+      // a private bitmap per shard when scattering: shard j's words start at a / 32 + j (its own words)
+      uint32_t* om = !out_mismatch ? nullptr : sorted ? out_mismatch + a / 32 : smm.data() + a / 32 + j;
+      rcs[j] = multi_shard(ctxs[j], base, base_len, D + a, b - a, oc, om);
+      if (rcs[j]) errs[j] = g_last_error;
     });
   }
   for (auto& t : th) t.join();
-  for (int r : rcs)
-    if (r) return r;
+  for (int j = 0; j < nctx; ++j)
+    if (rcs[j]) {
+      g_last_error = "lcrc_batch_multi shard " + std::to_string(j) + ": " + errs[j];
+      return rcs[j];
+    }
+  if (!sorted) {
+    for (int j = 0; j < nctx; ++j) {
+      const size_t a = cut[j], b = cut[j + 1];
+      for (size_t i = a; i < b; ++i) {
+        const size_t o = order[i];
+        out_crc[o] = scrc[i];
+        if (out_mismatch) {
+          const size_t w = a / 32 + j, bit = i - a;  // the shard's own bitmap, bit i - a
+          const bool bad = (smm[w + bit / 32] >> (bit & 31)) & 1u;
+          if (bad) out_mismatch[o >> 5] |= 1u << (o & 31);
+          else out_mismatch[o >> 5] &= ~(1u << (o & 31));
+        }
+      }
+    }
+    if (out_mismatch && (n & 31)) out_mismatch[n >> 5] &= (1u << (n & 31)) - 1u;  // bits past n, as lcrc_batch
+  }
   return LCRC_OK;
 }
 
@@ -1331,28 +1371,42 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
     return nullptr;
   };
   if (file_len < FOOTER_ENCODED_LENGTH) return corrupt("file is too short to be an sstable");
-  // the device-only scan first (one synchronisation); it grows its own result capacity as needed
-  {
+  // the device-only scan first (one synchronisation); it grows its own result capacity as needed. A filter
+  // policy name too long for the device's metaindex key, or a workspace the device scan cannot get, leaves the
+  // table to the paths below (read_meta opens such tables: table.rs:86-112).
+  const bool key_fits = !filter_name || strlen(filter_name) + 6 <= sizeof(((lcrc_tscan_key*)nullptr)->key);
+  if (key_fits) {
     uint64_t cap = std::max<uint64_t>(std::max<uint64_t>(max_blocks, ctx->ts_blocks.cap), 1024);
     lcrc_tscan_dev* hs = (lcrc_tscan_dev*)ctx->ts_host;
+    bool ran = true;
     for (int attempt = 0; attempt < 3; ++attempt) {
-      if ((rc = ctx->ts_blocks.ensure(cap)) || (rc = ctx->ts_count.ensure(1))) return rc;
-      if ((rc = lcrc_table_scan_async(ctx, file, file_len, filter_name, (lcrc_tblk*)ctx->ts_blocks.p, cap,
-                                      ctx->ts_count.p, ctx->ts_count_status, nullptr)))
-        return rc;
+      rc = ctx->ts_blocks.ensure(cap);
+      if (!rc) rc = ctx->ts_count.ensure(1);
+      if (!rc)
+        rc = lcrc_table_scan_async(ctx, file, file_len, filter_name, (lcrc_tblk*)ctx->ts_blocks.p, cap,
+                                   ctx->ts_count.p, ctx->ts_count_status, nullptr);
+      if (rc == LCRC_ENOMEM || rc == LCRC_EINVAL) {  // no device-only scan for this table: the paths below
+        ran = false;
+        break;
+      }
+      if (rc) return rc;
       HIPCHK(hipMemcpyAsync(hs, ctx->ts_state.p, sizeof(lcrc_tscan_dev), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       if (hs->status == 3) {  // capacity: grow to what the table needs and scan again
         cap = std::max<uint64_t>(hs->n_data + 16, cap * 2);
       } else if (hs->status == 2 && hs->gate == 1) {  // decoded frames over the workspace: grow it, scan again
-        if ((rc = ts_reserve(ctx, file_len, cap, hs->need_out + hs->need_out / 4 + 4096, hs->need_chunks + 64)))
-          return rc;
+        rc = ts_reserve(ctx, file_len, cap, hs->need_out + hs->need_out / 4 + 4096, hs->need_chunks + 64);
+        if (rc == LCRC_ENOMEM) {
+          ran = false;
+          break;
+        }
+        if (rc) return rc;
       } else {
         break;
       }
     }
-    if (hs->status == 1) return corrupt(lcrc_table_scan_message(hs->code));
-    if (hs->status == 0) {
+    if (ran && hs->status == 1) return corrupt(lcrc_table_scan_message(hs->code));
+    if (ran && hs->status == 0) {
       const size_t n = hs->n_total;
       *n_blocks = n;
       if (!blocks || max_blocks < n) return LCRC_ERANGE;
@@ -1558,6 +1612,9 @@ int lcrc_graph_begin(lcrc_ctx* ctx) {
   if (!ctx) return LCRC_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
+  // the queue lanes (lcrc_batch_queue, lcrc_wal_scan_queue) exist before the capture starts: a first-ever queued
+  // call inside the capture then creates no stream
+  if ((rc = ensure_lanes(ctx))) return rc;
   HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
   return LCRC_OK;
 }

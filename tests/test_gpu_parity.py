@@ -808,3 +808,122 @@ def test_batch_multi_shards(lcrc, orc, synth, nctx):
     for e in engs:
         e.close()
 
+
+
+def _wal_file(lcrc, synth, total, seed):
+    """The bench's WAL file (BASELINE configs[3]): synth.wal_lengths records through the LogWriter restatement."""
+    w = lcrc.LogWriter()
+    payload = synth.splitmix_bytes(seed + 1000, 1 << 20)
+    for n in synth.wal_lengths(total, seed=seed):
+        w.add_record(payload[:n] if n <= len(payload) else np.resize(payload, n))
+    return bytearray(w.contents())
+
+
+def _wal_check_scan(lcrc, orc, eng, data, mode):
+    """Every (header, length, type) of the device scan equals the reference reader's header walk
+    (log.rs:204-279), every crc the oracle's over type ++ payload, every verdict the stored-vs-computed compare
+    (log.rs:260-273); the async form returns the same records and count."""
+    dev = lcrc.DeviceBuffer.from_host(np.frombuffer(bytes(data), np.uint8))
+    want = _wal_expect(orc, data)
+    h = np.array([x[0] for x in want], np.uint64)
+    ln = np.array([x[1] for x in want], np.uint64)
+    ty = np.array([x[2] for x in want], np.uint8)
+    got = eng.wal_scan(dev, len(data))
+    assert len(got) == len(want)
+    assert np.array_equal(got["header"], h) and np.array_equal(got["length"], ln.astype(np.uint32))
+    assert np.array_equal(got["type"], ty)
+    crc, _ = orc.crc_ranges_mt(bytes(data), h + 6, ln + 1, 8, orc.ALGO_SSE42_C if mode else orc.ALGO_PCLMUL_REF)
+    assert np.array_equal(got["crc"], crc), np.nonzero(got["crc"] != crc)[0][:10]
+    a = np.frombuffer(bytes(data), np.uint8)
+    stored = (a[h.astype(np.int64)].astype(np.uint32) | (a[h.astype(np.int64) + 1].astype(np.uint32) << 8) |
+              (a[h.astype(np.int64) + 2].astype(np.uint32) << 16) | (a[h.astype(np.int64) + 3].astype(np.uint32) << 24))
+    assert np.array_equal(got["status"], (stored != crc).astype(np.uint8))
+    cap = len(data) // 7 + 1
+    rd = lcrc.DeviceBuffer(cap * lcrc.WAL_REC_DTYPE.itemsize)
+    cnt = lcrc.DeviceBuffer(8)
+    eng.wal_scan_async(dev, len(data), rd, cap, cnt)
+    eng.sync()
+    n = int(cnt.download(np.uint64, 1)[0])
+    assert n == len(got) and rd.download(lcrc.WAL_REC_DTYPE, n).tobytes() == got.tobytes()
+    return got
+
+
+def test_wal_config3_full_size(lcrc, orc, synth, engines):
+    """BASELINE configs[3] at its bench size: the 256 MiB log of 8,192 32 KiB blocks that bench.py --config wal
+    scans (128 header-walk parts of 64 blocks, so k_wal_emit's part sums run past 64), both modes and the async
+    form. REF: the stored crc32fast values verify; C: every record is flagged. Then the same log re-sealed with
+    CRC-32C headers on the device (as the bench does) scans clean in mode C."""
+    data = _wal_file(lcrc, synth, 256 << 20, synth.SEED_WAL)
+    nblocks = (len(data) + 32767) // 32768
+    assert nblocks == 8192 and (nblocks + 63) // 64 == 128
+    got = _wal_check_scan(lcrc, orc, engines[0], data, 0)
+    assert (got["status"] == 0).all() and len(got) > 70000
+    got_c = _wal_check_scan(lcrc, orc, engines[1], data, 1)
+    assert (got_c["status"] == 1).all()
+    # re-seal every header with the raw CRC-32C (lcrc_batch_seal, {h + 6, 1 + len, -6}): a clean mode-C log
+    d = np.zeros(len(got), lcrc.DESC_DTYPE)
+    d["offset"], d["length"], d["expect_rel"] = got["header"] + 6, got["length"] + 1, -6
+    dev = lcrc.DeviceBuffer.from_host(np.frombuffer(bytes(data), np.uint8))
+    dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8))
+    engines[1].batch_seal(dev, len(data), dd, len(got))
+    engines[1].sync()
+    sealed = bytearray(dev.download(np.uint8, len(data)).tobytes())
+    got_s = _wal_check_scan(lcrc, orc, engines[1], sealed, 1)
+    assert (got_s["status"] == 0).all()
+
+
+def test_wal_just_past_64_parts_with_corruption(lcrc, orc, synth, engines):
+    """A log of 4,161 blocks (65 header-walk parts, the last block partial) with corrupted payload bytes, a
+    corrupted length field and a zeroed header: every record, crc and verdict against the oracle's walk."""
+    data = _wal_file(lcrc, synth, 4161 * 32768, 0x5EED0013)
+    data = data[:4160 * 32768 + 1000]
+    assert (len(data) + 32767) // 32768 == 4161
+    rng = np.random.default_rng(0x65)
+    want = _wal_expect(orc, data)
+    for k in rng.choice(len(want), 40, replace=False):  # payload / type bytes: checksum mismatches
+        h, n, _ = want[int(k)]
+        data[h + 6 + int(rng.integers(0, n + 1))] ^= 1 << int(rng.integers(0, 8))
+    h, n, _ = want[len(want) // 3]
+    data[h + 5] ^= 0x80  # a length field: the walk of that block stops (bad length) or wanders
+    h, n, _ = want[2 * len(want) // 3]
+    data[h:h + 7] = bytes(7)  # a zero header: type 0, length 0 ends that block's walk
+    for mode in MODES:
+        got = _wal_check_scan(lcrc, orc, engines[mode], data, mode)
+        if mode == 0:
+            assert 0 < int(got["status"].sum()) <= 45
+
+
+def test_first_queued_call_inside_a_graph_capture(lcrc, orc):
+    """A fresh context whose very first lcrc_batch_queue is made inside lcrc_graph_begin/end: the queue's side
+    streams are created by lcrc_graph_begin before the capture starts, so the capture holds the fork and join
+    and its replays give the oracle's CRCs."""
+    eng = lcrc.Engine(0, lcrc.MODE_C)
+    rng = np.random.default_rng(0xF1)
+    jobs, keep, want = [], [], []
+    for k in range(3):
+        size = (1 + k) << 20
+        data = rng.integers(0, 256, size, dtype=np.uint8)
+        n = 300
+        lens = rng.integers(0, 20000, n).astype(np.uint32)
+        offs = np.array([int(rng.integers(0, size - int(L))) for L in lens], np.uint64)
+        d = np.zeros(n, lcrc.DESC_DTYPE)
+        d["offset"], d["length"], d["expect_rel"] = offs, lens, lcrc.NO_EXPECT
+        base, dd = lcrc.DeviceBuffer.from_host(data), lcrc.DeviceBuffer.from_host(d.view(np.uint8))
+        out = lcrc.DeviceBuffer(4 * n)
+        keep += [base, dd, out]
+        jobs.append((base, size, dd, n, out, None))
+        want.append(orc.crc_ranges(data.tobytes(), offs, lens, 1))
+    eng.reserve(3 << 20)
+    arr = lcrc.gjobs(jobs)
+    g = eng.graph_capture(lambda: eng.batch_queue(arr))
+    try:
+        for _ in range(2):
+            for j in jobs:
+                j[4].zero()
+            eng.graph_launch(g)
+            eng.sync()
+            for j, w in zip(jobs, want):
+                assert np.array_equal(j[4].download(np.uint32, j[3]), w)
+    finally:
+        eng.graph_destroy(g)
+        eng.close()

@@ -1,0 +1,42 @@
+"""The N-rank path with device-bound ranks (BASELINE configs[4]) on the one-GPU test box:
+`bench.py --gpus 2` spawns two rank processes before anything touches a GPU; LCRC_RANK_DEVICE_MOD=1 (test-only)
+binds rank r to device r % device_count, so both ranks drive the box's one MI355X through their own contexts,
+streams and device buffers, exactly the code the driver's 8-GPU run executes with rank r on device r. gloo
+carries only the barrier, the max-over-ranks time and the per-rank figures (no data-path collective)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NBLK = 4096
+
+
+def test_bench_two_device_ranks(orc, synth):
+    world = 2
+    env = dict(os.environ, LCRC_RANK_DEVICE_MOD="1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--blocks", str(NBLK),
+           "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(rows) == 1, r.stdout  # ONE line, from rank 0 only
+    res = json.loads(rows[0])
+    print(json.dumps({k: res[k] for k in ("value", "n_gpus", "ms_per_step", "per_gpu")}))
+    assert res["n_gpus"] == world and res["scaling"] == "weak"
+    assert [g["rank"] for g in res["per_gpu"]] == list(range(world))
+    assert [g["device"] for g in res["per_gpu"]] == [0] * world  # rank r on device r % 1
+    assert res["roofline"] is not None and res["roofline"]["frac"] > 0
+    for g in res["per_gpu"]:
+        # each rank checksummed its own batch on the device: its fingerprint is the oracle's (masked CRC-32C)
+        data = synth.splitmix_bytes(synth.SEED_FIXED + g["rank"] * 4, NBLK * 4096)
+        want = orc.mask_array(orc.crc_ranges(data, np.arange(NBLK, dtype=np.uint64) * 4096, np.full(NBLK, 4096), 1))
+        assert g["crc_xor"] == f"{int(np.bitwise_xor.reduce(want)):08x}"
+        assert g["launch_us"] > 0 and 0 < g["frac"] < 1.2  # each rank's own launch-carried HIP events
+    assert len({g["crc_xor"] for g in res["per_gpu"]}) == world
+    # the aggregate is all ranks' bytes over the slowest rank's time
+    assert abs(res["value"] - world * NBLK * 4096 / (res["ms_per_step"] / 1e3) / 2 ** 30) <= 0.01 * res["value"] + 0.02

@@ -448,3 +448,19 @@ def test_snappy_frames_device_all_element_forms(lcrc, orc, engines):
         if w_ is not None:
             assert g_ == w_
     assert sum(w is None for w in want) > 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("compression", [0, 1])
+def test_table_scan_long_filter_policy_name(lcrc, orc, engines, compression):
+    """A filter policy name longer than the device-only scan's metaindex key (124 B): read_meta opens such a
+    table (table.rs:86-112), so the synchronous lcrc_table_scan leaves it to the host-assisted walk instead of
+    failing -- the same blocks, crcs and statuses as the oracle's walk, the filter block found."""
+    name = "leveldb.LongFilterPolicy." + "x" * 150
+    f, _ = orc.table_build(_kvs(2500, 31 + compression), compression=compression, filter_name=name,
+                           filter_block=os.urandom(200))
+    got, err = _scan(lcrc, engines[lcrc.MODE_REF], f, name)
+    want, werr = orc.table_scan_expect(f, name)
+    assert err is None and werr is None
+    assert _as_tuples(got) == want
+    assert (got["kind"] == 1).sum() == 1
