@@ -52,6 +52,9 @@ NBUF = 4
 QMAX = 32  # batches per queued launch (MAX_QJOBS in lcrc_kernels.hip)
 MIXED_QUEUE = 1  # mixed config: steps per lcrc_batch_queue submission (1: one lcrc_batch per step)
 WAL_QUEUE = 1  # wal config: scans per lcrc_wal_scan_queue submission (1: one lcrc_wal_scan_async per step)
+WAL_KERNELS = 4  # lcrc_wal_scan_async: header walk, record emit, window pass, range pass
+TABLE_KERNELS = 15  # lcrc_table_scan_async: open, count, scan x2, emit, windows, blocks, finish, scan x2, decode,
+#                    chunk crcs, chunk check, content, final
 
 
 def parse(argv=None):
@@ -161,11 +164,12 @@ def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
     `prepare(first, count)` returns the submissions for steps first .. first+count-1 as (submit, launches,
     steps[, engine]) tuples (argument marshalling done before the clock starts). The wall clock covers all K
-    steps. kernel_events (the fixed config's fast path): the first submission's launch and every engine's last
-    one carry the events themselves (lcrc_timer_kernels -> hipExtLaunchKernelGGL), and the GPU clock runs from
-    the first launch's start to the latest end (lcrc_timer_span): every launch of the timed region, with no host
-    latency and no marker packet in between. Otherwise the clock is HIP events on the first engine's stream,
-    from the end of the first submission's work (an event enqueued behind it) over submissions 2..n.
+    steps. kernel_events: the first submission's first launch and every engine's last submission's launches carry
+    the events themselves (lcrc_timer_kernels -> hipExtLaunchKernelGGL), and the GPU clock runs from the first
+    launch's start to the latest end (lcrc_timer_span): every launch of the timed region, with no host latency and
+    no marker packet in between. Otherwise the clock is HIP events on the first engine's stream, from the end of
+    the first submission's work (an event enqueued behind it) over submissions 2..n, every engine joined before
+    the stop event.
     Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock
     covers)."""
     carried = bool(engines) and kernel_events
@@ -218,8 +222,12 @@ def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
     elapsed = time.perf_counter() - t0
     if carried:
         gpu_ms = span(first, last)
+    elif bool(engines) and len(subs) > 1:
+        for e in engines[1:]:  # the stop event closes over every engine's last step (lcrc_ctx_join)
+            engines[0].join(e)
+        gpu_ms = engines[0].timer_stop()
     else:
-        gpu_ms = engines[0].timer_stop() if (bool(engines) and len(subs) > 1) else None
+        gpu_ms = None
     dist.barrier()
     first = 0 if carried else 1
     cov_launches = sum(sub[1] for sub in subs[first:])
@@ -241,6 +249,23 @@ def single_launches(w, eng, count=12):
             us.append(ms * 1e3)
     eng.timer_kernels(2)
     return sorted(us)
+
+
+def timing_text(w, timers, one_stream):
+    kps = w.cfg.get("kernels_per_step", 1)
+    if w.kernel_events:
+        return ("HIP events carried by the launches themselves (hipExtLaunchKernelGGL): the first timed launch's start to "
+                "the last one's end, / the steps (back to back, dispatch gaps included" +
+                (f"; a step is {kps} dependent kernels, so this is the whole pipeline per step" if kps > 1 else "") +
+                (f"; {len(timers)} streams: consecutive steps overlap, the next one's workgroups filling the CUs this "
+                 "one's tail leaves, so this is the per-step rate of the stream of steps, below any single step's "
+                 "duration)" if len(timers) > 1 else ")"))
+    if one_stream:
+        return ("HIP events on the engine stream: from the end of the timed region's first submission to its end, / the "
+                "launches in between (back to back, dispatch gaps included)")
+    return ("HIP events on the first engine's stream from the end of the first step to the end of the timed region "
+            f"(every stream joined), / steps; with {len(timers)} streams the steps overlap, so this is wall per step of "
+            "the whole pipeline, not one kernel's duration")
 
 
 def aggregate_gibs(bytes_per_step, steps, world, elapsed_max):
@@ -279,8 +304,10 @@ class Workload:
     device's CRCs of that sample; xor(): xor of the device CRCs of step 0 (per-rank shard fingerprint)."""
 
     def __init__(self, run, nbytes, cfg, launches=None, sample=None, crcs=None, per_step_sync=False, engines=None,
-                 kernel_events=False):
+                 kernel_events=False, kernels_per_step=1):
         self.run, self.nbytes, self.cfg = run, nbytes, cfg
+        # kernel launches one step makes (the profile summary recomputes the line's measure from the kernel trace)
+        self.cfg["kernels_per_step"] = kernels_per_step
         self.launches = launches or (lambda count: count)
         self.sample, self.crcs = sample, crcs
         self.per_step_sync = per_step_sync
@@ -417,7 +444,8 @@ def workload_mixed(m, synth, engs, rank, device, args):
 
     cfg = {"workload": "SSTable file, block sizes 256 B-64 KiB zipf(1.1) (BASELINE configs[2])",
            "blocks": int(len(sizes)), "file_bytes": int(total), "mean_block": float(sizes.mean()), "submission": sub}
-    return Workload(run, int(lens.sum()), cfg, launches, ("ranges", data, offs, lens), crcs)
+    return Workload(run, int(lens.sum()), cfg, launches, ("ranges", data, offs, lens), crcs,
+                    kernels_per_step=1 if os.environ.get("LCRC_GENERAL") == "ranges" else 2, kernel_events=q == 1)
 
 
 def workload_wal(m, synth, engs, rank, device, args):
@@ -454,12 +482,15 @@ def workload_wal(m, synth, engs, rank, device, args):
     if (first["status"] != 0).any():
         raise RuntimeError("wal bench: a freshly written log has a record flagged as corrupt")
 
+    # two copies of the log, alternated per step: 2 x 268 MB > the 256 MiB Infinity Cache, so every scan reads HBM
+    devs = [dev, m.DeviceBuffer.from_host(data, device)]
     q = args.queue
     if q == 1:
         def run(first_, count):  # records and their count stay on the device
             for i in range(first_, first_ + count):
                 k = i % len(engs)
-                engs[k].wal_scan_async(dev, len(data), recs[k], maxr, counts[k])
+                engs[k].wal_scan_async(devs[i % 2], len(data), recs[k], maxr, counts[k])
+        run.keep = devs
         launches = None
         sub = f"one lcrc_wal_scan_async per step, rotated over {len(engs)} streams"
     else:  # lcrc_wal_scan_queue: q scans per submission (header walks of all first, window passes back to back)
@@ -470,18 +501,20 @@ def workload_wal(m, synth, engs, rank, device, args):
             subs = []
             for g, (i0, n) in enumerate(groups(first_, count, q)):
                 k = g % len(engs)
-                arr = m.wjobs([(dev, len(data), qrecs[j], maxr, qcounts[j]) for j in range(n)])
+                arr = m.wjobs([(devs[j % 2], len(data), qrecs[j], maxr, qcounts[j]) for j in range(n)])
                 subs.append((lambda e=engs[k], a=arr: e.wal_scan_queue(a), n, n, k))
             return subs
         run.prepares = True
+        run.keep = devs
         launches = lambda count: count  # noqa: E731  (one window pass per step)
         sub = f"lcrc_wal_scan_queue of {q} scans per submission ({len(engs)} stream(s) + the context's side stream)"
 
     cfg = {"workload": "WAL: 32 KiB log blocks, records n~U[1,2^k), k~U[1,16] (BASELINE configs[3])",
            "file_bytes": int(len(data)), "records": int(len(first)), "bytes_counted": "sum(1+len)",
-           "submission": sub}
+           "copies_rotated": 2, "submission": sub}
     sample = ("ranges_raw", data, h + 6, first["length"].astype(np.uint64) + 1)
-    return Workload(run, covered, cfg, launches, sample, lambda: first["crc"].copy())
+    return Workload(run, covered, cfg, launches, sample, lambda: first["crc"].copy(), kernels_per_step=WAL_KERNELS,
+                    kernel_events=q == 1)
 
 
 def workload_table(m, synth, engs, rank, device, args):
@@ -499,6 +532,8 @@ def workload_table(m, synth, engs, rank, device, args):
     seal.batch_seal(dev, len(f), dd, len(blocks))
     seal.sync()
     seal.close()
+    # two copies of the table, alternated per step (2 x 269 MB > the 256 MiB Infinity Cache)
+    devs = [dev, m.DeviceBuffer.from_host(dev.download(np.uint8, len(f)), device)]
     # the synchronous form's results land in pinned host memory (lcrc_host_alloc_pinned), as a caller that scans
     # often would keep them: the 1.5 MB copy then runs at the PCIe rate instead of through a pageable staging copy
     pinned = m.PinnedBuffer((len(blocks) + 8) * m.TBLK_DTYPE.itemsize)
@@ -530,11 +565,12 @@ def workload_table(m, synth, engs, rank, device, args):
     if args.table_sync:
         def run(first, count):  # synchronous: one device scan, results back on the host
             for i in range(first, first + count):
-                scanners[i % len(engs)].table_scan_into(dev, len(f), out)
+                scanners[i % len(engs)].table_scan_into(devs[i % 2], len(f), out)
     elif args.graph:
         # each scanner's whole scan (14 launches) captured once in a HIP graph and replayed per step
-        graphs = [e.graph_capture(lambda e=e, r=r: e.table_scan_async(dev, len(f), r[0], cap, r[1], r[2]))
-                  for e, r in zip(scanners, res)]
+        # (graph k scans copy k % 2)
+        graphs = [e.graph_capture(lambda e=e, r=r, d=devs[k % 2]: e.table_scan_async(d, len(f), r[0], cap, r[1], r[2]))
+                  for k, (e, r) in enumerate(zip(scanners, res))]
 
         def run(first, count):
             for i in range(first, first + count):
@@ -544,15 +580,16 @@ def workload_table(m, synth, engs, rank, device, args):
         def run(first, count):  # device-only: enqueued, results, count and verdict stay on the device
             for i in range(first, first + count):
                 k = i % len(engs)
-                scanners[k].table_scan_async(dev, len(f), res[k][0], cap, res[k][1], res[k][2])
+                scanners[k].table_scan_async(devs[i % 2], len(f), res[k][0], cap, res[k][1], res[k][2])
 
-    run.keep = (pinned, scanners, res, dev)  # (a graph holds raw pointers: the file must outlive it)
+    run.keep = (pinned, scanners, res, devs)  # (a graph holds raw pointers: the files must outlive it)
     cfg = {"workload": "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)",
            "blocks": len(blocks), "file_bytes": int(len(f)), "crc": "crc-32/iso-hdlc (crc32fast), the reference's trailers",
            "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else
            "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async"}
     return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None,
-                    per_step_sync=bool(args.table_sync), engines=scanners)
+                    per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS,
+                    kernel_events=not (args.table_sync or args.graph))
 
 
 def workload_seal(m, synth, engs, rank, device, args):
@@ -581,7 +618,7 @@ def workload_seal(m, synth, engs, rank, device, args):
 
     cfg = {"workload": "writer-side trailers: 64K x 4 KiB blocks of one SSTable sealed in place",
            "blocks": len(blocks), "file_bytes": int(len(f))}
-    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg)
+    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, kernels_per_step=3, kernel_events=True)
 
 
 def workload_snappy(m, synth, engs, rank, device, args):
@@ -748,6 +785,9 @@ def main(argv=None):
         per = w.launches(1)
         prepare = lambda f, c: [(lambda i=i: w.run(i, 1), per, 1) for i in range(f, f + c)]  # noqa: E731
     timers = w.engines if w.engines else engs
+    # one batch handed over alone (fixed config): timed before the warmup, so that the timed region's launches are
+    # the last ones of the dominant kernel in a profiled run (tools/summarize_profile.py)
+    single = single_launches(w, engs[0]) if (w.single is not None and engs) else None
     # this rank's fingerprint (gathered over gloo with the rates below), taken before the timed region so that
     # the timed launches are the last ones of the dominant kernel in a profiled run (tools/summarize_profile.py)
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
@@ -798,22 +838,11 @@ def main(argv=None):
             "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(args.config, args.mode),
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
-            "timing": ("HIP events carried by the launches themselves (hipExtLaunchKernelGGL): first launch's "
-                       "start to the last launch's end over every launch of the timed region, / the launches (back "
-                       "to back, dispatch gaps included" +
-                       (f"; {len(timers)} streams: consecutive launches overlap, the next one's workgroups filling "
-                        "the CUs this one's tail leaves, so this is the per-launch rate of the stream of launches, "
-                        "below any single launch's duration)" if len(timers) > 1 else ")")
-                       if w.kernel_events else
-                       "HIP events on the engine stream: from the end of the timed region's first submission to "
-                       "its end, / the launches in between (back to back, dispatch gaps included)" if one_stream else
-                       "HIP events on the first engine's stream from the end of the first step to the end of the "
-                       f"timed region, / steps; with {len(timers)} streams the steps overlap, so this is wall per "
-                       "step of the whole pipeline, not one kernel's duration"),
+            "timing": timing_text(w, timers, one_stream),
             "profile": load_profile(args.config, args.mode),
         }
-        if w.single is not None and engs:
-            one = single_launches(w, engs[0])
+        if single:
+            one = single
             med = one[len(one) // 2]
             result["roofline"]["frac_single_launch"] = round(bytes_per_launch / (med * 1e-6) / 1e9 / PEAK_GBS, 4)
             result["roofline"]["single_launch"] = {
@@ -821,7 +850,7 @@ def main(argv=None):
                 "launch_us_max": round(one[-1], 2), "launches": len(one),
                 "frac_best": round(bytes_per_launch / (one[0] * 1e-6) / 1e9 / PEAK_GBS, 4),
                 "timing": "one lcrc_batch_uniform launch alone on the GPU (the previous one's end waited for), its "
-                          "own start and end events; median over the launches (after the timed region)"}
+                          "own start and end events; median over the launches (before the warmup)"}
     else:
         result["roofline"] = None
     if (rank == 0 and world == 1 and not args.no_cpu_baseline and w.sample is not None

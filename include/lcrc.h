@@ -138,6 +138,10 @@ int lcrc_ctx_reserve(lcrc_ctx* ctx, uint64_t max_span);
 /* hipStream_t owned by the context (for callers that want to enqueue around it). */
 void* lcrc_ctx_stream(lcrc_ctx* ctx);
 int lcrc_ctx_sync(lcrc_ctx* ctx);
+/* Order two contexts' streams: ctx's stream waits, on the device, for everything enqueued on other's stream so
+ * far (an event; nothing synchronizes with the host). E.g. a scan on one context whose results another context
+ * consumes, or one event timer closing over several contexts' work (bench.py). */
+int lcrc_ctx_join(lcrc_ctx* ctx, lcrc_ctx* other);
 
 /* CRC of n ranges of the device buffer base[0, base_len). out_crc[i] (device) gets the CRC (masked if
  * LCRC_FLAG_MASK). out_mismatch (device, nullable, ceil(n/32) u32 words, zeroed by the call) gets bit i
@@ -340,10 +344,12 @@ int lcrc_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int lcrc_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int lcrc_memset_d(void* dst, int value, size_t bytes);
 int lcrc_device_sync(void);
-/* Event timing on the context stream (milliseconds between two recorded events). Or carried by the fast-path
- * launches themselves (lcrc_batch_uniform_queue): lcrc_timer_kernels(ctx, 0) before the first timed submission
- * (its launch records the start), lcrc_timer_kernels(ctx, 1) before the last (its launches record the end),
- * lcrc_timer_kernels(ctx, 2) disarms; no marker between launches. lcrc_timer_stop ends either form. */
+/* Event timing on the context stream (milliseconds between two recorded events). Or carried by the launches
+ * themselves (every batched device call: lcrc_batch_uniform[_queue], lcrc_batch, lcrc_batch_queue, lcrc_batch_seal,
+ * lcrc_wal_scan_async / _queue, lcrc_table_scan_async): lcrc_timer_kernels(ctx, 0) before the first timed call
+ * (its first launch records the start), lcrc_timer_kernels(ctx, 1) before the last (its launches record the end,
+ * the last one wins), lcrc_timer_kernels(ctx, 2) disarms; no marker between launches. lcrc_timer_stop ends either
+ * form. */
 int lcrc_timer_start(lcrc_ctx* ctx);
 int lcrc_timer_kernels(lcrc_ctx* ctx, int edge);
 int lcrc_timer_stop(lcrc_ctx* ctx, float* ms);

@@ -95,7 +95,7 @@ _lib = None
 ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
-    "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream",
+    "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream", "lcrc_ctx_join",
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_multi", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
     "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
@@ -168,6 +168,7 @@ def lib():
     sig("lcrc_memset_d", i32, vp, i32, sz)
     sig("lcrc_device_sync", i32)
     sig("lcrc_timer_start", i32, vp)
+    sig("lcrc_ctx_join", i32, vp, vp)
     sig("lcrc_timer_kernels", i32, vp, i32)
     sig("lcrc_timer_stop", i32, vp, ctypes.POINTER(ctypes.c_float))
     sig("lcrc_timer_span", i32, vp, vp, ctypes.POINTER(ctypes.c_float))
@@ -585,6 +586,10 @@ class Engine:
     @staticmethod
     def graph_destroy(graph):
         lib().lcrc_graph_destroy(graph)
+
+    def join(self, other):
+        """lcrc_ctx_join: this engine's stream waits (on the device) for the work enqueued on other's so far."""
+        _check(lib().lcrc_ctx_join(self.ctx, other.ctx), "lcrc_ctx_join")
 
     def timer_start(self):
         _check(lib().lcrc_timer_start(self.ctx), "lcrc_timer_start")

@@ -21,6 +21,8 @@
 #include "lcrc_table.h"
 
 extern "C" {
+void lcrc_launch_events_begin(hipEvent_t start, hipEvent_t stop);
+void lcrc_launch_events_end(bool* started, bool* stopped);
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
                                uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
                                const uint32_t* expected, uint32_t* mismatch, hipStream_t st,
@@ -147,6 +149,7 @@ struct lcrc_ctx {
   DevBuf<uint32_t> win2;      // lcrc_batch_queue: the second window buffer (batches alternate)
   hipStream_t side = nullptr, side2 = nullptr;  // the two lanes of the queued calls (lcrc_*_queue)
   hipEvent_t q_fork = nullptr, q_join = nullptr, q_join2 = nullptr;
+  hipEvent_t x_join = nullptr;  // lcrc_ctx_join: this context's stream as seen by another context
   DevBuf<uint8_t> chunk[2];   // host-resident pipeline staging
   DevBuf<uint32_t> hexp[2];   // expected values per chunk
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
@@ -201,6 +204,30 @@ struct lcrc_ctx {
 };
 
 namespace {
+
+// Kernel-carried timing (lcrc_timer_kernels) for the multi-kernel calls: while the OUTERMOST timed API call of a
+// context runs, every launch it makes carries the context's armed events (the first launch the start, each launch
+// the stop: the last one wins). Nested API calls (lcrc_batch_seal -> lcrc_batch) share the outer scope.
+thread_local int g_tk_depth = 0;
+struct TkScope {
+  lcrc_ctx* c;
+  bool outer;
+  explicit TkScope(lcrc_ctx* ctx) : c(ctx), outer(ctx && g_tk_depth == 0) {
+    ++g_tk_depth;
+    if (outer) lcrc_launch_events_begin(c->tk_start ? c->t0 : nullptr, c->tk_stop ? c->t1 : nullptr);
+  }
+  ~TkScope() {
+    --g_tk_depth;
+    if (!outer) return;
+    bool started = false, stopped = false;
+    lcrc_launch_events_end(&started, &stopped);
+    if (started) {
+      c->tk_any = true;
+      c->tk_start = false;
+    }
+    if (stopped) c->tk_end = true;
+  }
+};
 
 // The per-mode constant image (TAB_* layout, lcrc_device.h), uploaded to a new device allocation.
 int upload_tables(int mode, uint32_t** d_tab) {
@@ -315,7 +342,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
       return bail(fail_hip(e, "hipEventCreate"));
   // (the queue lanes' streams are created on first use, ensure_lanes: every stream a context creates takes one of
   // the process's few hardware queues, and two contexts' main streams sharing one serialize)
-  for (hipEvent_t* ev : {&ctx->q_fork, &ctx->q_join, &ctx->q_join2})
+  for (hipEvent_t* ev : {&ctx->q_fork, &ctx->q_join, &ctx->q_join2, &ctx->x_join})
     if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bail(fail_hip(e, "hipEventCreate"));
   if ((e = hipHostMalloc(&ctx->h_count, 8 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
     return bail(fail_hip(e, "hipHostMalloc"));
@@ -344,7 +371,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
     if (l) (void)hipStreamSynchronize(l);
   ctx->win.release();
   ctx->win2.release();
-  for (hipEvent_t ev : {ctx->q_fork, ctx->q_join, ctx->q_join2})
+  for (hipEvent_t ev : {ctx->q_fork, ctx->q_join, ctx->q_join2, ctx->x_join})
     if (ev) (void)hipEventDestroy(ev);
   for (int i = 0; i < 2; ++i) {
     ctx->chunk[i].release();
@@ -405,6 +432,15 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
 
 void* lcrc_ctx_stream(lcrc_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+// ctx's stream waits (on the device) for everything enqueued on other's stream so far
+int lcrc_ctx_join(lcrc_ctx* ctx, lcrc_ctx* other) {
+  if (!ctx || !other) return LCRC_EINVAL;
+  if (ctx == other) return LCRC_OK;
+  HIPCHK(hipEventRecord(other->x_join, other->stream));
+  HIPCHK(hipStreamWaitEvent(ctx->stream, other->x_join, 0));
+  return LCRC_OK;
+}
+
 int lcrc_ctx_sync(lcrc_ctx* ctx) {
   if (!ctx) return LCRC_EINVAL;
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -450,6 +486,7 @@ int lcrc_ctx_reserve(lcrc_ctx* ctx, uint64_t max_span) {
 #endif
 int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
                uint32_t* out_crc, uint32_t* out_mismatch, void* stream) {
+  TkScope tk_scope(ctx);
   if (!ctx || (n && (!descs || !out_crc || !base))) return LCRC_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
@@ -488,6 +525,7 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
 // lanes before anything enqueued after it: a fork and a join, so the call behaves as its batches would one
 // after another on `stream` (and captures into a graph as two branches).
 int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* stream) {
+  TkScope tk_scope(ctx);
   if (!ctx || (njobs && !jobs)) return LCRC_EINVAL;
   for (size_t k = 0; k < njobs; ++k)
     if (jobs[k].n && (!jobs[k].descs || !jobs[k].out_crc || !jobs[k].base)) return LCRC_EINVAL;
@@ -853,6 +891,7 @@ int lcrc_batch_multi(lcrc_ctx* const* ctxs, int nctx, const uint8_t* base, uint6
 
 int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, lcrc_wal_rec* recs, size_t max_recs,
                         uint64_t* n_recs, void* stream) {
+  TkScope tk_scope(ctx);
   if (!ctx || !n_recs || (file_len && !file) || (max_recs && !recs)) return LCRC_EINVAL;
   if (file_len >= LCRC_WAL_MAX_FILE) return LCRC_EINVAL;  // record indices and counts are 32-bit on the device
   int rc = set_device(ctx);
@@ -902,6 +941,7 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
 // `stream` before the call's end. Measured (config 4, 5 logs per call): 3.1K GiB/s against 3.4K for two
 // contexts taking alternate logs -- the lanes' fork and join cost ~35 us per call and an odd log runs alone.
 int lcrc_wal_scan_queue(lcrc_ctx* ctx, const lcrc_wjob* jobs, size_t njobs, void* stream) {
+  TkScope tk_scope(ctx);
   if (!ctx || (njobs && !jobs)) return LCRC_EINVAL;
   for (size_t k = 0; k < njobs; ++k)
     if (!jobs[k].n_recs || (jobs[k].file_len && !jobs[k].file) || (jobs[k].max_recs && !jobs[k].recs) ||
@@ -1280,6 +1320,7 @@ int lcrc_table_scan_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blo
 
 int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
                           lcrc_tblk* blocks, size_t max_blocks, uint64_t* n_blocks, uint32_t* status, void* stream) {
+  TkScope tk_scope(ctx);
   if (!ctx || !n_blocks || !status || (file_len && !file) || (max_blocks && !blocks)) return LCRC_EINVAL;
   lcrc_tscan_key key;
   memset(&key, 0, sizeof(key));
@@ -1556,6 +1597,7 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
 // ---- writer side: batch seal ----
 int lcrc_batch_seal(lcrc_ctx* ctx, uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
                     uint32_t* out_crc, void* stream) {
+  TkScope tk_scope(ctx);
   if (!ctx || (n && (!descs || !base))) return LCRC_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;

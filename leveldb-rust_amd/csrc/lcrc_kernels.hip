@@ -2865,7 +2865,40 @@ __global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, u
 // ---------------------------------------------------------------------------------------------------
 // host-side launchers (called from lcrc_api.cpp)
 // ---------------------------------------------------------------------------------------------------
+// Kernel-carried timing for every launcher (lcrc_timer_kernels on the general path, the WAL and table scans):
+// while an API call of a timed context runs (TkScope, lcrc_api.cpp), its launches carry the context's events --
+// the first launch records the start at its own start, every launch the stop at its end (the last one wins) --
+// through hipExtLaunchKernelGGL, so no marker packet sits between launches.
+thread_local hipEvent_t lcrc_tl_ev_start = nullptr, lcrc_tl_ev_stop = nullptr;
+thread_local bool lcrc_tl_ev_started = false, lcrc_tl_ev_stopped = false;
+#define LCRC_LAUNCH(kern, grid, block, shmem, st, ...)                                                       \
+  do {                                                                                                       \
+    hipEvent_t ev_s_ = lcrc_tl_ev_start, ev_e_ = lcrc_tl_ev_stop;                                            \
+    if (ev_s_ || ev_e_) {                                                                                    \
+      hipExtLaunchKernelGGL(kern, grid, block, shmem, st, ev_s_, ev_e_, 0, __VA_ARGS__);                    \
+      if (ev_s_) lcrc_tl_ev_started = true;                                                                  \
+      if (ev_e_) lcrc_tl_ev_stopped = true;                                                                  \
+      lcrc_tl_ev_start = nullptr;                                                                            \
+    } else {                                                                                                 \
+      hipLaunchKernelGGL(kern, grid, block, shmem, st, __VA_ARGS__);                                         \
+    }                                                                                                        \
+  } while (0)
+
 extern "C" {
+
+// the calling thread's launches carry (start, stop) until lcrc_launch_events_end; returns nothing
+void lcrc_launch_events_begin(hipEvent_t start, hipEvent_t stop) {
+  lcrc_tl_ev_start = start;
+  lcrc_tl_ev_stop = stop;
+  lcrc_tl_ev_started = lcrc_tl_ev_stopped = false;
+}
+// clears them; *started / *stopped: whether a launch recorded the start / the stop
+void lcrc_launch_events_end(bool* started, bool* stopped) {
+  *started = lcrc_tl_ev_started;
+  *stopped = lcrc_tl_ev_stopped;
+  lcrc_tl_ev_start = lcrc_tl_ev_stop = nullptr;
+  lcrc_tl_ev_started = lcrc_tl_ev_stopped = false;
+}
 
 #ifdef LCRC_PROBE_CLOCK
 // effective shader clock (MHz) of the last k_windows launch: median over workgroups of
@@ -2911,10 +2944,10 @@ hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, u
     hipExtLaunchKernelGGL(lcrc_dev::k_windows<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, t_start, t_stop, 0,
                           base, span, nreg, gtab, out, nblk, fin, flags, expected, mismatch);
   else if (final_mode)
-    hipLaunchKernelGGL(lcrc_dev::k_windows<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg, gtab,
+    LCRC_LAUNCH(lcrc_dev::k_windows<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg, gtab,
                        out, nblk, fin, flags, expected, mismatch);
   else
-    hipLaunchKernelGGL(lcrc_dev::k_windows<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg,
+    LCRC_LAUNCH(lcrc_dev::k_windows<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, span, nreg,
                        gtab, out, nblk, fin, flags, expected, mismatch);
   return hipGetLastError();
 }
@@ -2953,14 +2986,14 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
     hipExtLaunchKernelGGL(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, t_start, t_stop, 0, a, gtab,
                           fin, flags);
   else
-    hipLaunchKernelGGL(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, a, gtab, fin, flags);
+    LCRC_LAUNCH(lcrc_dev::k_windows_q, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, a, gtab, fin, flags);
   return hipGetLastError();
 }
 
 // ---- asynchronous table scan (lcrc_table_scan_async) ----
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                lcrc_tscan_dev* st, hipStream_t s) {
-  hipLaunchKernelGGL(lcrc_dev::k_ts_open, dim3(1), dim3(64), 0, s, file, file_len, *key, cap, st);
+  LCRC_LAUNCH(lcrc_dev::k_ts_open, dim3(1), dim3(64), 0, s, file, file_len, *key, cap, st);
   return hipGetLastError();
 }
 // grid: a bound on the restart segments (the workgroups past the device count return at once)
@@ -2968,7 +3001,7 @@ hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lc
                                 uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero,
                                 hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
-  hipLaunchKernelGGL(lcrc_dev::k_ts_count, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
+  LCRC_LAUNCH(lcrc_dev::k_ts_count, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
                      count, flag, zero, nzero);
   return hipGetLastError();
 }
@@ -2976,7 +3009,7 @@ hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tsca
                                const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t vcap, uint64_t bound, hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
-  hipLaunchKernelGGL(lcrc_dev::k_ts_emit, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
+  LCRC_LAUNCH(lcrc_dev::k_ts_emit, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
                      pos, fpos, out, descs, cap, vcap);
   return hipGetLastError();
 }
@@ -2985,13 +3018,13 @@ hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t*
                                  uint8_t* fstatus, const lcrc_tscan_dev* st, const uint32_t* gtab, uint32_t flags,
                                  hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_ts_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, blk, n, crc, mismatch,
+  LCRC_LAUNCH(lcrc_dev::k_ts_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, blk, n, crc, mismatch,
                      file, frames, size, nchunks, fstatus, st, gtab, flags);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, uint32_t* status_out,
                                hipStream_t s) {
-  hipLaunchKernelGGL(lcrc_dev::k_ts_final, dim3(1), dim3(64), 0, s, st, blk, n_out, status_out);
+  LCRC_LAUNCH(lcrc_dev::k_ts_final, dim3(1), dim3(64), 0, s, st, blk, n_out, status_out);
   return hipGetLastError();
 }
 
@@ -3012,10 +3045,10 @@ hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint6
   uint64_t need = (n + per_wg - 1) / per_wg;
   int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   if (uniform)
-    hipLaunchKernelGGL(lcrc_dev::k_blocks<true>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs, n,
+    LCRC_LAUNCH(lcrc_dev::k_blocks<true>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs, n,
                        ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev, recs);
   else
-    hipLaunchKernelGGL(lcrc_dev::k_blocks<false>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs,
+    LCRC_LAUNCH(lcrc_dev::k_blocks<false>, dim3(g), dim3(lcrc_dev::B_THREADS), 0, st, base, base_len, descs,
                        n, ustride, ulen, uexp, win, gtab, init, xorout, flags, out, mismatch, n_dev, recs);
   return hipGetLastError();
 }
@@ -3033,10 +3066,10 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
   const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
   const uint32_t* inv = gtab + TAB_INV;
   if (uniform)
-    hipLaunchKernelGGL(lcrc_dev::k_ranges<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, base_len, descs, n,
+    LCRC_LAUNCH(lcrc_dev::k_ranges<true>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, base_len, descs, n,
                        ustride, ulen, uexp, gtab, inv, x4096, poly, init, xorout, flags, out, mismatch, n_dev, recs);
   else
-    hipLaunchKernelGGL(lcrc_dev::k_ranges<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, base_len, descs,
+    LCRC_LAUNCH(lcrc_dev::k_ranges<false>, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, base, base_len, descs,
                        n, ustride, ulen, uexp, gtab, inv, x4096, poly, init, xorout, flags, out, mismatch, n_dev, recs);
   return hipGetLastError();
 }
@@ -3049,11 +3082,11 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  uint64_t* n_out, hipStream_t st) {
   const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
   if (nparts)
-    hipLaunchKernelGGL(lcrc_dev::k_wal_parse<LCRC_WAL_WIN>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
+    LCRC_LAUNCH(lcrc_dev::k_wal_parse<LCRC_WAL_WIN>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
                        slots, stops, local, part);
   const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
   const uint64_t g = (nt + 255) / 256;
-  hipLaunchKernelGGL(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
+  LCRC_LAUNCH(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
                      stops, local, part, recs, descs, max_recs, n_total, n_out);
   return hipGetLastError();
 }
@@ -3073,8 +3106,8 @@ hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t 
     gp = std::max<uint64_t>(gp, (j.nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB);
     ge = std::max<uint64_t>(ge, (j.nblocks * lcrc_dev::WAL_SLOTS + 255) / 256);
   }
-  hipLaunchKernelGGL(lcrc_dev::k_wal_parse_q<LCRC_WAL_WIN>, dim3((unsigned)gp, m), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(lcrc_dev::k_wal_emit_q, dim3((unsigned)ge, m), dim3(256), 0, st, a);
+  LCRC_LAUNCH(lcrc_dev::k_wal_parse_q<LCRC_WAL_WIN>, dim3((unsigned)gp, m), dim3(64), 0, st, a);
+  LCRC_LAUNCH(lcrc_dev::k_wal_emit_q, dim3((unsigned)ge, m), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -3082,7 +3115,7 @@ hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* fra
                                    uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
                                    hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_snappy_size, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, frames, n, size,
+  LCRC_LAUNCH(lcrc_dev::k_snappy_size, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, frames, n, size,
                      nchunks, status, maxes, n_dev);
   return hipGetLastError();
 }
@@ -3093,8 +3126,8 @@ hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, u
                              uint64_t* part, const uint64_t* n_dev, hipStream_t st) {
   const uint64_t g = n_dev ? n / 256 + 1 : (n + 255) / 256;
   if (g == 0) return hipMemsetAsync(out_a, 0, 8, st) == hipSuccess ? hipMemsetAsync(out_b, 0, 8, st) : hipErrorUnknown;
-  hipLaunchKernelGGL(lcrc_dev::k_scan2_local, dim3((unsigned)g), dim3(256), 0, st, a, b, n, out_a, out_b, part, n_dev);
-  hipLaunchKernelGGL(lcrc_dev::k_scan2_add, dim3((unsigned)g), dim3(256), 0, st, n, out_a, out_b, part, n_dev);
+  LCRC_LAUNCH(lcrc_dev::k_scan2_local, dim3((unsigned)g), dim3(256), 0, st, a, b, n, out_a, out_b, part, n_dev);
+  LCRC_LAUNCH(lcrc_dev::k_scan2_add, dim3((unsigned)g), dim3(256), 0, st, n, out_a, out_b, part, n_dev);
   return hipGetLastError();
 }
 
@@ -3110,7 +3143,7 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
   const uint32_t in_lim = max_in + 4 < SN_MAX ? (max_in + 4 + 15) & ~15u : SN_MAX;
   const uint32_t out_cap = max_out < SN_MAX ? (max_out + 15) & ~15u : SN_MAX;
   const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
-  hipLaunchKernelGGL(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
+  LCRC_LAUNCH(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
                      chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, ts, ts_out_cap,
                      ts_chunk_cap);
   return hipGetLastError();
@@ -3119,7 +3152,7 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st) {
   if (nch_bound == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_snappy_check, dim3((unsigned)((nch_bound + 255) / 256)), dim3(256), 0, st, crc, cexp,
+  LCRC_LAUNCH(lcrc_dev::k_snappy_check, dim3((unsigned)((nch_bound + 255) / 256)), dim3(256), 0, st, crc, cexp,
                      cframe, nch, status);
   return hipGetLastError();
 }
@@ -3130,10 +3163,10 @@ hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uin
   if (nres == 0) return hipSuccess;
   const dim3 g((nres + 255) / 256);
   if (pass2)
-    hipLaunchKernelGGL(lcrc_dev::k_idx_parse<true>, g, dim3(256), 0, st, d, len, nres, file_len, count, flag, pos, out,
+    LCRC_LAUNCH(lcrc_dev::k_idx_parse<true>, g, dim3(256), 0, st, d, len, nres, file_len, count, flag, pos, out,
                        descs);
   else
-    hipLaunchKernelGGL(lcrc_dev::k_idx_parse<false>, g, dim3(256), 0, st, d, len, nres, file_len, count, flag, pos, out,
+    LCRC_LAUNCH(lcrc_dev::k_idx_parse<false>, g, dim3(256), 0, st, d, len, nres, file_len, count, flag, pos, out,
                        descs);
   return hipGetLastError();
 }
@@ -3141,7 +3174,7 @@ hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uin
 hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                   const uint8_t* file, lcrc_desc_dev* frames, const uint64_t* n_dev, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_tbl_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, crc, mismatch,
+  LCRC_LAUNCH(lcrc_dev::k_tbl_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, crc, mismatch,
                      file, frames, n_dev);
   return hipGetLastError();
 }
@@ -3149,21 +3182,21 @@ hipError_t lcrc_launch_tbl_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t
 hipError_t lcrc_launch_tbl_content(lcrc_tblk_dev* blk, uint64_t n, const uint8_t* fstatus, uint32_t* unsorted,
                                    uint32_t gen, const uint64_t* n_dev, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_tbl_content, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, fstatus,
+  LCRC_LAUNCH(lcrc_dev::k_tbl_content, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, blk, n, fstatus,
                      unsorted, gen, n_dev);
   return hipGetLastError();
 }
 
 hipError_t lcrc_launch_gather_u8(const uint8_t* base, const uint64_t* pos, uint64_t n, uint8_t* out, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_gather_u8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, pos, n, out);
+  LCRC_LAUNCH(lcrc_dev::k_gather_u8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, pos, n, out);
   return hipGetLastError();
 }
 
 hipError_t lcrc_launch_store_crc(uint8_t* base, uint64_t base_len, const lcrc_desc_dev* descs, const uint32_t* crc, uint64_t n,
                                  hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lcrc_dev::k_store_crc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, base_len, descs,
+  LCRC_LAUNCH(lcrc_dev::k_store_crc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, base_len, descs,
                      crc, n);
   return hipGetLastError();
 }

@@ -82,20 +82,39 @@ def main(outdir, rnd, config, mode):
             # otherwise from the end of the first launch to the end of the last), dispatch gaps included
             nl = line["roofline"].get("launches") or 0
             trace = find(os.path.join(outdir, "trace"), "*kernel_trace.csv")
+            kps = line["config"].get("kernels_per_step") or 0
+            steps = line.get("steps") or 0
             if trace and nl:
-                ts = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace))
+                rows = list(csv.DictReader(open(trace)))
+                ts = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
                             if r["Kernel_Name"].split("(")[0] == dom[0])
                 kernel_events = "carried by the launches" in line["roofline"].get("timing", "")
-                timed = ts[-(nl + 1):] if len(ts) > nl else []
                 span = None
-                if kernel_events and len(ts) >= nl:  # first launch's start to the latest end (several streams)
+                if kps > 1 and steps > 1:
+                    # a step is kps dependent kernels. The timed steps are the last steps * kps dispatches in host
+                    # submission order (Dispatch_Id), the first step's kernels the first kps of them. Kernel-carried
+                    # events: the first timed launch's start to the last end, / steps; marker events: the end of the
+                    # first step to the last end (every stream joined), / (steps - 1).
+                    order = sorted(rows, key=lambda r: int(r["Dispatch_Id"]))
+                    timed = order[-steps * kps:]
+                    names = [r["Kernel_Name"].split("(")[0] for r in timed]
+                    if len(timed) == steps * kps and names.count(dom[0]) == steps:
+                        t_last = max(int(r["End_Timestamp"]) for r in timed)
+                        if kernel_events:
+                            span = (t_last - int(timed[0]["Start_Timestamp"])) / 1e3 / steps
+                        else:
+                            span = (t_last - max(int(r["End_Timestamp"]) for r in timed[:kps])) / 1e3 / (steps - 1)
+                        summary["timed_kernels"] = {n: names.count(n) for n in sorted(set(names))}
+                elif kernel_events and len(ts) >= nl:  # first launch's start to the latest end (several streams)
                     span = (max(e for _, e in ts[-nl:]) - ts[-nl][0]) / 1e3 / nl
-                elif timed:
+                elif len(ts) > nl:
+                    timed = ts[-(nl + 1):]
                     span = (timed[-1][1] - timed[0][1]) / 1e3 / nl
                 if span:
                     summary["trace_launch_us"] = round(span, 3)
                     summary["trace_gap_us"] = round(span - summary["avg_us"], 3)
                     summary["frac_from_trace"] = round(bpl / (span * 1e3) / 8000.0, 4)
+                    summary["kernels_per_step"] = kps or 1
                     summary["agreement"] = round(summary["frac_from_trace"] / line["roofline"]["frac"], 4)
             summary["note"] = ("frac: the dominant kernel's average duration alone (rocprofv3 kernel trace); "
                                "frac_from_trace: the bench line's measure (its timed launches, first to last, per "
