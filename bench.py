@@ -160,19 +160,21 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
+def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False, kernels_per_step=1):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
     `prepare(first, count)` returns the submissions for steps first .. first+count-1 as (submit, launches,
     steps[, engine]) tuples (argument marshalling done before the clock starts). The wall clock covers all K
-    steps. kernel_events: the first submission's first launch and every engine's last submission's launches carry
-    the events themselves (lcrc_timer_kernels -> hipExtLaunchKernelGGL), and the GPU clock runs from the first
-    launch's start to the latest end (lcrc_timer_span): every launch of the timed region, with no host latency and
-    no marker packet in between. Otherwise the clock is HIP events on the first engine's stream, from the end of
-    the first submission's work (an event enqueued behind it) over submissions 2..n, every engine joined before
-    the stop event.
+    steps. The GPU clock (HIP events, no marker packet between launches, no host latency before the first kernel):
+      * kernel_events, one kernel per step (the fast path): the first submission's launch records the start, every
+        engine's last launch the end (lcrc_timer_kernels -> hipExtLaunchKernelGGL); the clock runs from the first
+        launch's start to the latest end (lcrc_timer_span).
+      * kernel_events, several dependent kernels per step: the first launch records the start; after the last
+        submission the first engine's stream joins every other engine (lcrc_ctx_join) and an end event follows:
+        first launch's start to the end of the last kernel of any engine.
+      * otherwise: an event behind the first submission to the joined end event (steps 2..K).
     Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock
     covers)."""
-    carried = bool(engines) and kernel_events
+    mode = "marker" if not (engines and kernel_events) else "carried" if kernels_per_step == 1 else "start"
 
     def eng_of(sub):  # the engine a submission goes to (4th element; 0 when absent)
         return sub[3] if len(sub) > 3 else 0
@@ -183,53 +185,55 @@ def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False):
         last = {}
         for k, sub in enumerate(subs):
             last[eng_of(sub)] = k
-        return first, {k: e for e, k in last.items()}
+        return first, ({k: e for e, k in last.items()} if mode == "carried" else {})
 
-    def submit(subs, marker):
-        """marker: (not carried) start the marker timer behind the first submission"""
-        first, last = arm(subs) if carried else ({}, {})
+    def submit(subs):
+        first, last = arm(subs) if mode != "marker" else ({}, {})
         for k, sub in enumerate(subs):
             if k in first:
                 engines[first[k]].timer_kernels(0)
             if k in last:
                 engines[last[k]].timer_kernels(1)
             sub[0]()
-            if marker and k == 0 and engines and len(subs) > 1:
+            if mode == "marker" and k == 0 and engines and len(subs) > 1:
                 engines[0].timer_start()
         return first, last
 
-    def span(first, last):
-        """first launch's start to the latest end of any engine's last launch (ms); engines disarmed"""
-        e0 = engines[first[0]]
-        ms = max(e0.timer_span(engines[e]) for e in last.values())
+    def finish(first, last, nsubs):
+        """the GPU ms of the submissions just made (waits for their end event); engines disarmed"""
+        if mode == "carried":
+            e0 = engines[first[0]]
+            ms = max(e0.timer_span(engines[e]) for e in last.values())
+            for e in engines:
+                e.timer_kernels(2)
+            return ms
+        if not engines or (mode == "marker" and nsubs < 2):
+            return None
+        e0 = engines[first[0]] if first else engines[0]
+        for e in engines:  # the end event closes over every engine's last kernel (lcrc_ctx_join)
+            if e is not e0:
+                e0.join(e)
+        ms = e0.timer_stop()
         for e in engines:
             e.timer_kernels(2)
         return ms
 
     if warmup:
         wsubs = prepare(0, warmup)
-        fw, lw = submit(wsubs, False)  # the warmup goes through the timed region's launch path, events included
-        if carried:
-            span(fw, lw)
+        fw, lw = submit(wsubs)  # the warmup goes through the timed region's launch path, events included
+        finish(fw, lw, len(wsubs))
     subs = prepare(warmup, steps)
     for e in engines:
         e.sync()
     dist.barrier()
     t0 = time.perf_counter()
-    first, last = submit(subs, not carried)
+    first, last = submit(subs)
+    gpu_ms = finish(first, last, len(subs))
     for e in engines:
         e.sync()
     elapsed = time.perf_counter() - t0
-    if carried:
-        gpu_ms = span(first, last)
-    elif bool(engines) and len(subs) > 1:
-        for e in engines[1:]:  # the stop event closes over every engine's last step (lcrc_ctx_join)
-            engines[0].join(e)
-        gpu_ms = engines[0].timer_stop()
-    else:
-        gpu_ms = None
     dist.barrier()
-    first = 0 if carried else 1
+    first = 1 if mode == "marker" else 0
     cov_launches = sum(sub[1] for sub in subs[first:])
     cov_steps = sum(sub[2] for sub in subs[first:])
     return dist.max(elapsed), elapsed, gpu_ms, cov_launches, cov_steps
@@ -254,8 +258,10 @@ def single_launches(w, eng, count=12):
 def timing_text(w, timers, one_stream):
     kps = w.cfg.get("kernels_per_step", 1)
     if w.kernel_events:
-        return ("HIP events carried by the launches themselves (hipExtLaunchKernelGGL): the first timed launch's start to "
-                "the last one's end, / the steps (back to back, dispatch gaps included" +
+        return ("HIP events: the first timed launch's start (an event the launch carries, hipExtLaunchKernelGGL) to " +
+                ("the last one's end (carried likewise)" if kps == 1 else
+                 "the end of the last kernel of any stream (the streams joined, then an end event)") +
+                ", / the steps (back to back, dispatch gaps included" +
                 (f"; a step is {kps} dependent kernels, so this is the whole pipeline per step" if kps > 1 else "") +
                 (f"; {len(timers)} streams: consecutive steps overlap, the next one's workgroups filling the CUs this "
                  "one's tail leaves, so this is the per-step rate of the stream of steps, below any single step's "
@@ -791,8 +797,9 @@ def main(argv=None):
     # this rank's fingerprint (gathered over gloo with the rates below), taken before the timed region so that
     # the timed launches are the last ones of the dominant kernel in a profiled run (tools/summarize_profile.py)
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
-    elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(dist, prepare, args.steps, args.warmup, timers,
-                                                                      kernel_events=w.kernel_events)
+    elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(
+        dist, prepare, args.steps, args.warmup, timers, kernel_events=w.kernel_events,
+        kernels_per_step=w.cfg.get("kernels_per_step", 1))
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
     # this rank's per-launch figure of the dominant kernel (its own HIP events; -1 when not timed on the GPU)
     launch_us = gpu_ms * 1e3 / cov_launches if (timers and gpu_ms and cov_launches) else -1.0
@@ -839,6 +846,8 @@ def main(argv=None):
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
             "timing": timing_text(w, timers, one_stream),
+            "clock": ("marker" if not w.kernel_events else
+                      "carried" if w.cfg.get("kernels_per_step", 1) == 1 else "start"),
             "profile": load_profile(args.config, args.mode),
         }
         if single:

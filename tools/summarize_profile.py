@@ -88,7 +88,9 @@ def main(outdir, rnd, config, mode):
                 rows = list(csv.DictReader(open(trace)))
                 ts = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
                             if r["Kernel_Name"].split("(")[0] == dom[0])
-                kernel_events = "carried by the launches" in line["roofline"].get("timing", "")
+                clock = line["roofline"].get("clock")
+                kernel_events = clock in ("carried", "start") if clock else \
+                    "carried by the launches" in line["roofline"].get("timing", "")
                 span = None
                 if kps > 1 and steps > 1:
                     # a step is kps dependent kernels. The timed steps are the last steps * kps dispatches in host
