@@ -60,6 +60,12 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t m, hipStream_t st);
+hipError_t lcrc_launch_wal_windows(int grid, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
+                                   const uint32_t* gtab, uint32_t* win, uint32_t* counts, uint2* slots, uint8_t* stops,
+                                   uint64_t* local, uint64_t* part, hipStream_t st);
+hipError_t lcrc_launch_wal_emit(const uint8_t* file, uint64_t nblocks, uint32_t* counts, uint2* slots, uint8_t* stops,
+                                uint64_t* local, uint64_t* part, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
+                                uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
                                    uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
                                    hipStream_t st);
@@ -201,6 +207,7 @@ struct lcrc_ctx {
   void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
   uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
   int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan (LCRC_TS_BLOCKS_DIV, measurement)
+  bool wal_fused = true;  // WAL scan: header walk inside the window pass (LCRC_WAL_FUSED=0: the separate k_wal_parse)
 };
 
 namespace {
@@ -358,6 +365,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   ctx->x4096 = lcrc::x8n(4096, poly);
   if (const char* g = getenv("LCRC_GENERAL")) ctx->general = !strcmp(g, "ranges") ? 1 : !strcmp(g, "blocks") ? 2 : 0;
   if (const char* g = getenv("LCRC_TS_BLOCKS_DIV")) ctx->ts_blocks_div = std::max(1, atoi(g));
+  if (const char* g = getenv("LCRC_WAL_FUSED")) ctx->wal_fused = strcmp(g, "0") != 0;
   *out = ctx;
   return LCRC_OK;
 }
@@ -448,6 +456,9 @@ int lcrc_ctx_sync(lcrc_ctx* ctx) {
 }
 
 static size_t lcrc_wal_queue_max() { return 16; }  // MAX_WJOBS in lcrc_kernels.hip
+#ifndef LCRC_WAL_GRID_DIV
+#define LCRC_WAL_GRID_DIV 1  // the WAL scan's range pass: the full grid (half: 100.6 vs 96.2 us per launch, same 2-stream wall)
+#endif
 #ifndef LCRC_WALQ_WG_PER_CU
 #define LCRC_WALQ_WG_PER_CU 2  // range-pass workgroups per CU beside a window pass (its 76 KiB workgroup must fit)
 #endif
@@ -910,10 +921,22 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   uint64_t* n_total = ctx->wal_offsets.p;
   uint64_t* local = ctx->wal_offsets.p + 1;
   uint64_t* part = ctx->wal_offsets.p + 1 + nblocks;
-  // One stream: the header walk, the records at their file-order positions, the window pass over the whole
-  // file, then one k_blocks over all records (the log format stores the raw crc: no mask) that also stores
-  // each record's crc and verdict. (Run beside the window pass on a second stream the latency-bound header
-  // walk slowed down ~3x and ended later.)
+  // The default (window/range path): ONE streaming pass computes every 256 B window value AND walks the record
+  // headers on the data it holds (k_wal_windows + k_wal_part), then the records at their file-order positions
+  // (k_wal_emit), then one k_blocks over all records (the log format stores the raw crc: no mask) that also
+  // stores each record's crc and verdict. (The header walk as its own kernel -- k_wal_parse, a dependent chain of
+  // memory round trips per 32 KiB block -- took ~20 us alone and ~50 us beside another scan's window pass.)
+  // LCRC_WAL_FUSED=0 (measurement), the one-pass range kernel or max_recs 0: the separate header walk first.
+  if (max_recs && ctx->general != 1 && ctx->wal_fused) {
+    HIPCHK(lcrc_launch_wal_windows(ctx->grid_a, file, file_len, nblocks, ctx->d_tab, ctx->win.p, ctx->wal_counts.p,
+                                   ctx->wal_slots.p, ctx->wal_stops.p, local, part, st));
+    HIPCHK(lcrc_launch_wal_emit(file, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local, part,
+                                (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, n_total, n_recs, st));
+    HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_WAL_GRID_DIV, file, file_len, ctx->wal_descs.p, max_recs, 0, 0,
+                              nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr,
+                              n_total, (lcrc_wal_rec_dev*)recs, st));
+    return LCRC_OK;
+  }
   HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local,
                                part, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, n_total, n_recs, st));
   if (max_recs && ctx->general == 1) {
@@ -923,9 +946,6 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   } else if (max_recs) {
     HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
                                st));
-#ifndef LCRC_WAL_GRID_DIV
-#define LCRC_WAL_GRID_DIV 1  // the full grid here (half: 100.6 vs 96.2 us per launch, the same 2-stream wall)
-#endif
     HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_WAL_GRID_DIV, file, file_len, ctx->wal_descs.p, max_recs, 0, 0, nullptr,
                               ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr, n_total,
                               (lcrc_wal_rec_dev*)recs, st));

@@ -1807,6 +1807,216 @@ __global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
                 J.n_out, blockIdx.x);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// k_wal_windows: the WAL scan's window pass and its header walk in ONE streaming pass. Every byte of the log is
+// loaded once for the window values anyway, so the header walk of LogReader::read_physical_record
+// (src/db/log.rs:204-279) runs on the region data already in registers instead of as a chain of dependent memory
+// round trips (k_wal_parse: ~20 us alone, ~50 us beside another scan's window pass). A wave takes a whole 32 KiB log
+// block at a time -- its two 16 KiB regions one after the other, so the chain carries from the first into the
+// second -- and walks, per region, the headers that lie in it: a header byte at a (wave-uniform) offset sits in a
+// known lane and register of the pre-transpose LX half-tiles, read by M0-relative register indexing and v_readlane
+// (a few scalar instructions per byte, no memory access). Three half-tile buffers rotate so that both halves of the
+// region are resident when the walk starts while the next half-tile's loads stay in flight (the walk of the
+// second-to-last loaded half refills one buffer, the last one the other). Outputs exactly k_wal_parse's per-block
+// record slots, counts and stop reasons; k_wal_part then forms k_wal_emit's per-part offsets.
+// ---------------------------------------------------------------------------------------------------
+struct WalWalk {
+  uint32_t consumed, nrec, nsingle, stop, saved;
+  bool done;
+};
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+// byte o (wave-uniform) of a region held in two pre-transpose LX half-tiles (A: bytes [0, 128) of every 256 B
+// window, B: [128, 256)): lane k + 8 c2 + 16 c0 + 32 c1, register 4 j + dword, j = pi(window >> 3)
+__device__ __forceinline__ uint32_t lx_byte(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t o) {
+  const uint32_t w = o >> 8, x = o & 255u, c = (x >> 4) & 7u;
+  const uint32_t lane = (w & 7u) | (((c >> 2) & 1u) << 3) | ((c & 1u) << 4) | (((c >> 1) & 1u) << 5);
+  const uint32_t J = w >> 3;
+  const uint32_t j = ((J & 1u) << 2) | (J & 2u) | ((J >> 2) & 1u);
+  const uint32_t R = 4u * j + ((x >> 2) & 3u);
+  // each half-tile as one 32-register vector read at the uniform index R (s_set_gpr_idx_on + v_mov: M0-relative);
+  // indexing the arrays through a pointer instead left them in scratch memory
+  typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+  u32x32 fa, fb;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) fa[k] = A[k >> 2][k & 3];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) fb[k] = B[k >> 2][k & 3];
+  const uint32_t va = fa[R], vb = fb[R];
+  const uint32_t v = (x & 128u) ? vb : va;
+  return ((uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane) >> (8u * (x & 3u))) & 0xFFu;
+}
+
+// region h (0: block bytes [0, 16 KiB), 1: [16 KiB, 32 KiB)) of log block b's header walk, exactly as k_wal_parse
+// (log.rs:229-258): the headers whose 7 bytes lie below this region's end (region 1 reads a header straddling the
+// two from the last dword of region 0, kept in W.saved). cap: the block's bytes.
+__device__ __forceinline__ void wal_walk_region(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t h, uint64_t b,
+                                                uint32_t cap, WalWalk& W, uint2* __restrict__ slots, uint32_t lane) {
+  const uint32_t lo = 16384u * h;
+  const uint32_t hi = (h == 0 && cap > 16384u) ? 16384u : cap;
+  while (!W.done && W.consumed + 7 <= hi) {  // (implies cap - consumed >= 7)
+    const uint32_t p = W.consumed;
+    uint32_t hb[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t q = p + 4 + k;
+      hb[k] = q < lo ? (W.saved >> (8u * (q - (lo - 4u)))) & 0xFFu : lx_byte(A, B, q - lo);
+    }
+    const uint32_t length = hb[0] | (hb[1] << 8), type = hb[2];
+    if (7 + length > cap - p) {
+      W.stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
+      W.done = true;
+      break;
+    }
+    if (type == 0 && length == 0) {
+      W.stop = LCRC_WAL_STOP_ZERO_DEV;
+      W.done = true;
+      break;
+    }
+    const uint32_t one = wal_single(b, p, length);
+    if (W.nrec < WAL_SLOTS && lane == 0) slots[b * WAL_SLOTS + W.nrec] = make_uint2(p | (length << 16), type | (one << 8));
+    ++W.nrec;
+    W.nsingle += one;
+    W.consumed = p + 7 + length;
+  }
+  if (h == 0 && cap > 16384u) {  // block bytes 16380..16383 for a header straddling the two regions
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v |= lx_byte(A, B, 16380u + k) << (8 * k);
+    W.saved = v;
+  }
+}
+
+struct WalSched {  // a wave's position: block cur (region h of it), the next block (ticket taken at h == 0)
+  uint64_t cur, next;
+  uint32_t h;
+};
+
+// One region of the fused pass. A, B: both half-tiles of region r_i = 2 cur + h (resident); C: half 0 of r_{i+1}
+// (in flight). Walks the headers, then the two halves; A is refilled with half 1 of r_{i+1}, B with half 0 of
+// r_{i+2}, so the next region's call takes (C, A, B). Returns true when the wave has no block left.
+__device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], const uint8_t* __restrict__ file, uint64_t file_len,
+                                          uint64_t nblocks, uint64_t nreg, const void* L, const Rot& R, WalSched& S,
+                                          WalWalk& W, uint32_t* wg_ticket, uint32_t* __restrict__ win,
+                                          uint32_t* __restrict__ counts, uint2* __restrict__ slots,
+                                          uint8_t* __restrict__ stops, uint64_t* __restrict__ packed, uint32_t lane,
+                                          uint32_t voff_a, uint32_t voff_b) {
+  // the schedule is wave-uniform; say so (left to itself the compiler kept it in VGPRs and wrapped every load of
+  // the pass in a waterfall loop over its buffer descriptor)
+  S.cur = uniform64(S.cur);
+  S.next = uniform64(S.next);
+  S.h = __builtin_amdgcn_readfirstlane(S.h);
+  if (S.cur == NO_REGION) return true;
+  if (S.h == 0) {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(wg_ticket, 1u);
+    v = __builtin_amdgcn_readfirstlane(v);
+    const uint64_t nb = blockIdx.x + (uint64_t)v * gridDim.x;
+    S.next = nb < nblocks ? nb : NO_REGION;
+    W.consumed = W.nrec = W.nsingle = W.saved = 0;
+    W.stop = LCRC_WAL_STOP_TRAILER_DEV;
+    W.done = false;
+  }
+  const uint64_t t = 2 * S.cur + S.h;
+  const uint64_t rem = file_len - S.cur * 32768ull;
+  const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
+  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, slots, lane);
+  // r_{i+1} = (cur, 1) or (next, 0); r_{i+2} = (next, h)
+  const uint64_t b1 = S.h == 0 ? S.cur : S.next;
+  const uint64_t t1 = b1 == NO_REGION ? nreg : 2 * b1 + (S.h ^ 1u);
+  const uint64_t t2 = S.next == NO_REGION ? nreg : 2 * S.next + S.h;
+  const __amdgpu_buffer_rsrc_t rs1 = region_rsrc(file, file_len, t1, nreg);
+  const __amdgpu_buffer_rsrc_t rs2 = region_rsrc(file, file_len, t2, nreg);
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t x = walk_half<true, KW_LAY, false>(L, R, A, 0u, rs1, voff_b);
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t p = walk_half<true, KW_LAY>(L, R, B, x, rs2, voff_a);
+  if (t < nreg) win[t * 64 + window_of_lane<KW_LAY>(lane)] = p;
+  if (S.h == 1) {
+    if (lane == 0) {
+      counts[S.cur] = W.nrec;
+      stops[S.cur] = (uint8_t)W.stop;
+      packed[S.cur] = (uint64_t)W.nrec | ((uint64_t)W.nsingle << 32);
+    }
+    S.cur = S.next;
+    S.h = 0;
+  } else {
+    S.h = 1;
+  }
+  return false;
+}
+
+__global__ void __launch_bounds__(A_THREADS) k_wal_windows(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                          uint64_t nblocks, const uint32_t* __restrict__ gtab,
+                                                          uint32_t* __restrict__ win, uint32_t* __restrict__ counts,
+                                                          uint2* __restrict__ slots, uint8_t* __restrict__ stops,
+                                                          uint64_t* __restrict__ packed) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[A_ZT / 4];  // the slice sets only (no block tree)
+  __shared__ uint32_t wg_ticket;
+  const uint32_t lane = __lane_id();
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t nreg = (file_len + REGION - 1) / REGION;
+  const uint32_t voff_a = lane_voff<KW_LAY>(lane, 0), voff_b = lane_voff<KW_LAY>(lane, 1);
+  // log blocks dealt round-robin over the workgroups; a wave's first one static, then tickets
+  WalSched S;
+  {
+    const uint64_t b0 = blockIdx.x + (uint64_t)wv * gridDim.x;
+    S.cur = b0 < nblocks ? b0 : NO_REGION;
+    S.next = NO_REGION;
+    S.h = 0;
+  }
+  u32x4 X[8], Y[8], Z[8];
+  {
+    const uint64_t t0 = S.cur == NO_REGION ? nreg : 2 * S.cur;
+    const __amdgpu_buffer_rsrc_t r0 = region_rsrc(file, file_len, t0, nreg);
+    const __amdgpu_buffer_rsrc_t r1 = region_rsrc(file, file_len, t0 + 1 < nreg ? t0 + 1 : nreg, nreg);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half<KW_LAY>(X, r0, voff_a);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half<KW_LAY>(Y, r0, voff_b);
+    __builtin_amdgcn_sched_barrier(0);
+    load_half<KW_LAY>(Z, r1, voff_a);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  build_tables<false>(L, gtab, wv, lane);
+  if (tid == 0) wg_ticket = A_THREADS / 64;  // tickets 0 .. waves-1 were the static first blocks
+  lds_barrier();
+  const Rot R = make_rot(lane);
+  WalWalk W{};
+  for (;;) {
+    if (wal_phase(X, Y, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed, lane,
+                  voff_a, voff_b))
+      break;
+    if (wal_phase(Z, X, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed, lane,
+                  voff_a, voff_b))
+      break;
+    if (wal_phase(Y, Z, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed, lane,
+                  voff_a, voff_b))
+      break;
+  }
+}
+
+// k_wal_windows' per-block packed counts (records | one-window records << 32) -> k_wal_emit's inputs, as k_wal_parse
+// leaves them: the exclusive offsets inside each part of WAL_PARTB blocks (in place) and the part totals
+__global__ void __launch_bounds__(64) k_wal_part(uint64_t nblocks, uint64_t* __restrict__ local,
+                                                 uint64_t* __restrict__ part) {
+  static_assert(WAL_PARTB == 64, "one wave per part");
+  const uint64_t b = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint64_t mine = b < nblocks ? local[b] : 0;
+  uint64_t inc = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t v = __shfl_up(inc, d, 64);
+    if (threadIdx.x >= (uint32_t)d) inc += v;
+  }
+  if (b < nblocks) local[b] = inc - mine;
+  if (threadIdx.x == 63) part[blockIdx.x] = inc;
+}
+
 
 // ---------------------------------------------------------------------------------------------------
 // Snappy framing (the `snap` crate's FrameEncoder / FrameDecoder used for compressed SSTable blocks,
@@ -3088,6 +3298,32 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
   const uint64_t g = (nt + 255) / 256;
   LCRC_LAUNCH(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
                      stops, local, part, recs, descs, max_recs, n_total, n_out);
+  return hipGetLastError();
+}
+
+// the fused WAL window pass + header walk (k_wal_windows), then the per-part offsets (k_wal_part); `grid` = CUs.
+// local: k_wal_emit's per-block offsets (nblocks words), part: its per-64-block totals
+hipError_t lcrc_launch_wal_windows(int grid, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
+                                   const uint32_t* gtab, uint32_t* win, uint32_t* counts, uint2* slots, uint8_t* stops,
+                                   uint64_t* local, uint64_t* part, hipStream_t st) {
+  if (nblocks == 0) return hipSuccess;
+  const uint64_t need = (nblocks + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
+  const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
+  LCRC_LAUNCH(lcrc_dev::k_wal_windows, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, file, file_len, nblocks, gtab, win,
+              counts, slots, stops, local);
+  const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
+  LCRC_LAUNCH(lcrc_dev::k_wal_part, dim3((unsigned)nparts), dim3(64), 0, st, nblocks, local, part);
+  return hipGetLastError();
+}
+
+// the record emit alone (after lcrc_launch_wal_windows)
+hipError_t lcrc_launch_wal_emit(const uint8_t* file, uint64_t nblocks, uint32_t* counts, uint2* slots, uint8_t* stops,
+                                uint64_t* local, uint64_t* part, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
+                                uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, hipStream_t st) {
+  const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
+  const uint64_t g = (nt + 255) / 256;
+  LCRC_LAUNCH(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots, stops,
+              local, part, recs, descs, max_recs, n_total, n_out);
   return hipGetLastError();
 }
 
