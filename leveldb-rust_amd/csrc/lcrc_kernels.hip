@@ -1823,49 +1823,56 @@ __global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
 struct WalWalk {
   uint32_t consumed, nrec, nsingle, stop, saved;
   bool done;
+  uint32_t sx, sy;  // the block's first WAL_SLOTS record slots, slot i in lane i (stored once, at the block's end)
 };
 
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
-// byte o (wave-uniform) of a region held in two pre-transpose LX half-tiles (A: bytes [0, 128) of every 256 B
-// window, B: [128, 256)): lane k + 8 c2 + 16 c0 + 32 c1, register 4 j + dword, j = pi(window >> 3)
-__device__ __forceinline__ uint32_t lx_byte(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t o) {
+// The aligned dword at region offset o (wave-uniform, o % 4 == 0) of a region held in two pre-transpose LX
+// half-tiles (A: bytes [0, 128) of every 256 B window, B: [128, 256)): lane k + 8 c2 + 16 c0 + 32 c1, register
+// 4 j + dword, j = pi(window >> 3). The register is picked by a scalar branch tree over the 64 (half, register)
+// cases, each a v_readlane of a FIXED register, so the compiler waits (vmcnt) only for that register's load --
+// M0-relative indexing made it drain every load in flight, including the next half-tile's.
+#define LCRC_LX4(H, V, J)                                               \
+  case 32 * H + 4 * J + 0: d = __builtin_amdgcn_readlane(V[J].x, lane); break; \
+  case 32 * H + 4 * J + 1: d = __builtin_amdgcn_readlane(V[J].y, lane); break; \
+  case 32 * H + 4 * J + 2: d = __builtin_amdgcn_readlane(V[J].z, lane); break; \
+  case 32 * H + 4 * J + 3: d = __builtin_amdgcn_readlane(V[J].w, lane); break;
+__device__ __forceinline__ uint32_t lx_dword(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t o) {
   const uint32_t w = o >> 8, x = o & 255u, c = (x >> 4) & 7u;
   const uint32_t lane = (w & 7u) | (((c >> 2) & 1u) << 3) | ((c & 1u) << 4) | (((c >> 1) & 1u) << 5);
   const uint32_t J = w >> 3;
   const uint32_t j = ((J & 1u) << 2) | (J & 2u) | ((J >> 2) & 1u);
-  const uint32_t R = 4u * j + ((x >> 2) & 3u);
-  // each half-tile as one 32-register vector read at the uniform index R (s_set_gpr_idx_on + v_mov: M0-relative);
-  // indexing the arrays through a pointer instead left them in scratch memory
-  typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
-  u32x32 fa, fb;
-#pragma unroll
-  for (int k = 0; k < 32; ++k) fa[k] = A[k >> 2][k & 3];
-#pragma unroll
-  for (int k = 0; k < 32; ++k) fb[k] = B[k >> 2][k & 3];
-  const uint32_t va = fa[R], vb = fb[R];
-  const uint32_t v = (x & 128u) ? vb : va;
-  return ((uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane) >> (8u * (x & 3u))) & 0xFFu;
+  const uint32_t sel = ((x >> 7) << 5) | (4u * j + ((x >> 2) & 3u));
+  uint32_t d = 0;
+  switch (sel) {
+    LCRC_LX4(0, A, 0) LCRC_LX4(0, A, 1) LCRC_LX4(0, A, 2) LCRC_LX4(0, A, 3)
+    LCRC_LX4(0, A, 4) LCRC_LX4(0, A, 5) LCRC_LX4(0, A, 6) LCRC_LX4(0, A, 7)
+    LCRC_LX4(1, B, 0) LCRC_LX4(1, B, 1) LCRC_LX4(1, B, 2) LCRC_LX4(1, B, 3)
+    LCRC_LX4(1, B, 4) LCRC_LX4(1, B, 5) LCRC_LX4(1, B, 6) LCRC_LX4(1, B, 7)
+    default: break;
+  }
+  return d;
 }
+#undef LCRC_LX4
 
 // region h (0: block bytes [0, 16 KiB), 1: [16 KiB, 32 KiB)) of log block b's header walk, exactly as k_wal_parse
 // (log.rs:229-258): the headers whose 7 bytes lie below this region's end (region 1 reads a header straddling the
 // two from the last dword of region 0, kept in W.saved). cap: the block's bytes.
 __device__ __forceinline__ void wal_walk_region(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t h, uint64_t b,
-                                                uint32_t cap, WalWalk& W, uint2* __restrict__ slots, uint32_t lane) {
+                                                uint32_t cap, WalWalk& W, uint32_t lane) {
   const uint32_t lo = 16384u * h;
   const uint32_t hi = (h == 0 && cap > 16384u) ? 16384u : cap;
   while (!W.done && W.consumed + 7 <= hi) {  // (implies cap - consumed >= 7)
     const uint32_t p = W.consumed;
-    uint32_t hb[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const uint32_t q = p + 4 + k;
-      hb[k] = q < lo ? (W.saved >> (8u * (q - (lo - 4u)))) & 0xFFu : lx_byte(A, B, q - lo);
-    }
-    const uint32_t length = hb[0] | (hb[1] << 8), type = hb[2];
+    // header bytes 4..6 from the dwords at q0 and q0 + 4 (block offsets; below lo: the saved dword of region 0)
+    const uint32_t q0 = (p + 4) & ~3u, sh = (p + 4) & 3u;
+    const uint32_t d0 = q0 < lo ? W.saved : lx_dword(A, B, q0 - lo);
+    const uint32_t d1 = sh <= 1 ? 0u : lx_dword(A, B, q0 + 4 - lo);  // (q0 + 4 >= lo: q0 >= lo - 4)
+    const uint64_t hb = (((uint64_t)d1 << 32) | d0) >> (8 * sh);
+    const uint32_t length = (uint32_t)hb & 0xFFFFu, type = (uint32_t)(hb >> 16) & 0xFFu;
     if (7 + length > cap - p) {
       W.stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
       W.done = true;
@@ -1877,17 +1884,16 @@ __device__ __forceinline__ void wal_walk_region(const u32x4 (&A)[8], const u32x4
       break;
     }
     const uint32_t one = wal_single(b, p, length);
-    if (W.nrec < WAL_SLOTS && lane == 0) slots[b * WAL_SLOTS + W.nrec] = make_uint2(p | (length << 16), type | (one << 8));
+    // slot nrec kept in lane nrec (a select): no memory store inside the walk -- a store there made the compiler
+    // drain every load in flight before the loop
+    const bool mine = lane == W.nrec;
+    W.sx = mine ? (p | (length << 16)) : W.sx;
+    W.sy = mine ? (type | (one << 8)) : W.sy;
     ++W.nrec;
     W.nsingle += one;
     W.consumed = p + 7 + length;
   }
-  if (h == 0 && cap > 16384u) {  // block bytes 16380..16383 for a header straddling the two regions
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v |= lx_byte(A, B, 16380u + k) << (8 * k);
-    W.saved = v;
-  }
+  if (h == 0 && cap > 16384u) W.saved = lx_dword(A, B, 16380u);  // for a header straddling the two regions
 }
 
 struct WalSched {  // a wave's position: block cur (region h of it), the next block (ticket taken at h == 0)
@@ -1895,15 +1901,16 @@ struct WalSched {  // a wave's position: block cur (region h of it), the next bl
   uint32_t h;
 };
 
-// One region of the fused pass. A, B: both half-tiles of region r_i = 2 cur + h (resident); C: half 0 of r_{i+1}
-// (in flight). Walks the headers, then the two halves; A is refilled with half 1 of r_{i+1}, B with half 0 of
-// r_{i+2}, so the next region's call takes (C, A, B). Returns true when the wave has no block left.
-__device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], const uint8_t* __restrict__ file, uint64_t file_len,
-                                          uint64_t nblocks, uint64_t nreg, const void* L, const Rot& R, WalSched& S,
-                                          WalWalk& W, uint32_t* wg_ticket, uint32_t* __restrict__ win,
-                                          uint32_t* __restrict__ counts, uint2* __restrict__ slots,
-                                          uint8_t* __restrict__ stops, uint64_t* __restrict__ packed, uint32_t lane,
-                                          uint32_t voff_a, uint32_t voff_b) {
+// One region of the fused pass. A, B: both half-tiles of region r_i = 2 cur + h (loaded one region earlier); C, D:
+// free. The next region's two half-tiles are issued into C, D first (they have this whole region's walk to arrive),
+// then the headers are walked on A, B, then A and B are walked (no refills). The next region's call takes
+// (C, D, A, B). Returns true when the wave has no block left.
+__device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], u32x4 (&C)[8], u32x4 (&D)[8],
+                                          const uint8_t* __restrict__ file, uint64_t file_len, uint64_t nblocks,
+                                          uint64_t nreg, const void* L, const Rot& R, WalSched& S, WalWalk& W,
+                                          uint32_t* wg_ticket, uint32_t* __restrict__ win, uint32_t* __restrict__ counts,
+                                          uint2* __restrict__ slots, uint8_t* __restrict__ stops,
+                                          uint64_t* __restrict__ packed, uint32_t lane, uint32_t voff_a, uint32_t voff_b) {
   // the schedule is wave-uniform; say so (left to itself the compiler kept it in VGPRs and wrapped every load of
   // the pass in a waterfall loop over its buffer descriptor)
   S.cur = uniform64(S.cur);
@@ -1921,21 +1928,25 @@ __device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], const ui
     W.done = false;
   }
   const uint64_t t = 2 * S.cur + S.h;
-  const uint64_t rem = file_len - S.cur * 32768ull;
-  const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
-  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, slots, lane);
-  // r_{i+1} = (cur, 1) or (next, 0); r_{i+2} = (next, h)
+  // r_{i+1} = (cur, 1) or (next, 0)
   const uint64_t b1 = S.h == 0 ? S.cur : S.next;
   const uint64_t t1 = b1 == NO_REGION ? nreg : 2 * b1 + (S.h ^ 1u);
-  const uint64_t t2 = S.next == NO_REGION ? nreg : 2 * S.next + S.h;
   const __amdgpu_buffer_rsrc_t rs1 = region_rsrc(file, file_len, t1, nreg);
-  const __amdgpu_buffer_rsrc_t rs2 = region_rsrc(file, file_len, t2, nreg);
   __builtin_amdgcn_sched_barrier(0);
-  const uint32_t x = walk_half<true, KW_LAY, false>(L, R, A, 0u, rs1, voff_b);
+  load_half<KW_LAY>(C, rs1, voff_a);
   __builtin_amdgcn_sched_barrier(0);
-  const uint32_t p = walk_half<true, KW_LAY>(L, R, B, x, rs2, voff_a);
+  load_half<KW_LAY>(D, rs1, voff_b);
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t rem = file_len - S.cur * 32768ull;
+  const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
+  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t x = walk_half<false, KW_LAY, false>(L, R, A, 0u, rs1, voff_a);
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t p = walk_half<false, KW_LAY>(L, R, B, x, rs1, voff_b);
   if (t < nreg) win[t * 64 + window_of_lane<KW_LAY>(lane)] = p;
   if (S.h == 1) {
+    if (lane < W.nrec && lane < WAL_SLOTS) slots[S.cur * WAL_SLOTS + lane] = make_uint2(W.sx, W.sy);
     if (lane == 0) {
       counts[S.cur] = W.nrec;
       stops[S.cur] = (uint8_t)W.stop;
@@ -1969,17 +1980,13 @@ __global__ void __launch_bounds__(A_THREADS) k_wal_windows(const uint8_t* __rest
     S.next = NO_REGION;
     S.h = 0;
   }
-  u32x4 X[8], Y[8], Z[8];
+  u32x4 X[8], Y[8], Z[8], Q[8];
   {
-    const uint64_t t0 = S.cur == NO_REGION ? nreg : 2 * S.cur;
-    const __amdgpu_buffer_rsrc_t r0 = region_rsrc(file, file_len, t0, nreg);
-    const __amdgpu_buffer_rsrc_t r1 = region_rsrc(file, file_len, t0 + 1 < nreg ? t0 + 1 : nreg, nreg);
+    const __amdgpu_buffer_rsrc_t r0 = region_rsrc(file, file_len, S.cur == NO_REGION ? nreg : 2 * S.cur, nreg);
     __builtin_amdgcn_sched_barrier(0);
     load_half<KW_LAY>(X, r0, voff_a);
     __builtin_amdgcn_sched_barrier(0);
     load_half<KW_LAY>(Y, r0, voff_b);
-    __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_LAY>(Z, r1, voff_a);
     __builtin_amdgcn_sched_barrier(0);
   }
   build_tables<false>(L, gtab, wv, lane);
@@ -1988,14 +1995,11 @@ __global__ void __launch_bounds__(A_THREADS) k_wal_windows(const uint8_t* __rest
   const Rot R = make_rot(lane);
   WalWalk W{};
   for (;;) {
-    if (wal_phase(X, Y, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed, lane,
-                  voff_a, voff_b))
+    if (wal_phase(X, Y, Z, Q, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed,
+                  lane, voff_a, voff_b))
       break;
-    if (wal_phase(Z, X, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed, lane,
-                  voff_a, voff_b))
-      break;
-    if (wal_phase(Y, Z, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed, lane,
-                  voff_a, voff_b))
+    if (wal_phase(Z, Q, X, Y, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed,
+                  lane, voff_a, voff_b))
       break;
   }
 }
