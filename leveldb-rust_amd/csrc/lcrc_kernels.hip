@@ -1832,31 +1832,25 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 
 // The aligned dword at region offset o (wave-uniform, o % 4 == 0) of a region held in two pre-transpose LX
 // half-tiles (A: bytes [0, 128) of every 256 B window, B: [128, 256)): lane k + 8 c2 + 16 c0 + 32 c1, register
-// 4 j + dword, j = pi(window >> 3). The register is picked by a scalar branch tree over the 64 (half, register)
-// cases, each a v_readlane of a FIXED register, so the compiler waits (vmcnt) only for that register's load --
-// M0-relative indexing made it drain every load in flight, including the next half-tile's.
-#define LCRC_LX4(H, V, J)                                               \
-  case 32 * H + 4 * J + 0: d = __builtin_amdgcn_readlane(V[J].x, lane); break; \
-  case 32 * H + 4 * J + 1: d = __builtin_amdgcn_readlane(V[J].y, lane); break; \
-  case 32 * H + 4 * J + 2: d = __builtin_amdgcn_readlane(V[J].z, lane); break; \
-  case 32 * H + 4 * J + 3: d = __builtin_amdgcn_readlane(V[J].w, lane); break;
+// 4 j + dword, j = pi(window >> 3). Each half-tile is read as one 32-register vector at the uniform index (M0-relative:
+// s_set_gpr_idx_on + v_mov), then v_readlane. (The compiler cannot tell which register such a read touches and waits
+// for every load in flight before it: the walk therefore runs before the next region's loads are issued.)
 __device__ __forceinline__ uint32_t lx_dword(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t o) {
   const uint32_t w = o >> 8, x = o & 255u, c = (x >> 4) & 7u;
   const uint32_t lane = (w & 7u) | (((c >> 2) & 1u) << 3) | ((c & 1u) << 4) | (((c >> 1) & 1u) << 5);
   const uint32_t J = w >> 3;
   const uint32_t j = ((J & 1u) << 2) | (J & 2u) | ((J >> 2) & 1u);
-  const uint32_t sel = ((x >> 7) << 5) | (4u * j + ((x >> 2) & 3u));
-  uint32_t d = 0;
-  switch (sel) {
-    LCRC_LX4(0, A, 0) LCRC_LX4(0, A, 1) LCRC_LX4(0, A, 2) LCRC_LX4(0, A, 3)
-    LCRC_LX4(0, A, 4) LCRC_LX4(0, A, 5) LCRC_LX4(0, A, 6) LCRC_LX4(0, A, 7)
-    LCRC_LX4(1, B, 0) LCRC_LX4(1, B, 1) LCRC_LX4(1, B, 2) LCRC_LX4(1, B, 3)
-    LCRC_LX4(1, B, 4) LCRC_LX4(1, B, 5) LCRC_LX4(1, B, 6) LCRC_LX4(1, B, 7)
-    default: break;
-  }
-  return d;
+  const uint32_t R = 4u * j + ((x >> 2) & 3u);
+  typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+  u32x32 fa, fb;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) fa[k] = A[k >> 2][k & 3];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) fb[k] = B[k >> 2][k & 3];
+  const uint32_t va = fa[R], vb = fb[R];
+  const uint32_t v = (x & 128u) ? vb : va;
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
-#undef LCRC_LX4
 
 // region h (0: block bytes [0, 16 KiB), 1: [16 KiB, 32 KiB)) of log block b's header walk, exactly as k_wal_parse
 // (log.rs:229-258): the headers whose 7 bytes lie below this region's end (region 1 reads a header straddling the
@@ -1902,9 +1896,10 @@ struct WalSched {  // a wave's position: block cur (region h of it), the next bl
 };
 
 // One region of the fused pass. A, B: both half-tiles of region r_i = 2 cur + h (loaded one region earlier); C, D:
-// free. The next region's two half-tiles are issued into C, D first (they have this whole region's walk to arrive),
-// then the headers are walked on A, B, then A and B are walked (no refills). The next region's call takes
-// (C, D, A, B). Returns true when the wave has no block left.
+// free. The headers are walked on A, B (nothing else in flight: the compiler's conservative wait before the
+// M0-relative reads is the exact one), then the next region's two half-tiles are issued into C, D (they have this
+// region's walk to arrive), then A and B are walked (no refills). The next region's call takes (C, D, A, B). Returns
+// true when the wave has no block left.
 __device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], u32x4 (&C)[8], u32x4 (&D)[8],
                                           const uint8_t* __restrict__ file, uint64_t file_len, uint64_t nblocks,
                                           uint64_t nreg, const void* L, const Rot& R, WalSched& S, WalWalk& W,
@@ -1932,14 +1927,13 @@ __device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], u32x4 (&
   const uint64_t b1 = S.h == 0 ? S.cur : S.next;
   const uint64_t t1 = b1 == NO_REGION ? nreg : 2 * b1 + (S.h ^ 1u);
   const __amdgpu_buffer_rsrc_t rs1 = region_rsrc(file, file_len, t1, nreg);
+  const uint64_t rem = file_len - S.cur * 32768ull;
+  const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
+  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, lane);
   __builtin_amdgcn_sched_barrier(0);
   load_half<KW_LAY>(C, rs1, voff_a);
   __builtin_amdgcn_sched_barrier(0);
   load_half<KW_LAY>(D, rs1, voff_b);
-  __builtin_amdgcn_sched_barrier(0);
-  const uint64_t rem = file_len - S.cur * 32768ull;
-  const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
-  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, lane);
   __builtin_amdgcn_sched_barrier(0);
   const uint32_t x = walk_half<false, KW_LAY, false>(L, R, A, 0u, rs1, voff_a);
   __builtin_amdgcn_sched_barrier(0);
