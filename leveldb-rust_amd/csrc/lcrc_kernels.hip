@@ -1833,8 +1833,8 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 // The aligned dword at region offset o (wave-uniform, o % 4 == 0) of a region held in two pre-transpose LX
 // half-tiles (A: bytes [0, 128) of every 256 B window, B: [128, 256)): lane k + 8 c2 + 16 c0 + 32 c1, register
 // 4 j + dword, j = pi(window >> 3). Each half-tile is read as one 32-register vector at the uniform index (M0-relative:
-// s_set_gpr_idx_on + v_mov), then v_readlane. (The compiler cannot tell which register such a read touches and waits
-// for every load in flight before it: the walk therefore runs before the next region's loads are issued.)
+// s_set_gpr_idx_on + v_mov), then v_readlane. (The compiler cannot tell which register such a read touches: its
+// caller waits for A and B explicitly before it, see wal_phase.)
 __device__ __forceinline__ uint32_t lx_dword(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t o) {
   const uint32_t w = o >> 8, x = o & 255u, c = (x >> 4) & 7u;
   const uint32_t lane = (w & 7u) | (((c >> 2) & 1u) << 3) | ((c & 1u) << 4) | (((c >> 1) & 1u) << 5);
@@ -1896,10 +1896,9 @@ struct WalSched {  // a wave's position: block cur (region h of it), the next bl
 };
 
 // One region of the fused pass. A, B: both half-tiles of region r_i = 2 cur + h (loaded one region earlier); C, D:
-// free. The headers are walked on A, B (nothing else in flight: the compiler's conservative wait before the
-// M0-relative reads is the exact one), then the next region's two half-tiles are issued into C, D (they have this
-// region's walk to arrive), then A and B are walked (no refills). The next region's call takes (C, D, A, B). Returns
-// true when the wave has no block left.
+// free. Once A and B are in, the next region's two half-tiles are issued into C, D (they have this region's header
+// walk and walk to arrive), the headers are walked on A, B, then A and B are walked (no refills). The next region's
+// call takes (C, D, A, B). Returns true when the wave has no block left.
 __device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], u32x4 (&C)[8], u32x4 (&D)[8],
                                           const uint8_t* __restrict__ file, uint64_t file_len, uint64_t nblocks,
                                           uint64_t nreg, const void* L, const Rot& R, WalSched& S, WalWalk& W,
@@ -1929,11 +1928,17 @@ __device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], u32x4 (&
   const __amdgpu_buffer_rsrc_t rs1 = region_rsrc(file, file_len, t1, nreg);
   const uint64_t rem = file_len - S.cur * 32768ull;
   const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
-  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, lane);
+  // A and B are all this wave has in flight: wait for them HERE, explicitly -- the compiler then knows they are in
+  // registers and inserts no wait of its own before the header walk's M0-relative reads (it cannot tell which
+  // register those touch, and would otherwise drain the next region's loads too) -- then issue the next region,
+  // which stays in flight during the header walk and the two half walks
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __builtin_amdgcn_sched_barrier(0);
   load_half<KW_LAY>(C, rs1, voff_a);
   __builtin_amdgcn_sched_barrier(0);
   load_half<KW_LAY>(D, rs1, voff_b);
+  __builtin_amdgcn_sched_barrier(0);
+  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, lane);
   __builtin_amdgcn_sched_barrier(0);
   const uint32_t x = walk_half<false, KW_LAY, false>(L, R, A, 0u, rs1, voff_a);
   __builtin_amdgcn_sched_barrier(0);
