@@ -207,7 +207,7 @@ struct lcrc_ctx {
   void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
   uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
   int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan (LCRC_TS_BLOCKS_DIV, measurement)
-  bool wal_fused = true;  // WAL scan: header walk inside the window pass (LCRC_WAL_FUSED=0: the separate k_wal_parse)
+  bool wal_fused = false;  // WAL scan: header walk inside the window pass (LCRC_WAL_FUSED=1; measured slower, DESIGN)
 };
 
 namespace {
@@ -365,7 +365,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   ctx->x4096 = lcrc::x8n(4096, poly);
   if (const char* g = getenv("LCRC_GENERAL")) ctx->general = !strcmp(g, "ranges") ? 1 : !strcmp(g, "blocks") ? 2 : 0;
   if (const char* g = getenv("LCRC_TS_BLOCKS_DIV")) ctx->ts_blocks_div = std::max(1, atoi(g));
-  if (const char* g = getenv("LCRC_WAL_FUSED")) ctx->wal_fused = strcmp(g, "0") != 0;
+  if (const char* g = getenv("LCRC_WAL_FUSED")) ctx->wal_fused = strcmp(g, "1") == 0;
   *out = ctx;
   return LCRC_OK;
 }
@@ -921,12 +921,12 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   uint64_t* n_total = ctx->wal_offsets.p;
   uint64_t* local = ctx->wal_offsets.p + 1;
   uint64_t* part = ctx->wal_offsets.p + 1 + nblocks;
-  // The default (window/range path): ONE streaming pass computes every 256 B window value AND walks the record
-  // headers on the data it holds (k_wal_windows + k_wal_part), then the records at their file-order positions
-  // (k_wal_emit), then one k_blocks over all records (the log format stores the raw crc: no mask) that also
-  // stores each record's crc and verdict. (The header walk as its own kernel -- k_wal_parse, a dependent chain of
-  // memory round trips per 32 KiB block -- took ~20 us alone and ~50 us beside another scan's window pass.)
-  // LCRC_WAL_FUSED=0 (measurement), the one-pass range kernel or max_recs 0: the separate header walk first.
+  // LCRC_WAL_FUSED=1: ONE streaming pass computes every 256 B window value AND walks the record headers on the data
+  // it holds (k_wal_windows + k_wal_part), then the records at their file-order positions (k_wal_emit), then one
+  // k_blocks over all records that also stores each record's crc and verdict. Measured slower than the default
+  // below (k_wal_windows 57-59 us alone vs 45 for the plain window pass: the scalar header walk lengthens every
+  // wave; and on two streams the separate header walk already hides behind the other scan's window pass), so it
+  // is opt-in; both forms pass the same parity tests.
   if (max_recs && ctx->general != 1 && ctx->wal_fused) {
     HIPCHK(lcrc_launch_wal_windows(ctx->grid_a, file, file_len, nblocks, ctx->d_tab, ctx->win.p, ctx->wal_counts.p,
                                    ctx->wal_slots.p, ctx->wal_stops.p, local, part, st));
@@ -937,6 +937,9 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
                               n_total, (lcrc_wal_rec_dev*)recs, st));
     return LCRC_OK;
   }
+  // The default: one stream, the header walk (k_wal_parse, one lane per 32 KiB block following the 7-byte headers,
+  // then k_wal_emit), the window pass over the whole file, then one k_blocks over all records (the log format stores
+  // the raw crc: no mask) that also stores each record's crc and verdict.
   HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local,
                                part, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, n_total, n_recs, st));
   if (max_recs && ctx->general == 1) {

@@ -927,3 +927,54 @@ def test_first_queued_call_inside_a_graph_capture(lcrc, orc):
     finally:
         eng.graph_destroy(g)
         eng.close()
+
+
+@pytest.mark.parametrize("blocks", [8195, 4161])
+def test_wal_fused_window_pass(lcrc, orc, synth, blocks, monkeypatch):
+    """LCRC_WAL_FUSED=1: the record headers walked inside the window pass (k_wal_windows, the region data read from
+    the wave's registers) instead of by k_wal_parse -- every record, crc and verdict the same as the oracle's walk,
+    on the full-size configs[3] log and on the corrupted 4,161-block log (a header straddling the two 16 KiB regions
+    of a block is read from the saved last dword of the first)."""
+    monkeypatch.setenv("LCRC_WAL_FUSED", "1")
+    engs = {m: lcrc.Engine(0, m) for m in MODES}
+    try:
+        if blocks == 8195:
+            data = _wal_file(lcrc, synth, 256 << 20, synth.SEED_WAL)
+        else:
+            data = _wal_file(lcrc, synth, 4161 * 32768, 0x5EED0013)[:4160 * 32768 + 1000]
+            rng = np.random.default_rng(0x65)
+            want = _wal_expect(orc, data)
+            for k in rng.choice(len(want), 40, replace=False):
+                h, n, _ = want[int(k)]
+                data[h + 6 + int(rng.integers(0, n + 1))] ^= 1 << int(rng.integers(0, 8))
+            h, n, _ = want[len(want) // 3]
+            data[h + 5] ^= 0x80
+        for mode in MODES:
+            _wal_check_scan(lcrc, orc, engs[mode], data, mode)
+    finally:
+        for e in engs.values():
+            e.close()
+
+
+def test_wal_fused_headers_straddling_regions(lcrc, orc, monkeypatch):
+    """k_wal_windows walks a 32 KiB block as two 16 KiB regions: logs whose blocks put a header at every offset
+    16372..16389 around the boundary (its length and type bytes in the first region, the second, or both) parse
+    and verify exactly as the oracle's walk (log.rs:204-279)."""
+    monkeypatch.setenv("LCRC_WAL_FUSED", "1")
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    try:
+        recs = []
+        for at in range(16372, 16390):
+            # first record fills the block up to `at` (header 7 + payload), then short records
+            recs.append(b"\xab" * (at - 7))
+            recs += [bytes([at & 0xFF]) * 5, b"", b"\x01" * 300]
+            # pad the rest of the block with one record so the next logical record starts a fresh block
+            used = at + (7 + 5) + 7 + (7 + 300)
+            recs.append(b"\x02" * (32768 - used - 7))
+        data = orc.log_write(recs)
+        got = _wal_check_scan(lcrc, orc, eng, bytearray(data), 0)
+        assert (got["status"] == 0).all()
+        starts = set(int(h) % 32768 for h in got["header"])
+        assert set(range(16372, 16390)) <= starts
+    finally:
+        eng.close()
