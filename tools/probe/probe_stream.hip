@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <algorithm>
+#include <hip/hip_ext.h>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -123,7 +125,27 @@ static float best_ms(F f, int iters) {
   return best;
 }
 
-int main() {
+// one isolated launch at a time, timed by events carried by the launch itself (start of the first
+// wave to end of the last): the single-launch floor of a plain streaming read, to set beside k_windows
+template <typename F>
+static float single_us(F f) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  float v[12];
+  for (int rep = 0; rep < 15; ++rep) {
+    (void)hipDeviceSynchronize();
+    f(rep, a, b);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    if (rep >= 3) v[rep - 3] = ms * 1e3f;
+  }
+  std::sort(v, v + 12);
+  return (v[5] + v[6]) / 2;
+}
+
+int main(int argc, char** argv) {
   const size_t NB = 256ull << 20;
   const int NBUF = 4;
   uint8_t* buf;
@@ -133,6 +155,27 @@ int main() {
   k_fill<<<4096, 256>>>(buf, NB * NBUF);
   CK(hipDeviceSynchronize());
   auto rep = [&](const char* name, float ms) { printf("%-36s %7.1f us  %7.1f GB/s\n", name, ms * 1e3, NB / ms / 1e6); };
+  if (argc > 1) {  // buffers rotated as in bench.py's single launches (1 GiB in all, past the MALL)
+    for (int g : {256, 512, 1024, 2048, 4096}) {
+      char nm[64];
+      snprintf(nm, 64, "single buffer d8 nt g%d", g);
+      rep(nm, 1e-3f * single_us([&](int i, hipEvent_t a, hipEvent_t b) {
+            hipExtLaunchKernelGGL(k_buffer<8, 2>, dim3(g), dim3(256), 0, 0, a, b, 0,
+                                  (const uint8_t*)(buf + (i % NBUF) * NB), NB, out); }));
+      snprintf(nm, 64, "single buffer d16 nt g%d", g);
+      rep(nm, 1e-3f * single_us([&](int i, hipEvent_t a, hipEvent_t b) {
+            hipExtLaunchKernelGGL(k_buffer<16, 2>, dim3(g), dim3(256), 0, 0, a, b, 0,
+                                  (const uint8_t*)(buf + (i % NBUF) * NB), NB, out); }));
+      snprintf(nm, 64, "single global d8 nt g%d", g);
+      rep(nm, 1e-3f * single_us([&](int i, hipEvent_t a, hipEvent_t b) {
+            hipExtLaunchKernelGGL(k_global<8, true>, dim3(g), dim3(256), 0, 0, a, b, 0,
+                                  (const u32x4*)(buf + (i % NBUF) * NB), NB / 16, out); }));
+      snprintf(nm, 64, "single same-buffer buffer d8 nt g%d", g);
+      rep(nm, 1e-3f * single_us([&](int, hipEvent_t a, hipEvent_t b) {
+            hipExtLaunchKernelGGL(k_buffer<8, 2>, dim3(g), dim3(256), 0, 0, a, b, 0, (const uint8_t*)buf, NB, out); }));
+    }
+    return 0;
+  }
   for (int g : {1024, 2048, 4096}) {
     char nm[64];
     snprintf(nm, 64, "global d4 plain g%d", g);
