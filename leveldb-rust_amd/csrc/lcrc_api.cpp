@@ -35,20 +35,21 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
 hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
                                      uint32_t fin, uint32_t flags, hipStream_t st, hipEvent_t t_start,
                                      hipEvent_t t_stop);
-hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
-                               lcrc_tscan_dev* st, hipStream_t s);
-hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
-                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero,
-                                hipStream_t s);
-hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
-                               const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
+hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
+                                lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
+                                uint64_t bound, uint32_t* zero, uint64_t nzero, hipStream_t s);
+hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
+                               const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t vcap, uint64_t bound, hipStream_t s);
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
-                                 const uint8_t* file, lcrc_desc_dev* frames, uint64_t* size, uint64_t* nchunks,
-                                 uint8_t* fstatus, const lcrc_tscan_dev* st, const uint32_t* gtab, uint32_t flags,
-                                 hipStream_t s);
-hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, uint32_t* status_out,
-                               hipStream_t s);
+                                 const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
+                                 uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, const lcrc_tscan_dev* st,
+                                 const uint32_t* gtab, uint32_t flags, hipStream_t s);
+hipError_t lcrc_launch_ts_close(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t bound, const uint8_t* fstatus,
+                               const uint64_t* choff, const uint64_t* nch, const uint32_t* cmm, uint64_t* n_out,
+                               uint32_t* status_out, hipStream_t s);
+hipError_t lcrc_launch_scan2_add(uint64_t n, uint64_t* out_a, uint64_t* out_b, const uint64_t* part,
+                                 const uint64_t* n_dev, hipStream_t st);
 int lcrc_blocks_per_cu();
 hipError_t lcrc_launch_blocks(bool uniform, int grid, const uint8_t* base, uint64_t base_len,
                               const lcrc_desc_dev* descs, uint64_t n, uint64_t ustride, uint32_t ulen,
@@ -75,7 +76,7 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
                                      uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
-                                     uint64_t ts_chunk_cap, hipStream_t st);
+                                     uint64_t ts_chunk_cap, uint32_t inline_exp, hipStream_t st);
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
 hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
@@ -188,6 +189,7 @@ struct lcrc_ctx {
   DevBuf<uint32_t> sn_max;  // largest compressed / decoded chunk of a batch (sizes the decode's LDS)
   DevBuf<lcrc_desc_dev> sn_cdesc;
   DevBuf<uint32_t> sn_cexp, sn_cframe, sn_ccrc;
+  DevBuf<uint32_t> sn_cmm;  // the table scan's chunk mismatch bits (set or cleared by the CRC pass)
   DevBuf<uint64_t> sn_out_off;  // table scan: frame output offsets
   DevBuf<lcrc_tblk_dev> tbl_blk;  // table scan on the device: the blocks being assembled
   DevBuf<uint32_t> tbl_flag;      // = tbl_gen when that scan's blocks are out of offset order
@@ -409,7 +411,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   if (ctx->d_tab_c) (void)hipFree(ctx->d_tab_c);
   for (auto* b : {&ctx->sn_size, &ctx->sn_nch, &ctx->sn_choff, &ctx->sn_part, &ctx->sn_out_off}) b->release();
   ctx->sn_max.release();
-  for (auto* b : {&ctx->sn_cexp, &ctx->sn_cframe, &ctx->sn_ccrc}) b->release();
+  for (auto* b : {&ctx->sn_cexp, &ctx->sn_cframe, &ctx->sn_ccrc, &ctx->sn_cmm}) b->release();
   ctx->sn_cdesc.release();
   ctx->tbl_blk.release();
   ctx->tbl_flag.release();
@@ -1071,7 +1073,7 @@ static int snappy_run(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* f
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
-                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, 0, 0, st));
+                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, 0, 0, 0, st));
   // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
   if (ctx->general == 1) {
     static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
@@ -1327,7 +1329,8 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
       (rc = ctx->tbl_frames.ensure(nb)) || (rc = ctx->sn_size.ensure(nb)) || (rc = ctx->sn_nch.ensure(nb)) ||
       (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) || (rc = ctx->sn_status.ensure(nb)) ||
       (rc = ctx->sn_max.ensure(2)) || (rc = ctx->sn_cdesc.ensure(cc)) || (rc = ctx->sn_cexp.ensure(cc)) ||
-      (rc = ctx->sn_cframe.ensure(cc)) || (rc = ctx->sn_ccrc.ensure(cc)) || (rc = ctx->sn_out.ensure(decoded_cap + 16)) ||
+      (rc = ctx->sn_cframe.ensure(cc)) || (rc = ctx->sn_ccrc.ensure(cc)) || (rc = ctx->sn_cmm.ensure(cc / 32 + 1)) ||
+      (rc = ctx->sn_out.ensure(decoded_cap + 16)) ||
       (rc = ctx->win.ensure(window_words(max_file_len))))
     return rc;
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
@@ -1363,16 +1366,13 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   const uint64_t cap = max_blocks;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
-  // footer, index block header, the metaindex filter entry (optimistic: checksums come with the batch)
-  HIPCHK(lcrc_launch_ts_open(file, file_len, &key, cap, S, st));
-  // the index block's restart segments: entry counts, their scan, the handles and the verify descriptors
-  const uint64_t* nres_dev = &S->nres;
+  // Nine dependent launches. The footer, the index block header and the metaindex filter entry (optimistic:
+  // checksums come with the batch) with the index block's restart segments: entry counts, scanned per tile
   const uint64_t vcap = ts_verify_cap(cap, file_len);
-  HIPCHK(lcrc_launch_ts_count(file, file_len, S, ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->tbl_mm.p, vcap / 32 + 1,
-                              st));
-  HIPCHK(lcrc_launch_scan2(ctx->idx_count.p, ctx->idx_flag.p, cap, ctx->idx_pos.p, ctx->idx_fpos.p, ctx->sn_part.p,
-                           nres_dev, st));
-  HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_pos.p, ctx->idx_fpos.p, blk, ctx->tbl_descs.p, cap, vcap, cap,
+  HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
+                              ctx->tbl_mm.p, vcap / 32 + 1, st));
+  // the handles and the verify descriptors
+  HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_count.p, ctx->sn_part.p, blk, ctx->tbl_descs.p, cap, vcap, cap,
                              st));
   // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
   const uint64_t* ntot = &S->n_total;
@@ -1389,24 +1389,24 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
                                 nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     }
-    // read_block_from_file's type dispatch and the Snappy framing walk; the frames decoded (the decoded total
-    // checked against the workspace on the device) and their chunks' masked CRC-32C checked
-    HIPCHK(lcrc_launch_ts_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ctx->sn_size.p,
-                                 ctx->sn_nch.p, ctx->sn_status.p, S, ctx->d_tab, ctx->flags, st));
-    HIPCHK(lcrc_launch_scan2(ctx->sn_size.p, ctx->sn_nch.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_part.p,
-                             ntot, st));
+    // read_block_from_file's type dispatch and the Snappy framing walk (the frames' sizes scanned per workgroup,
+    // the scan finished by the add); the frames decoded (the decoded total checked against the workspace on the
+    // device), each chunk followed by its stored CRC, which the CRC pass compares
+    HIPCHK(lcrc_launch_ts_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ctx->sn_out_off.p,
+                                 ctx->sn_choff.p, ctx->sn_part.p, ctx->sn_nch.p, ctx->sn_status.p, S, ctx->d_tab,
+                                 ctx->flags, st));
+    HIPCHK(lcrc_launch_scan2_add(cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_part.p, ntot, st));
     HIPCHK(lcrc_launch_snappy_decode(file, ctx->tbl_frames.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_out.p,
                                      ctx->sn_status.p, ctx->sn_cdesc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, 8192, 8192,
-                                     ntot, S, ctx->ts_decoded_cap, ctx->ts_chunk_cap, st));  // 8 KiB LDS staging each way
+                                     ntot, S, ctx->ts_decoded_cap, ctx->ts_chunk_cap, 1, st));  // 8 KiB LDS staging each way
     HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, ctx->sn_out.p, ctx->ts_decoded_cap, ctx->sn_cdesc.p, ctx->ts_chunk_cap,
                               0, 0, nullptr, tab_c, x4096_c, lcrc::POLY_C, lcrc::CRC_INIT, lcrc::CRC_XOROUT,
-                              LCRC_FLAG_MASK, ctx->sn_ccrc.p, nullptr, &S->n_chunks, nullptr, st));
-    HIPCHK(lcrc_launch_snappy_check(ctx->sn_ccrc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, &S->n_chunks, ctx->ts_chunk_cap,
-                                    ctx->sn_status.p, st));
-    HIPCHK(lcrc_launch_tbl_content(blk, cap, ctx->sn_status.p, &S->unsorted, 1, ntot, st));
+                              LCRC_FLAG_MASK | LCRC_KFLAG_SETCLR, ctx->sn_ccrc.p, ctx->sn_cmm.p, &S->n_chunks, nullptr,
+                              st));
   }
-  // the reference's order of outcomes; the count and the status for the caller
-  HIPCHK(lcrc_launch_ts_final(S, blk, n_blocks, status, st));
+  // the content verdicts and the reference's order of outcomes; the count and the status for the caller
+  HIPCHK(lcrc_launch_ts_close(S, blk, cap, ctx->sn_status.p, ctx->sn_choff.p, ctx->sn_nch.p, ctx->sn_cmm.p, n_blocks,
+                              status, st));
   return LCRC_OK;
 }
 

@@ -16,7 +16,8 @@
 //   * k_ranges does arbitrary ranges in one pass instead: 4 KiB chunks per 16-lane row with k_windows'
 //     loads and walk, zero-padded by the buffer range check, the padding undone by one GF(2) multiply.
 //   * Snappy framing: k_snappy_size (framing walk), k_snappy_decode_wave (one wave per frame, LDS-staged,
-//     data-parallel element parse), k_snappy_check; table scan: k_idx_parse, k_tbl_finish, k_tbl_content.
+//     data-parallel element parse), k_snappy_check; table scan: k_idx_parse, k_tbl_finish, k_tbl_content
+//     (host-walked index), and the device-only scan k_ts_index, k_ts_emit, k_ts_finish, k_ts_close.
 //   * k_wal_parse walks the 7-byte headers of every 32 KiB log block (src/db/log.rs:204-279) into
 //     record descriptors for k_blocks.
 #include <hip/hip_runtime.h>
@@ -2047,9 +2048,12 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
 
 // the framing walk of one frame p[0, len): decoded size, data-chunk count, largest compressed data (after the
 // crc) and decoded chunk; false when the framing is malformed
+// padded: the bytes the table scan's decode takes, each chunk 16-aligned with its stored CRC in the 16 B after it
 __device__ __forceinline__ bool snappy_frame_size(const uint8_t* __restrict__ p, uint32_t len, uint64_t& total,
-                                                  uint64_t& chunks, uint32_t& max_in, uint32_t& max_out) {
+                                                  uint64_t& chunks, uint32_t& max_in, uint32_t& max_out,
+                                                  uint64_t& padded) {
   total = 0;
+  padded = 0;
   chunks = 0;
   max_in = 0;
   max_out = 0;
@@ -2081,6 +2085,7 @@ __device__ __forceinline__ bool snappy_frame_size(const uint8_t* __restrict__ p,
       if (type == 0 && cl - 4 > max_in) max_in = cl - 4;
       if (ulen > max_out) max_out = ulen;
       total += ulen;
+      padded += ((ulen + 15) & ~15u) + 16;
       ++chunks;
     } else if (type <= 0x7f) {
       ok = false;  // reserved unskippable
@@ -2102,7 +2107,8 @@ __global__ void __launch_bounds__(256) k_snappy_size(const uint8_t* __restrict__
   const uint32_t len = f < n ? frames[f].length : 0u;
   uint64_t total, chunks;
   uint32_t max_in, max_out;
-  const bool ok = snappy_frame_size(p, len, total, chunks, max_in, max_out);
+  uint64_t padded;
+  const bool ok = snappy_frame_size(p, len, total, chunks, max_in, max_out, padded);
   if (f < n) {
     size[f] = ok ? total : 0;
     nchunks[f] = ok ? chunks : 0;
@@ -2364,7 +2370,7 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
                                                            uint32_t in_lim, uint32_t out_cap,
                                                            const uint64_t* __restrict__ n_dev,
                                                            lcrc_tscan_dev* __restrict__ ts, uint64_t ts_out_cap,
-                                                           uint64_t ts_chunk_cap) {
+                                                           uint64_t ts_chunk_cap, uint32_t inline_exp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sn_lds[];
   if (n_dev) n = *n_dev < n ? *n_dev : n;
   if (ts) {
@@ -2487,15 +2493,20 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
         o = ((uint64_t)bcast((uint32_t)(o >> 32)) << 32) | bcast((uint32_t)o);
       }
       if (!ok) break;
+      // inline_exp (table scan): the stored CRC goes into the 16 B after the 16-aligned chunk, where the CRC pass
+      // compares it (expect_rel) -- no separate check launch; the next chunk starts 16-aligned
+      const uint32_t clen = (uint32_t)(o - start), pad = (clen + 15) & ~15u;
       if (lane == 0) {
         lcrc_desc_dev d;
         d.offset = start;
-        d.length = (uint32_t)(o - start);
-        d.expect_rel = LCRC_NO_EXPECT_DEV;
+        d.length = clen;
+        d.expect_rel = inline_exp ? (int32_t)pad : LCRC_NO_EXPECT_DEV;
         cdesc[c] = d;
         cexp[c] = want;
         cframe[c] = (uint32_t)f;
+        if (inline_exp) *(uint32_t*)(out + start + pad) = want;
       }
+      if (inline_exp) o = start + pad + 16;
       ++c;
     }
     if (!ok && lane == 0) {
@@ -2558,11 +2569,9 @@ __device__ __forceinline__ uint32_t dev_varint(const uint8_t* __restrict__ d, ui
 // (tblk offset/size, kind DATA) at pos[i] .. and their verify descriptors; a handle past the end of the file
 // gets an empty descriptor and status TRUNCATED.
 template <bool PASS2>
-__device__ __forceinline__ void idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
-                                            uint64_t file_len, uint64_t* __restrict__ count,
-                                            uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos,
-                                            lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs,
-                                            uint64_t i);
+__device__ __forceinline__ uint64_t idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
+                                                uint64_t file_len, uint64_t o0, lcrc_tblk_dev* __restrict__ out,
+                                                lcrc_desc_dev* __restrict__ descs, uint64_t i, bool& bad);
 
 template <bool PASS2>
 __global__ void __launch_bounds__(256) k_idx_parse(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
@@ -2570,20 +2579,25 @@ __global__ void __launch_bounds__(256) k_idx_parse(const uint8_t* __restrict__ d
                                                    uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos,
                                                    lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nres) idx_segment<PASS2>(d, len, nres, file_len, count, flag, pos, out, descs, i);
+  if (i >= nres) return;
+  bool bad;
+  const uint64_t n = idx_segment<PASS2>(d, len, nres, file_len, PASS2 ? pos[i] : 0, out, descs, i, bad);
+  if (!PASS2) {
+    count[i] = bad ? 0 : n;
+    flag[i] = bad ? 1 : 0;
+  }
 }
 
+// PASS 1: returns the entries of segment i (bad: the host must walk it). PASS 2: writes them from slot o0 on.
 template <bool PASS2>
-__device__ __forceinline__ void idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
-                                            uint64_t file_len, uint64_t* __restrict__ count,
-                                            uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos,
-                                            lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs,
-                                            uint64_t i) {
+__device__ __forceinline__ uint64_t idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
+                                                uint64_t file_len, uint64_t o0, lcrc_tblk_dev* __restrict__ out,
+                                                lcrc_desc_dev* __restrict__ descs, uint64_t i, bool& bad) {
   const uint32_t restarts = len - (1 + nres) * 4;
   auto rst = [&](uint32_t k) { return load_le32(d + restarts + 4 * k); };
   const uint32_t start = rst((uint32_t)i);
   const uint32_t end = i + 1 < nres ? rst((uint32_t)i + 1) : restarts;
-  bool bad = (i == 0 && start != 0) || start > end || end > restarts;
+  bad = (i == 0 && start != 0) || start > end || end > restarts;
   uint64_t n = 0;
   uint32_t off = start;
   for (uint32_t guard = 0; !bad && off < end; ++guard) {
@@ -2609,7 +2623,7 @@ __device__ __forceinline__ void idx_segment(const uint8_t* __restrict__ d, uint3
       break;
     }
     if (PASS2) {
-      const uint64_t o = pos[i] + n;
+      const uint64_t o = o0 + n;
       lcrc_tblk_dev b;
       b.offset = hoff;
       b.size = hsize;
@@ -2633,10 +2647,7 @@ __device__ __forceinline__ void idx_segment(const uint8_t* __restrict__ d, uint3
     ++n;
     off = (uint32_t)(p + non_shared + vlen);
   }
-  if (!PASS2) {
-    count[i] = bad ? 0 : n;
-    flag[i] = bad ? 1 : 0;
-  }
+  return n;
 }
 
 // per block: computed crc, stored type, status (mismatch / bad type), and the Snappy frame to check when
@@ -2687,32 +2698,28 @@ __global__ void __launch_bounds__(256) k_tbl_content(lcrc_tblk_dev* __restrict__
 // Asynchronous whole-table scan (lcrc_table_scan_async): Table::open + read_meta + one verify of every block
 // (table.rs:39-146, format.rs:146-213) with no host round trip. The index and metaindex are walked
 // OPTIMISTICALLY, before their own checksums are known: both are verified in the same batch as the data
-// blocks, and k_ts_final applies the reference's order afterwards (index checksum before any index-contents
+// blocks, and k_ts_close applies the reference's order afterwards (index checksum before any index-contents
 // error; the filter block named by a metaindex that does not verify is dropped, as read_meta swallows it).
 // Whatever the device walk cannot vouch for sets status 2 and the synchronous wrapper walks on the host.
 // ---------------------------------------------------------------------------------------------------
 enum { TS_OK = 0, TS_CORRUPT = 1, TS_HOST = 2, TS_CAPACITY = 3 };
 enum { TSM_SHORT = 1, TSM_MAGIC = 2, TSM_VARINT = 3, TSM_CHECKSUM = 4, TSM_TYPE = 5, TSM_SMALL = 6, TSM_CONTENTS = 7 };
 
-// footer, index block header, metaindex filter entry: one thread
-__global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                const lcrc_tscan_key fkey, uint64_t seg_cap,
-                                                lcrc_tscan_dev* __restrict__ st) {
-  __shared__ uint8_t key[256];
-  if (threadIdx.x != 0) return;
-  lcrc_tscan_dev s = {};
-  auto done = [&]() { *st = s; };
+// footer, index block header and (meta) the metaindex filter entry, by one thread; key: 256 B of LDS
+__device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_len, const lcrc_tscan_key& fkey,
+                              uint64_t seg_cap, uint8_t* __restrict__ key, bool meta, lcrc_tscan_dev& s) {
+  s = {};
   if (file_len < 48) {
     s.status = TS_CORRUPT;
     s.code = TSM_SHORT;
-    return done();
+    return;
   }
   const uint8_t* f = file + file_len - 48;
   const uint64_t magic = (uint64_t)load_le32(f + 40) | ((uint64_t)load_le32(f + 44) << 32);
   if (magic != 0xdb4775248b80fb57ull) {
     s.status = TS_CORRUPT;
     s.code = TSM_MAGIC;
-    return done();
+    return;
   }
   uint32_t p = dev_varint<64>(f, 0, 48, &s.meta_off);
   if (p != ~0u) p = dev_varint<64>(f, p, 48, &s.meta_size);
@@ -2721,18 +2728,18 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
   if (p == ~0u) {
     s.status = TS_CORRUPT;
     s.code = TSM_VARINT;
-    return done();
+    return;
   }
   // Table::open reads the index block (verified: paranoid_checks); its checksum comes with the batch
   if (s.idx_off > file_len || s.idx_size + 5 > file_len - s.idx_off || s.idx_size + 1 > 0x7FFFFFFFull) {
     s.status = TS_HOST;  // "truncated block read" and its kin: the host walk
-    return done();
+    return;
   }
   const uint8_t itype = file[s.idx_off + s.idx_size];
   const uint64_t clen = s.idx_size;
   if (itype == 1) {
     s.status = TS_HOST;  // a Snappy-framed index block: decoded on the host path
-    return done();
+    return;
   }
   if (itype > 1) {
     s.pcode = TSM_TYPE;
@@ -2744,24 +2751,24 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
       s.pcode = TSM_CONTENTS;
     } else if (nres == 0 || (clen - 4) / nres > 4096) {
       s.status = TS_HOST;  // no restart points / long segments: the sequential host walk
-      return done();
+      return;
     } else if (nres + 2 > seg_cap) {
       s.status = TS_CAPACITY;  // at least one block per segment: more than the result can hold
       s.n_data = nres + 2;
-      return done();
+      return;
     } else {
       s.nres = nres;
     }
   }
   // read_meta (only with a filter policy): the first metaindex key >= "filter" + name; a malformed
   // metaindex yields no filter, as the reference swallows read_meta's errors
-  if (fkey.len && s.meta_off <= file_len && s.meta_size + 5 <= file_len - s.meta_off && s.meta_size <= 0xFFFFFFFFull) {
+  if (meta && fkey.len && s.meta_off <= file_len && s.meta_size + 5 <= file_len - s.meta_off && s.meta_size <= 0xFFFFFFFFull) {
     const uint8_t* d = file + s.meta_off;
     const uint64_t n = s.meta_size;
     const uint8_t mtype = d[n];
     if (mtype == 1) {
       s.status = TS_HOST;  // compressed metaindex: the host path decodes it
-      return done();
+      return;
     }
     if (mtype == 0 && n >= 4) {
       const uint32_t nr = load_le32(d + n - 4);
@@ -2777,7 +2784,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
           if (q == ~0u || (uint64_t)restarts - q < non_shared + vlen || klen < shared) break;
           if (shared + non_shared > sizeof(key)) {
             s.status = TS_HOST;  // a key longer than the walk's buffer
-            return done();
+            return;
           }
           for (uint32_t i = 0; i < non_shared; ++i) key[shared + i] = d[q + i];
           klen = (uint32_t)(shared + non_shared);
@@ -2804,43 +2811,132 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
       }
     }
   }
-  done();
 }
 
-// pass 1 over the restart segments, the count taken from the device state (grid-stride)
-__global__ void __launch_bounds__(256) k_ts_count(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                  const lcrc_tscan_dev* __restrict__ st, uint64_t* __restrict__ count,
-                                                  uint64_t* __restrict__ flag, uint32_t* __restrict__ zero,
-                                                  uint64_t nzero) {
+// Workgroup-wide exclusive scan of two u64 values per thread (256 threads): e* = the sums over the threads
+// before this one, t* = the workgroup's totals. s*: 4 words of LDS each.
+__device__ __forceinline__ void wg_scan2(uint64_t va, uint64_t vb, uint64_t* sa, uint64_t* sb, uint64_t& ea,
+                                         uint64_t& eb, uint64_t& ta, uint64_t& tb) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long ia = va, ib = vb;
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long xa = __shfl_up(ia, d, 64), xb = __shfl_up(ib, d, 64);
+    if (lane >= (uint32_t)d) {
+      ia += xa;
+      ib += xb;
+    }
+  }
+  if (lane == 63) {
+    sa[w] = ia;
+    sb[w] = ib;
+  }
+  __syncthreads();
+  uint64_t pa = 0, pb = 0;
+  ta = tb = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    if (k < w) {
+      pa += sa[k];
+      pb += sb[k];
+    }
+    ta += sa[k];
+    tb += sb[k];
+  }
+  __syncthreads();  // the caller may reuse sa / sb
+  ea = pa + ia - va;
+  eb = pb + ib - vb;
+}
+
+// sums of part[2 w] and part[2 w + 1] over w in [lo, hi), by a 256-thread workgroup (every thread gets them)
+__device__ __forceinline__ void wg_sum_parts(const uint64_t* __restrict__ part, uint64_t lo, uint64_t hi, uint64_t* sa,
+                                             uint64_t* sb, uint64_t& ra, uint64_t& rb) {
+  unsigned long long xa = 0, xb = 0;
+  for (uint64_t w = lo + threadIdx.x; w < hi; w += 256) {
+    xa += part[2 * w];
+    xb += part[2 * w + 1];
+  }
+  for (int d = 1; d < 64; d <<= 1) {
+    xa += __shfl_xor(xa, d, 64);
+    xb += __shfl_xor(xb, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sa[threadIdx.x >> 6] = xa;
+    sb[threadIdx.x >> 6] = xb;
+  }
+  __syncthreads();
+  ra = sa[0] + sa[1] + sa[2] + sa[3];
+  rb = sb[0] + sb[1] + sb[2] + sb[3];
+  __syncthreads();
+}
+
+// The table scan's first launch: the footer and the index block header (thread 0 of every workgroup, so that
+// no launch waits on them; workgroup 0 also walks the metaindex and records the state), then pass 1 over the
+// restart segments in 256-segment tiles: entry counts and fallback flags, scanned within the tile (local[i]),
+// the tile totals in part[2 t], part[2 t + 1]. k_ts_emit adds the totals of the tiles before.
+__global__ void __launch_bounds__(256) k_ts_index(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                  const lcrc_tscan_key fkey, uint64_t seg_cap,
+                                                  lcrc_tscan_dev* __restrict__ st, uint64_t* __restrict__ local_c,
+                                                  uint64_t* __restrict__ local_f, uint64_t* __restrict__ part,
+                                                  uint32_t* __restrict__ zero, uint64_t nzero) {
+  __shared__ uint8_t key[256];
+  __shared__ uint64_t hdr[3], sa[4], sb[4];
   // the batch's mismatch bitmap starts at zero (no memset launch)
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (uint64_t)gridDim.x * blockDim.x)
     zero[i] = 0;
-  if (st->status != TS_OK) return;
-  const uint64_t nres = st->nres;
-  const uint8_t* d = file + st->idx_off;
-  const uint32_t len = (uint32_t)st->idx_size;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nres; i += (uint64_t)gridDim.x * blockDim.x)
-    idx_segment<false>(d, len, (uint32_t)nres, file_len, count, flag, nullptr, nullptr, nullptr, i);
+  if (threadIdx.x == 0) {
+    lcrc_tscan_dev s;
+    ts_open_state(file, file_len, fkey, seg_cap, key, blockIdx.x == 0, s);
+    if (blockIdx.x == 0) *st = s;
+    hdr[0] = s.nres;  // 0 unless the index block can be walked (a later metaindex verdict changes nothing here)
+    hdr[1] = s.idx_off;
+    hdr[2] = s.idx_size;
+  }
+  __syncthreads();
+  const uint64_t nres = hdr[0];
+  const uint8_t* d = file + hdr[1];
+  const uint32_t len = (uint32_t)hdr[2];
+  for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = t0 + threadIdx.x;
+    uint64_t c = 0, f = 0;
+    if (i < nres) {
+      bool bad;
+      const uint64_t n = idx_segment<false>(d, len, (uint32_t)nres, file_len, 0, nullptr, nullptr, i, bad);
+      c = bad ? 0 : n;
+      f = bad ? 1 : 0;
+    }
+    uint64_t ec, ef, tc, tf;
+    wg_scan2(c, f, sa, sb, ec, ef, tc, tf);
+    if (i < nres) {
+      local_c[i] = ec;
+      local_f[i] = ef;
+    }
+    if (threadIdx.x == 0) {
+      part[2 * (t0 / 256)] = tc;
+      part[2 * (t0 / 256) + 1] = tf;
+    }
+  }
 }
 
-// after the scan of the counts: the data-block total, the capacity check and the fallback flags (decided
-// alike by every workgroup from the scan; workgroup 0 records them), then pass 2 writes the handles and
-// thread 0 appends the filter, metaindex and index blocks with their descriptors
+// after pass 1: the data-block total, the capacity check and the fallback flags (decided alike by every
+// workgroup from the tile totals; workgroup 0 records them), then pass 2 writes the handles (slot = the tiles
+// before + the segment's place in its tile) and thread 0 appends the filter, metaindex and index blocks with
+// their descriptors
 __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                 lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ pos,
-                                                 const uint64_t* __restrict__ fpos, lcrc_tblk_dev* __restrict__ out,
+                                                 lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ local_c,
+                                                 const uint64_t* __restrict__ part, lcrc_tblk_dev* __restrict__ out,
                                                  lcrc_desc_dev* __restrict__ descs, uint64_t cap, uint64_t vcap) {
-  const uint32_t status = st->status;  // as k_ts_open left it (workgroup 0 changes it only to a non-OK value)
+  __shared__ uint64_t sa[4], sb[4];
+  const uint32_t status = st->status;  // as k_ts_index left it
   const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
   if (status != TS_OK) {
     if (lead) st->n_total = 0;
     return;
   }
   const uint64_t nres = st->nres;
-  const uint64_t nd = nres ? pos[nres] : 0;
+  uint64_t nd = 0, nflag = 0;
+  wg_sum_parts(part, 0, (nres + 255) / 256, sa, sb, nd, nflag);
   const bool hf = st->has_filter;
   const uint64_t ntot = nd + (hf ? 3 : 2);
-  if (nres && fpos[nres]) {
+  if (nres && nflag) {
     // a segment the device walk cannot vouch for. The reference checks the index block's checksum before its
     // contents: verify it alone, and let the host walk give the contents' message only if it holds
     if (lead) {
@@ -2857,7 +2953,7 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
       b.kind = 3;  // LCRC_TBLK_INDEX
       lcrc_desc_dev dd;
       dd.offset = st->idx_off;
-      dd.length = (uint32_t)(st->idx_size + 1);  // in the file: checked by k_ts_open
+      dd.length = (uint32_t)(st->idx_size + 1);  // in the file: checked by k_ts_index
       dd.expect_rel = (int32_t)(st->idx_size + 1);
       out[0] = b;
       descs[0] = dd;
@@ -2892,8 +2988,13 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
   }
   const uint8_t* d = file + st->idx_off;
   const uint32_t len = (uint32_t)st->idx_size;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nres; i += (uint64_t)gridDim.x * blockDim.x)
-    idx_segment<true>(d, len, (uint32_t)nres, file_len, nullptr, nullptr, pos, out, descs, i);
+  for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
+    uint64_t base, bf;
+    wg_sum_parts(part, 0, t0 / 256, sa, sb, base, bf);
+    const uint64_t i = t0 + threadIdx.x;
+    bool bad;
+    if (i < nres) idx_segment<true>(d, len, (uint32_t)nres, file_len, base + local_c[i], out, descs, i, bad);
+  }
   if (blockIdx.x == 0 && threadIdx.x < 3) {
     const uint32_t k = threadIdx.x;  // 0 filter (if any), then metaindex, index
     if (k == 0 && !hf) return;
@@ -2938,14 +3039,18 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
 
 // read_block_from_file's type dispatch for every block (k_tbl_finish) and, in the same thread, the framing
 // walk of the block's Snappy frame (k_snappy_size)
+// The frames' decoded sizes (padded, see snappy_frame_size) and chunk counts are scanned within the workgroup
+// (out_off, choff) with the workgroup totals in part[2 b], part[2 b + 1]: k_scan2_add finishes the scan.
 __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
                                                    const uint32_t* __restrict__ crc,
                                                    const uint32_t* __restrict__ mismatch,
                                                    const uint8_t* __restrict__ file, lcrc_desc_dev* __restrict__ frames,
-                                                   uint64_t* __restrict__ size, uint64_t* __restrict__ nchunks,
+                                                   uint64_t* __restrict__ out_off, uint64_t* __restrict__ choff,
+                                                   uint64_t* __restrict__ part, uint64_t* __restrict__ nchunks,
                                                    uint8_t* __restrict__ fstatus, const lcrc_tscan_dev* __restrict__ st,
                                                    const uint32_t* __restrict__ gtab, uint32_t flags) {
   __shared__ uint32_t z64k[1024];
+  __shared__ uint64_t sa[4], sb[4];
   n = st->n_total < n ? st->n_total : n;
   const uint64_t nd = st->n_data;
   const bool hf = st->has_filter;
@@ -2960,49 +3065,63 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
     for (uint32_t j = threadIdx.x; j < 1024; j += blockDim.x) z64k[j] = gtab[TAB_Z64K + j];
     __syncthreads();
   }
+  if ((uint64_t)blockIdx.x * blockDim.x >= n) return;  // a whole workgroup past the count (uniform)
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  lcrc_tblk_dev b = blk[i];
-  uint32_t flen = 0;
-  if (b.status != 2) {
-    b.crc = crc[i];
-    b.type = file[b.offset + b.size];
-    b.status = (mismatch[i >> 5] >> (i & 31)) & 1;
-    const uint32_t k = i < nd ? 3u : (uint32_t)(i - nd) + (hf ? 0u : 1u);
-    if (k < 3 && st->pcnt[k]) {
-      // a block verified as pieces: crc(A || B) = Z_|B|(crc(A)) ^ crc(B) (init = xorout = ~0); every piece
-      // after the first is 64 KiB long
-      const uint32_t* pc = crc + st->pbase[k];
-      const uint32_t np = st->pcnt[k];
-      const bool masked = flags & LCRC_FLAG_MASK;
-      auto unmask = [&](uint32_t v) {
-        if (!masked) return v;
-        const uint32_t r = v - 0xa282ead8u;
-        return (r >> 17) | (r << 15);
-      };
-      uint32_t c = unmask(pc[0]);
-      for (uint32_t q = 1; q < np; ++q)
-        c = z64k[c & 0xff] ^ z64k[256 + ((c >> 8) & 0xff)] ^ z64k[512 + ((c >> 16) & 0xff)] ^ z64k[768 + (c >> 24)] ^
-            unmask(pc[q]);
-      if (masked) c = mask32c(c);
-      b.crc = c;
-      b.status = c != load_le32(file + b.offset + b.size + 1);
+  uint64_t fsize = 0, fch = 0;
+  if (i < n) {
+    lcrc_tblk_dev b = blk[i];
+    uint32_t flen = 0;
+    if (b.status != 2) {
+      b.crc = crc[i];
+      b.type = file[b.offset + b.size];
+      b.status = (mismatch[i >> 5] >> (i & 31)) & 1;
+      const uint32_t k = i < nd ? 3u : (uint32_t)(i - nd) + (hf ? 0u : 1u);
+      if (k < 3 && st->pcnt[k]) {
+        // a block verified as pieces: crc(A || B) = Z_|B|(crc(A)) ^ crc(B) (init = xorout = ~0); every piece
+        // after the first is 64 KiB long
+        const uint32_t* pc = crc + st->pbase[k];
+        const uint32_t np = st->pcnt[k];
+        const bool masked = flags & LCRC_FLAG_MASK;
+        auto unmask = [&](uint32_t v) {
+          if (!masked) return v;
+          const uint32_t r = v - 0xa282ead8u;
+          return (r >> 17) | (r << 15);
+        };
+        uint32_t c = unmask(pc[0]);
+        for (uint32_t q = 1; q < np; ++q)
+          c = z64k[c & 0xff] ^ z64k[256 + ((c >> 8) & 0xff)] ^ z64k[512 + ((c >> 16) & 0xff)] ^ z64k[768 + (c >> 24)] ^
+              unmask(pc[q]);
+        if (masked) c = mask32c(c);
+        b.crc = c;
+        b.status = c != load_le32(file + b.offset + b.size + 1);
+      }
+      if (b.status == 0 && b.type > 1) b.status = 4;  // LCRC_TBLK_BAD_TYPE
+      if (b.status == 0 && b.type == 1) flen = (uint32_t)b.size;
     }
-    if (b.status == 0 && b.type > 1) b.status = 4;  // LCRC_TBLK_BAD_TYPE
-    if (b.status == 0 && b.type == 1) flen = (uint32_t)b.size;
+    lcrc_desc_dev f;
+    f.offset = flen ? b.offset : 0;
+    f.length = flen;
+    f.expect_rel = LCRC_NO_EXPECT_DEV;
+    blk[i] = b;
+    frames[i] = f;
+    uint64_t total, chunks, padded;
+    uint32_t mi, mo;
+    const bool ok = snappy_frame_size(file + f.offset, flen, total, chunks, mi, mo, padded);
+    fsize = ok ? padded : 0;
+    fch = ok ? chunks : 0;
+    nchunks[i] = fch;
+    fstatus[i] = ok ? 0 : 1;
   }
-  lcrc_desc_dev f;
-  f.offset = flen ? b.offset : 0;
-  f.length = flen;
-  f.expect_rel = LCRC_NO_EXPECT_DEV;
-  blk[i] = b;
-  frames[i] = f;
-  uint64_t total, chunks;
-  uint32_t mi, mo;
-  const bool ok = snappy_frame_size(file + f.offset, flen, total, chunks, mi, mo);
-  size[i] = ok ? total : 0;
-  nchunks[i] = ok ? chunks : 0;
-  fstatus[i] = ok ? 0 : 1;
+  uint64_t eo, ec, to, tc;
+  wg_scan2(fsize, fch, sa, sb, eo, ec, to, tc);
+  if (i < n) {
+    out_off[i] = eo;
+    choff[i] = ec;
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = to;
+    part[2 * blockIdx.x + 1] = tc;
+  }
 }
 
 // the reference's order of outcomes, once every checksum is known; the count and the status for the caller
@@ -3033,15 +3152,41 @@ __device__ void ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restr
       s.n_total = n - 1;
     }
   }
-  *st = s;
+  // only the fields decided here (k_ts_close's other threads may be setting st->unsorted)
+  st->status = s.status;
+  st->code = s.code;
+  st->n_total = s.n_total;
   *n_out = s.status == TS_OK ? s.n_total : s.status == TS_CAPACITY ? s.n_data : 0;
   status_out[0] = s.status;
   status_out[1] = s.code;
 }
 
-__global__ void __launch_bounds__(64) k_ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
-                                                 uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out) {
-  if (threadIdx.x == 0) ts_final(st, blk, n_out, status_out);
+// The table scan's last launch. Every block's content verdict -- its Snappy frame failed the framing walk or
+// the decode (fstatus), or one of its chunks' masked CRC-32C differs from the stored one (the CRC pass's
+// mismatch bits cmm; not read when the gate sent the frames to the host) -- and the order check of the
+// offsets, then the reference's order of outcomes (ts_final). The last three blocks (filter, metaindex,
+// index), which ts_final may move, are thread 0 of workgroup 0's alone.
+__global__ void __launch_bounds__(256) k_ts_close(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
+                                                  const uint8_t* __restrict__ fstatus,
+                                                  const uint64_t* __restrict__ choff, const uint64_t* __restrict__ nch,
+                                                  const uint32_t* __restrict__ cmm, uint64_t* __restrict__ n_out,
+                                                  uint32_t* __restrict__ status_out) {
+  const uint64_t n = st->n_total;
+  const bool bits = st->gate == 0;
+  auto content = [&](uint64_t j) {
+    bool bad = fstatus[j] != 0;
+    if (bits)
+      for (uint64_t c = choff[j], ce = c + nch[j]; !bad && c < ce; ++c) bad = (cmm[c >> 5] >> (c & 31)) & 1;
+    if (bad) blk[j].status = 3;  // LCRC_TBLK_BAD_CONTENT
+    if (j > 0 && blk[j - 1].offset > blk[j].offset) st->unsorted = 1;
+  };
+  const uint64_t tail = n > 3 ? n - 3 : 0;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < tail) content(i);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (uint64_t j = tail; j < n; ++j) content(j);
+    ts_final(st, blk, n_out, status_out);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -3204,40 +3349,38 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
 }
 
 // ---- asynchronous table scan (lcrc_table_scan_async) ----
-hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
-                               lcrc_tscan_dev* st, hipStream_t s) {
-  LCRC_LAUNCH(lcrc_dev::k_ts_open, dim3(1), dim3(64), 0, s, file, file_len, *key, cap, st);
-  return hipGetLastError();
-}
-// grid: a bound on the restart segments (the workgroups past the device count return at once)
-hipError_t lcrc_launch_ts_count(const uint8_t* file, uint64_t file_len, const lcrc_tscan_dev* st, uint64_t* count,
-                                uint64_t* flag, uint64_t bound, uint32_t* zero, uint64_t nzero,
-                                hipStream_t s) {
+// grid: a bound on the restart segments (the workgroups past the device count only zero their share)
+hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
+                                lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
+                                uint64_t bound, uint32_t* zero, uint64_t nzero, hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
-  LCRC_LAUNCH(lcrc_dev::k_ts_count, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
-                     count, flag, zero, nzero);
+  LCRC_LAUNCH(lcrc_dev::k_ts_index, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, *key, cap,
+              st, local_c, local_f, part, zero, nzero);
   return hipGetLastError();
 }
-hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* pos,
-                               const uint64_t* fpos, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
+hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
+                               const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t vcap, uint64_t bound, hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
   LCRC_LAUNCH(lcrc_dev::k_ts_emit, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
-                     pos, fpos, out, descs, cap, vcap);
+              local_c, part, out, descs, cap, vcap);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
-                                 const uint8_t* file, lcrc_desc_dev* frames, uint64_t* size, uint64_t* nchunks,
-                                 uint8_t* fstatus, const lcrc_tscan_dev* st, const uint32_t* gtab, uint32_t flags,
-                                 hipStream_t s) {
+                                 const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
+                                 uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, const lcrc_tscan_dev* st,
+                                 const uint32_t* gtab, uint32_t flags, hipStream_t s) {
   if (n == 0) return hipSuccess;
   LCRC_LAUNCH(lcrc_dev::k_ts_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, blk, n, crc, mismatch,
-                     file, frames, size, nchunks, fstatus, st, gtab, flags);
+              file, frames, out_off, choff, part, nchunks, fstatus, st, gtab, flags);
   return hipGetLastError();
 }
-hipError_t lcrc_launch_ts_final(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t* n_out, uint32_t* status_out,
-                               hipStream_t s) {
-  LCRC_LAUNCH(lcrc_dev::k_ts_final, dim3(1), dim3(64), 0, s, st, blk, n_out, status_out);
+// grid: a bound on the blocks
+hipError_t lcrc_launch_ts_close(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t bound, const uint8_t* fstatus,
+                               const uint64_t* choff, const uint64_t* nch, const uint32_t* cmm, uint64_t* n_out,
+                               uint32_t* status_out, hipStream_t s) {
+  LCRC_LAUNCH(lcrc_dev::k_ts_close, dim3((unsigned)(bound / 256 + 1)), dim3(256), 0, s, st, blk, fstatus, choff, nch,
+              cmm, n_out, status_out);
   return hipGetLastError();
 }
 
@@ -3361,6 +3504,14 @@ hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* fra
 
 // out_a / out_b: n + 1 entries (exclusive scans, totals at [n]); part: 2 * ceil(n / 256) scratch words
 // n_dev (nullable): the count produced on the device, n is then its bound (the grid is sized by n + 1)
+// the second half of lcrc_launch_scan2, after a kernel that scanned within its 256-entry workgroups
+hipError_t lcrc_launch_scan2_add(uint64_t n, uint64_t* out_a, uint64_t* out_b, const uint64_t* part,
+                                 const uint64_t* n_dev, hipStream_t st) {
+  const uint64_t g = n_dev ? n / 256 + 1 : (n + 255) / 256;
+  if (g == 0) return hipMemsetAsync(out_a, 0, 8, st) == hipSuccess ? hipMemsetAsync(out_b, 0, 8, st) : hipErrorUnknown;
+  LCRC_LAUNCH(lcrc_dev::k_scan2_add, dim3((unsigned)g), dim3(256), 0, st, n, out_a, out_b, part, n_dev);
+  return hipGetLastError();
+}
 hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
                              uint64_t* part, const uint64_t* n_dev, hipStream_t st) {
   const uint64_t g = n_dev ? n / 256 + 1 : (n + 255) / 256;
@@ -3374,7 +3525,7 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
                                      uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
-                                     uint64_t ts_chunk_cap, hipStream_t st) {
+                                     uint64_t ts_chunk_cap, uint32_t inline_exp, hipStream_t st) {
   using lcrc_dev::SN_MAX;
   if (n == 0) return hipSuccess;
   const uint64_t g = n < 16384 ? n : 16384;  // one wave per frame, grid-stride
@@ -3384,7 +3535,7 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
   const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
   LCRC_LAUNCH(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
                      chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, ts, ts_out_cap,
-                     ts_chunk_cap);
+                     ts_chunk_cap, inline_exp);
   return hipGetLastError();
 }
 
