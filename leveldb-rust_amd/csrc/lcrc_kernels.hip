@@ -2782,7 +2782,7 @@ __device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_le
           if (q != ~0u) q = dev_varint<32>(d, q, restarts, &non_shared);
           if (q != ~0u) q = dev_varint<32>(d, q, restarts, &vlen);
           if (q == ~0u || (uint64_t)restarts - q < non_shared + vlen || klen < shared) break;
-          if (shared + non_shared > sizeof(key)) {
+          if (shared + non_shared > 256) {  // the LDS key buffer
             s.status = TS_HOST;  // a key longer than the walk's buffer
             return;
           }
