@@ -37,10 +37,10 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
                                      hipEvent_t t_stop);
 hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                 lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
-                                uint64_t bound, uint32_t* zero, uint64_t nzero, hipStream_t s);
+                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, hipStream_t s);
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
                                const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t vcap, uint64_t bound, hipStream_t s);
+                               uint64_t vcap, uint64_t bound, uint32_t gcap, hipStream_t s);
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
                                  uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, const lcrc_tscan_dev* st,
@@ -208,6 +208,7 @@ struct lcrc_ctx {
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
   void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
   uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
+  uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (LCRC_TS_GRID: tests reach the tile loops with it)
   int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan (LCRC_TS_BLOCKS_DIV, measurement)
   bool wal_fused = false;  // WAL scan: header walk inside the window pass (LCRC_WAL_FUSED=1; measured slower, DESIGN)
 };
@@ -367,6 +368,7 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   ctx->x4096 = lcrc::x8n(4096, poly);
   if (const char* g = getenv("LCRC_GENERAL")) ctx->general = !strcmp(g, "ranges") ? 1 : !strcmp(g, "blocks") ? 2 : 0;
   if (const char* g = getenv("LCRC_TS_BLOCKS_DIV")) ctx->ts_blocks_div = std::max(1, atoi(g));
+  if (const char* g = getenv("LCRC_TS_GRID")) ctx->ts_grid = (uint32_t)std::max(1, atoi(g));
   if (const char* g = getenv("LCRC_WAL_FUSED")) ctx->wal_fused = strcmp(g, "1") == 0;
   *out = ctx;
   return LCRC_OK;
@@ -1370,10 +1372,10 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   // checksums come with the batch) with the index block's restart segments: entry counts, scanned per tile
   const uint64_t vcap = ts_verify_cap(cap, file_len);
   HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
-                              ctx->tbl_mm.p, vcap / 32 + 1, st));
+                              ctx->ts_grid, ctx->tbl_mm.p, vcap / 32 + 1, st));
   // the handles and the verify descriptors
   HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_count.p, ctx->sn_part.p, blk, ctx->tbl_descs.p, cap, vcap, cap,
-                             st));
+                             ctx->ts_grid, st));
   // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
   const uint64_t* ntot = &S->n_total;
   const uint64_t* nver = &S->n_verify;

@@ -3350,19 +3350,20 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
 
 // ---- asynchronous table scan (lcrc_table_scan_async) ----
 // grid: a bound on the restart segments (the workgroups past the device count only zero their share)
+// gcap: the most workgroups (the rest of the tiles grid-stride)
 hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                 lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
-                                uint64_t bound, uint32_t* zero, uint64_t nzero, hipStream_t s) {
+                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
-  LCRC_LAUNCH(lcrc_dev::k_ts_index, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, *key, cap,
+  LCRC_LAUNCH(lcrc_dev::k_ts_index, dim3((unsigned)(g < gcap ? g : gcap)), dim3(256), 0, s, file, file_len, *key, cap,
               st, local_c, local_f, part, zero, nzero);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
                                const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t vcap, uint64_t bound, hipStream_t s) {
+                               uint64_t vcap, uint64_t bound, uint32_t gcap, hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
-  LCRC_LAUNCH(lcrc_dev::k_ts_emit, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, file, file_len, st,
+  LCRC_LAUNCH(lcrc_dev::k_ts_emit, dim3((unsigned)(g < gcap ? g : gcap)), dim3(256), 0, s, file, file_len, st,
               local_c, part, out, descs, cap, vcap);
   return hipGetLastError();
 }

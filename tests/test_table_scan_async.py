@@ -248,3 +248,40 @@ def test_async_long_meta_blocks(lcrc, orc, mode, masked):
         assert err == "block checksum mismatch"
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [1, 3])
+def test_async_tile_loops(lcrc, orc, grid, monkeypatch):
+    """k_ts_index / k_ts_emit with fewer workgroups than 256-segment tiles (LCRC_TS_GRID caps their grid): a
+    workgroup scans several tiles and emit adds the totals of every tile before each one."""
+    monkeypatch.setenv("LCRC_TS_GRID", str(grid))
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    try:
+        f, blocks = orc.table_build(_kvs(6000, 41), block_size=256, compression=1, index_restart_interval=1,
+                                    filter_name=FILTER, filter_block=b"z" * 100)
+        assert len(blocks) > 256 * grid + 256  # more tiles than workgroups
+        assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks) + 4) == OK
+        g = bytearray(f)
+        d = [b for b in blocks if b[2] == 0]
+        for off, n, _ in (d[300], d[-2]):  # a data block in a later tile, and one near the end
+            g[off + n // 2] ^= 0x10
+        assert _expect_async(lcrc, eng, orc, bytes(g), FILTER, cap=len(blocks) + 4) == OK
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_async_multi_chunk_frames(lcrc, orc, engines):
+    """Blocks whose Snappy frame holds several chunks: each decoded chunk lands 16-aligned with its stored masked
+    CRC-32C after it, compared by the CRC pass; a chunk corrupted in the middle of a frame (block checksum
+    recomputed) fails only its block."""
+    f, blocks = orc.table_build(_kvs(3000, 59, vlen=400), block_size=200_000, compression=1)
+    comp = [b for b in blocks if b[2] == 0 and f[b[0] + b[1]] == 1]
+    assert len(comp) >= 3 and all(b[1] > 65536 for b in comp[:3])  # several chunks per frame
+    assert _expect_async(lcrc, engines[lcrc.MODE_REF], orc, f) == OK
+    g = bytearray(f)
+    off, n, _ = comp[1]
+    g[off + n // 2] ^= 0x21  # inside a middle chunk's bytes
+    g[off + n + 1:off + n + 5] = orc.crc(bytes(g[off:off + n + 1]), 0).to_bytes(4, "little")
+    assert _expect_async(lcrc, engines[lcrc.MODE_REF], orc, bytes(g)) == OK
