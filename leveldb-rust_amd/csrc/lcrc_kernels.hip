@@ -3171,7 +3171,10 @@ __global__ void __launch_bounds__(256) k_ts_close(lcrc_tscan_dev* __restrict__ s
                                                   const uint64_t* __restrict__ choff, const uint64_t* __restrict__ nch,
                                                   const uint32_t* __restrict__ cmm, uint64_t* __restrict__ n_out,
                                                   uint32_t* __restrict__ status_out) {
-  const uint64_t n = st->n_total;
+  // the block count k_ts_emit set, from fields ts_final leaves alone (it may shrink n_total, and workgroups of this
+  // launch may start after workgroup 0 is done); not OK / index-only: only thread 0's three blocks matter
+  const bool live = st->status == TS_OK && !st->idx_only;
+  const uint64_t n = live ? st->n_data + (st->has_filter ? 3 : 2) : 0;
   const bool bits = st->gate == 0;
   auto content = [&](uint64_t j) {
     bool bad = fstatus[j] != 0;
@@ -3184,7 +3187,8 @@ __global__ void __launch_bounds__(256) k_ts_close(lcrc_tscan_dev* __restrict__ s
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < tail) content(i);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    for (uint64_t j = tail; j < n; ++j) content(j);
+    const uint64_t n0 = st->n_total;  // = n when live
+    for (uint64_t j = n0 > 3 ? n0 - 3 : 0; j < n0; ++j) content(j);
     ts_final(st, blk, n_out, status_out);
   }
 }
