@@ -210,6 +210,8 @@ struct lcrc_ctx {
   uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
   uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (LCRC_TS_GRID: tests reach the tile loops with it)
   int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan (LCRC_TS_BLOCKS_DIV, measurement)
+  uint32_t batch_grid_b = 0;  // lcrc_batch's k_blocks grid (LCRC_BATCH_GRID_B, measurement; 0: 2 per CU)
+  uint32_t wal_grid_b = 0;    // the WAL scan's k_blocks grid (LCRC_WAL_GRID_B, measurement; 0: every resident workgroup)
   bool wal_fused = false;  // WAL scan: header walk inside the window pass (LCRC_WAL_FUSED=1; measured slower, DESIGN)
 };
 
@@ -368,6 +370,8 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   ctx->x4096 = lcrc::x8n(4096, poly);
   if (const char* g = getenv("LCRC_GENERAL")) ctx->general = !strcmp(g, "ranges") ? 1 : !strcmp(g, "blocks") ? 2 : 0;
   if (const char* g = getenv("LCRC_TS_BLOCKS_DIV")) ctx->ts_blocks_div = std::max(1, atoi(g));
+  if (const char* g = getenv("LCRC_BATCH_GRID_B")) ctx->batch_grid_b = (uint32_t)std::max(0, atoi(g));
+  if (const char* g = getenv("LCRC_WAL_GRID_B")) ctx->wal_grid_b = (uint32_t)std::max(0, atoi(g));
   if (const char* g = getenv("LCRC_TS_GRID")) ctx->ts_grid = (uint32_t)std::max(1, atoi(g));
   if (const char* g = getenv("LCRC_WAL_FUSED")) ctx->wal_fused = strcmp(g, "1") == 0;
   *out = ctx;
@@ -523,7 +527,8 @@ int lcrc_batch(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc
                                st));
     win = ctx->win.p;
   }
-  HIPCHK(lcrc_launch_blocks(false, std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU), base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
+  const uint32_t gb = ctx->batch_grid_b ? ctx->batch_grid_b : std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU);
+  HIPCHK(lcrc_launch_blocks(false, gb, base, base_len, (const lcrc_desc_dev*)descs, n, 0, 0, nullptr, win,
                             ctx->d_tab, ctx->init, ctx->xorout, kflags, out_crc,
                             out_mismatch, nullptr, nullptr, st));
   return LCRC_OK;
@@ -953,7 +958,8 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   } else if (max_recs) {
     HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
                                st));
-    HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_WAL_GRID_DIV, file, file_len, ctx->wal_descs.p, max_recs, 0, 0, nullptr,
+    HIPCHK(lcrc_launch_blocks(false, ctx->wal_grid_b ? ctx->wal_grid_b : ctx->grid_b / LCRC_WAL_GRID_DIV, file, file_len,
+                              ctx->wal_descs.p, max_recs, 0, 0, nullptr,
                               ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr, n_total,
                               (lcrc_wal_rec_dev*)recs, st));
   }
