@@ -10,7 +10,7 @@ for r in $(seq 1 $N); do
     name=${v%%=*}; path=${v#*=}
     if [ "$name" = prod ]; then unset LCRC_LIB_PATH; else export LCRC_LIB_PATH=$path; fi
     for c in $CONFIGS; do
-      timeout -k 10 120 python -u bench.py --no-cpu-baseline --config $c --steps 20 --warmup 5 > $O/${c}_${name}_$r.json 2>> $O/err.log || exit 1
+      timeout -k 10 120 python -u bench.py --no-cpu-baseline --config $c --steps 20 --warmup 5 $BENCH_ARGS > $O/${c}_${name}_$r.json 2>> $O/err.log || exit 1
     done
   done
 done
