@@ -978,3 +978,59 @@ def test_wal_fused_headers_straddling_regions(lcrc, orc, monkeypatch):
         assert set(range(16372, 16390)) <= starts
     finally:
         eng.close()
+
+
+# ---- round 3: the range pass's per-row loop far past its usual ~3 iterations ---------------------------------
+@pytest.mark.parametrize("grid", [1, 7])
+def test_range_pass_small_grid(lcrc, orc, synth, grid, monkeypatch):
+    """k_blocks with a grid of 1 or 7 workgroups (LCRC_BATCH_GRID_B, a measurement knob) over a 24 MiB slice of
+    BASELINE configs[2]'s zipf SSTable layout (~4,100 blocks): each 16-lane row walks 130 or 18 ranges in turn, so
+    the descriptor prefetch, the mismatch-bit set/clear of words shared across iterations and the last range's
+    clear of the bits past n all run far beyond the bench's ~3 iterations per row. Every CRC and mismatch bit
+    equals the oracle's, both modes (format.rs:162-171)."""
+    monkeypatch.setenv("LCRC_BATCH_GRID_B", str(grid))
+    monkeypatch.setenv("LCRC_GENERAL", "blocks")
+    sizes = synth.mixed_sizes(24 << 20, seed=synth.SEED_MIXED + 7)
+    offs, total = synth.sstable_layout(sizes)
+    lens = sizes.astype(np.uint64) + 1
+    base = synth.splitmix_bytes(synth.SEED_MIXED + 1007, total)
+    rng = np.random.default_rng(grid)
+    bad = sorted({int(i) for i in rng.choice(len(sizes) - 1, 9, replace=False)} | {len(sizes) - 1})
+    for mode, flags, algo in ((0, 0, orc.ALGO_PCLMUL_REF), (1, lcrc.FLAG_MASK, orc.ALGO_SSE42_C)):
+        want, _ = orc.crc_ranges_mt(base, offs, lens, 8, algo)
+        if mode:
+            want = orc.mask_array(want)
+        f = base.copy()
+        slot = (offs + lens).astype(np.int64)
+        for k in range(4):
+            f[slot + k] = ((want >> np.uint32(8 * k)) & 0xFF).astype(np.uint8)
+        for i in bad:
+            f[int(offs[i] + lens[i] // 2)] ^= 0x10
+        eng = lcrc.Engine(0, mode, flags)
+        crcs, mm = eng.crc_ranges(f, offs, lens, expect_rel=lens.astype(np.int64))
+        eng.close()
+        got_want, _ = orc.crc_ranges_mt(f, offs, lens, 8, algo)
+        if mode:
+            got_want = orc.mask_array(got_want)
+        assert np.array_equal(crcs, got_want), (mode, np.nonzero(crcs != got_want)[0][:10])
+        assert np.nonzero(mm)[0].tolist() == bad
+
+
+@pytest.mark.parametrize("grid", [1, 5])
+def test_wal_range_pass_small_grid(lcrc, orc, synth, grid, monkeypatch):
+    """The WAL scan's range pass with 1 or 5 workgroups (LCRC_WAL_GRID_B): a 40 MiB log's ~11,000 records, the
+    one-window records first, walked ~350 or ~70 per row, with corrupted records; every record, crc and verdict
+    against the oracle's walk (log.rs:204-279)."""
+    monkeypatch.setenv("LCRC_WAL_GRID_B", str(grid))
+    data = _wal_file(lcrc, synth, 40 << 20, 0x5EED0021 + grid)
+    rng = np.random.default_rng(0x77 + grid)
+    want = _wal_expect(orc, data)
+    for k in rng.choice(len(want), 25, replace=False):
+        h, n, _ = want[int(k)]
+        data[h + 6 + int(rng.integers(0, n + 1))] ^= 1 << int(rng.integers(0, 8))
+    for mode in MODES:
+        eng = lcrc.Engine(0, mode)
+        got = _wal_check_scan(lcrc, orc, eng, data, mode)
+        eng.close()
+        if mode == 0:
+            assert 0 < int(got["status"].sum()) <= 25
