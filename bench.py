@@ -668,10 +668,12 @@ def load_traffic(config, mode):
         return json.load(f).get("hbm_bytes_per_launch")
 
 
-def load_profile(config, mode):
-    """The newest committed rocprofv3 summary of this config (tools/profile_round.sh): the dominant
-    kernel's average duration and the roofline fraction it implies for the bytes per launch of that run."""
+def load_profile(config, mode, streams=2):
+    """The newest committed rocprofv3 summary of this config (tools/profile_round.sh) taken with the same stream
+    count (one-stream profiles carry an `s1` round tag, e.g. r03s1_*): the dominant kernel's average duration and
+    the roofline fraction it implies for the bytes per launch of that run."""
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_{mode}_summary.json")))
+    cands = [p for p in cands if os.path.basename(p).split("_")[0].endswith("s1") == (streams == 1)]
     for path in reversed(cands):
         with open(path) as f:
             s = json.load(f)
@@ -847,7 +849,7 @@ def main(argv=None):
             "timing": timing_text(w, timers, one_stream),
             "clock": ("marker" if not w.kernel_events else
                       "carried" if w.cfg.get("kernels_per_step", 1) == 1 else "start"),
-            "profile": load_profile(args.config, args.mode),
+            "profile": load_profile(args.config, args.mode, len(engs)),
         }
         if single:
             one = single
