@@ -1577,7 +1577,17 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
   if constexpr (WIN == 0) {
     while (cap - consumed >= 7) {
       uint32_t length, type;
-      wal_header(blk, consumed, length, type);
+      // bytes 4..7 at the header inside the block: ONE dword load per hop (the length and type bytes), instead of
+      // three byte loads -- beside another scan's window pass a CU's address units are shared, and every lane's
+      // hop is its own cache line (measured: WAL on two streams 3,494 vs 3,469 GiB/s, 6 alternated runs)
+      if (cap - consumed >= 8) {
+        typedef uint32_t u32_ua __attribute__((aligned(1)));
+        const uint32_t v = *(const u32_ua*)(blk + consumed + 4);
+        length = v & 0xFFFFu;
+        type = (v >> 16) & 0xFFu;
+      } else {
+        wal_header(blk, consumed, length, type);
+      }
       if (7 + length > cap - consumed) {
         stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
         break;
