@@ -43,7 +43,7 @@ hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tsca
                                uint64_t vcap, uint64_t bound, uint32_t gcap, hipStream_t s);
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
-                                 uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, const lcrc_tscan_dev* st,
+                                 uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, lcrc_tscan_dev* st,
                                  const uint32_t* gtab, uint32_t flags, hipStream_t s);
 hipError_t lcrc_launch_ts_close(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t bound, const uint8_t* fstatus,
                                const uint64_t* choff, const uint64_t* nch, const uint32_t* cmm, uint64_t* n_out,
@@ -76,7 +76,8 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
                                      uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
-                                     uint64_t ts_chunk_cap, uint32_t inline_exp, hipStream_t st);
+                                     uint64_t ts_chunk_cap, uint32_t inline_exp, const uint64_t* tparts,
+                                     const uint64_t* tnch, hipStream_t st);
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
 hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
@@ -1081,7 +1082,8 @@ static int snappy_run(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* f
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
-                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, 0, 0, 0, st));
+                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, 0, 0, 0, nullptr,
+                                   nullptr, st));
   // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
   if (ctx->general == 1) {
     static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
@@ -1374,7 +1376,7 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   const uint64_t cap = max_blocks;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
-  // Nine dependent launches. The footer, the index block header and the metaindex filter entry (optimistic:
+  // Eight dependent launches. The footer, the index block header and the metaindex filter entry (optimistic:
   // checksums come with the batch) with the index block's restart segments: entry counts, scanned per tile
   const uint64_t vcap = ts_verify_cap(cap, file_len);
   HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
@@ -1398,15 +1400,15 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     }
     // read_block_from_file's type dispatch and the Snappy framing walk (the frames' sizes scanned per workgroup,
-    // the scan finished by the add); the frames decoded (the decoded total checked against the workspace on the
+    // the scan finished inside the decode); the frames decoded (the decoded total checked against the workspace on the
     // device), each chunk followed by its stored CRC, which the CRC pass compares
     HIPCHK(lcrc_launch_ts_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ctx->sn_out_off.p,
                                  ctx->sn_choff.p, ctx->sn_part.p, ctx->sn_nch.p, ctx->sn_status.p, S, ctx->d_tab,
                                  ctx->flags, st));
-    HIPCHK(lcrc_launch_scan2_add(cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_part.p, ntot, st));
     HIPCHK(lcrc_launch_snappy_decode(file, ctx->tbl_frames.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_out.p,
                                      ctx->sn_status.p, ctx->sn_cdesc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, 8192, 8192,
-                                     ntot, S, ctx->ts_decoded_cap, ctx->ts_chunk_cap, 1, st));  // 8 KiB LDS staging each way
+                                     ntot, S, ctx->ts_decoded_cap, ctx->ts_chunk_cap, 1, ctx->sn_part.p, ctx->sn_nch.p,
+                                     st));  // 8 KiB LDS staging each way; the frame-offset scan finished inside
     HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, ctx->sn_out.p, ctx->ts_decoded_cap, ctx->sn_cdesc.p, ctx->ts_chunk_cap,
                               0, 0, nullptr, tab_c, x4096_c, lcrc::POLY_C, lcrc::CRC_INIT, lcrc::CRC_XOROUT,
                               LCRC_FLAG_MASK | LCRC_KFLAG_SETCLR, ctx->sn_ccrc.p, ctx->sn_cmm.p, &S->n_chunks, nullptr,

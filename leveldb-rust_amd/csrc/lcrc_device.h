@@ -96,7 +96,8 @@ struct lcrc_tscan_dev {
   uint32_t unsorted, gate;
   uint64_t need_out, need_chunks;  // the decoded bytes and chunks the Snappy frames need (set by the gate)
   uint32_t idx_only;  // a restart segment the device walk cannot vouch for: only the index block is verified
-  uint32_t pad;
+  uint32_t any_frame;  // k_ts_finish: some block has a Snappy frame with decoded bytes or chunks (0: the decode gate
+                       // needs no sums)
   uint64_t n_verify;  // descriptors of the batched verify: the n_total blocks and the pieces below
   // filter, metaindex, index: a block longer than LCRC_TS_PIECE is verified as pieces of that size (one row of
   // the batch kernel each, instead of one row folding thousands of windows), combined afterwards

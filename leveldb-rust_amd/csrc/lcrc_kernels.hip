@@ -2380,14 +2380,40 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
                                                            uint32_t in_lim, uint32_t out_cap,
                                                            const uint64_t* __restrict__ n_dev,
                                                            lcrc_tscan_dev* __restrict__ ts, uint64_t ts_out_cap,
-                                                           uint64_t ts_chunk_cap, uint32_t inline_exp) {
+                                                           uint64_t ts_chunk_cap, uint32_t inline_exp,
+                                                           const uint64_t* __restrict__ tparts,
+                                                           const uint64_t* __restrict__ tnch) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sn_lds[];
   if (n_dev) n = *n_dev < n ? *n_dev : n;
+  const uint32_t lane = __lane_id();
+  // tparts (table scan): out_off / chunk_off are exclusive scans WITHIN 256-frame tiles (k_ts_finish), the tile
+  // totals in tparts[2 t], tparts[2 t + 1]; a wave adds the tiles before its frame itself (no scan launch) and
+  // writes the frame's final chunk offset back for k_ts_close
+  auto tile_sum = [&](uint64_t lo, uint64_t hi, uint64_t& so, uint64_t& sc) {
+    unsigned long long xo = 0, xc = 0;
+    for (uint64_t w = lo + lane; w < hi; w += 64) {
+      xo += tparts[2 * w];
+      xc += tparts[2 * w + 1];
+    }
+    for (int d = 1; d < 64; d <<= 1) {
+      xo += __shfl_xor(xo, d, 64);
+      xc += __shfl_xor(xc, d, 64);
+    }
+    so += xo;
+    sc += xc;
+  };
   if (ts) {
     // async table scan: the decoded total and the chunk count against the workspace, decided alike by every
-    // workgroup from the scans; workgroup 0 records it (over: the host path; no chunk: nothing to decode)
+    // workgroup from the scans; workgroup 0 records it (over: the host path; no chunk: nothing to decode). A table
+    // without Snappy frames (any_frame 0) needs no sums: both are 0.
     const uint64_t m = ts->status == 0 ? n : 0;
-    const uint64_t total = m ? out_off[m] : 0, chunks = m ? chunk_off[m] : 0;
+    uint64_t total = 0, chunks = 0;
+    if (!tparts) {
+      total = m ? out_off[m] : 0;
+      chunks = m ? chunk_off[m] : 0;
+    } else if (m && ts->any_frame) {
+      tile_sum(0, (m + 255) / 256, total, chunks);
+    }
     const bool over = total > ts_out_cap || chunks > ts_chunk_cap;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       ts->need_out = total;
@@ -2400,13 +2426,19 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
   }
   uint8_t* const lin = sn_lds;
   uint8_t* const lout = sn_lds + in_lim + SN_SLACK;
-  const uint32_t lane = __lane_id();
+  uint64_t before_o = 0, before_c = 0, tiles_done = 0;  // tparts: the totals of the tiles before tiles_done
   for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
+    if (tparts && f / 256 > tiles_done) {
+      tile_sum(tiles_done, f / 256, before_o, before_c);
+      tiles_done = f / 256;
+    }
     if (status[f]) continue;
     const uint8_t* p = base + frames[f].offset;
     const uint32_t len = frames[f].length;
-    uint64_t o = out_off[f];
-    uint64_t c = chunk_off[f];
+    uint64_t o = out_off[f] + before_o;
+    uint64_t c = chunk_off[f] + before_c;
+    const uint64_t c_end = tparts ? c + tnch[f] : chunk_off[f + 1];
+    if (tparts && lane == 0) ((uint64_t*)chunk_off)[f] = c;  // k_ts_close reads the frame's chunk range
     sn_reader rd;
     rd.init(p, len, lane);
     const uint32_t end = rd.lim;
@@ -2522,7 +2554,7 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
     if (!ok && lane == 0) {
       status[f] = 1;
       // the chunk slots this frame did not fill: empty ranges that match by construction
-      for (const uint64_t ce = chunk_off[f + 1]; c < ce; ++c) {
+      for (const uint64_t ce = c_end; c < ce; ++c) {
         lcrc_desc_dev d;
         d.offset = 0;
         d.length = 0;
@@ -3050,14 +3082,16 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
 // read_block_from_file's type dispatch for every block (k_tbl_finish) and, in the same thread, the framing
 // walk of the block's Snappy frame (k_snappy_size)
 // The frames' decoded sizes (padded, see snappy_frame_size) and chunk counts are scanned within the workgroup
-// (out_off, choff) with the workgroup totals in part[2 b], part[2 b + 1]: k_scan2_add finishes the scan.
+// (out_off, choff) with the workgroup totals in part[2 b], part[2 b + 1]: k_snappy_decode_wave adds the totals of
+// the tiles before each frame itself (no scan launch between), and sums them all for its gate only when a tile
+// had frames (any_frame).
 __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
                                                    const uint32_t* __restrict__ crc,
                                                    const uint32_t* __restrict__ mismatch,
                                                    const uint8_t* __restrict__ file, lcrc_desc_dev* __restrict__ frames,
                                                    uint64_t* __restrict__ out_off, uint64_t* __restrict__ choff,
                                                    uint64_t* __restrict__ part, uint64_t* __restrict__ nchunks,
-                                                   uint8_t* __restrict__ fstatus, const lcrc_tscan_dev* __restrict__ st,
+                                                   uint8_t* __restrict__ fstatus, lcrc_tscan_dev* __restrict__ st,
                                                    const uint32_t* __restrict__ gtab, uint32_t flags) {
   __shared__ uint32_t z64k[1024];
   __shared__ uint64_t sa[4], sb[4];
@@ -3131,6 +3165,7 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
   if (threadIdx.x == 0) {
     part[2 * blockIdx.x] = to;
     part[2 * blockIdx.x + 1] = tc;
+    if (to | tc) st->any_frame = 1u;  // tiles with frames only (every writer stores the same 1: no atomic)
   }
 }
 
@@ -3383,7 +3418,7 @@ hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tsca
 }
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
-                                 uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, const lcrc_tscan_dev* st,
+                                 uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, lcrc_tscan_dev* st,
                                  const uint32_t* gtab, uint32_t flags, hipStream_t s) {
   if (n == 0) return hipSuccess;
   LCRC_LAUNCH(lcrc_dev::k_ts_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, blk, n, crc, mismatch,
@@ -3540,7 +3575,8 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
                                      const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
                                      uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
-                                     uint64_t ts_chunk_cap, uint32_t inline_exp, hipStream_t st) {
+                                     uint64_t ts_chunk_cap, uint32_t inline_exp, const uint64_t* tparts,
+                                     const uint64_t* tnch, hipStream_t st) {
   using lcrc_dev::SN_MAX;
   if (n == 0) return hipSuccess;
   const uint64_t g = n < 16384 ? n : 16384;  // one wave per frame, grid-stride
@@ -3550,7 +3586,7 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
   const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
   LCRC_LAUNCH(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
                      chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, ts, ts_out_cap,
-                     ts_chunk_cap, inline_exp);
+                     ts_chunk_cap, inline_exp, tparts, tnch);
   return hipGetLastError();
 }
 
