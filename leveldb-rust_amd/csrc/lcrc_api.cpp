@@ -73,7 +73,7 @@ hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* fra
 hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
                              uint64_t* part, const uint64_t* n_dev, hipStream_t st);
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
-                                     const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
+                                     const uint64_t* out_off, uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
                                      uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
                                      uint64_t ts_chunk_cap, uint32_t inline_exp, const uint64_t* tparts,

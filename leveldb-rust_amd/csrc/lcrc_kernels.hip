@@ -2373,7 +2373,7 @@ __device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, u
 __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __restrict__ base,
                                                            const lcrc_desc_dev* __restrict__ frames, uint64_t n,
                                                            const uint64_t* __restrict__ out_off,
-                                                           const uint64_t* __restrict__ chunk_off,
+                                                           uint64_t* __restrict__ chunk_off,  // (table scan: each frame's final offset written back)
                                                            uint8_t* __restrict__ out, uint8_t* __restrict__ status,
                                                            lcrc_desc_dev* __restrict__ cdesc,
                                                            uint32_t* __restrict__ cexp, uint32_t* __restrict__ cframe,
@@ -2438,7 +2438,7 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
     uint64_t o = out_off[f] + before_o;
     uint64_t c = chunk_off[f] + before_c;
     const uint64_t c_end = tparts ? c + tnch[f] : chunk_off[f + 1];
-    if (tparts && lane == 0) ((uint64_t*)chunk_off)[f] = c;  // k_ts_close reads the frame's chunk range
+    if (tparts && lane == 0) chunk_off[f] = c;  // k_ts_close reads the frame's chunk range
     sn_reader rd;
     rd.init(p, len, lane);
     const uint32_t end = rd.lim;
@@ -3572,7 +3572,7 @@ hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, u
 }
 
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
-                                     const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
+                                     const uint64_t* out_off, uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
                                      uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
                                      uint64_t ts_chunk_cap, uint32_t inline_exp, const uint64_t* tparts,
