@@ -29,7 +29,7 @@ themselves (fixed config, both submissions; over two streams the span runs from 
 latest end of any stream's last launch) -- the launches rocprofv3's kernel trace reports (tools/profile_round.sh
 profiles this exact command). `roofline.profile` repeats the figure from the committed rocprofv3 summary in
 profiles/ for the same config. `cpu_baseline` times the oracle's restatement of the reference's CPU CRC on
-this host's usable cores (rank 0, N=1 only) and cross-checks the device CRCs against it.
+this host's usable cores (rank 0, after the timed region, at any N) and cross-checks the device CRCs against it.
 """
 import argparse
 import glob
@@ -450,7 +450,7 @@ def workload_mixed(m, synth, engs, rank, device, args):
     cfg = {"workload": "SSTable file, block sizes 256 B-64 KiB zipf(1.1) (BASELINE configs[2])",
            "blocks": int(len(sizes)), "file_bytes": int(total), "mean_block": float(sizes.mean()), "submission": sub}
     return Workload(run, int(lens.sum()), cfg, launches, ("ranges", data, offs, lens), crcs,
-                    kernels_per_step=1 if os.environ.get("LCRC_GENERAL") == "ranges" else 2, kernel_events=q == 1)
+                    kernels_per_step=2, kernel_events=q == 1)
 
 
 def workload_wal(m, synth, engs, rank, device, args):
@@ -863,9 +863,14 @@ def main(argv=None):
                           "own start and end events; median over the launches (before the warmup)"}
     else:
         result["roofline"] = None
-    if (rank == 0 and world == 1 and not args.no_cpu_baseline and w.sample is not None
-            and args.engine == "device"):
+    # the CPU baseline (north_star: "next to the reference's own CPU CRC32C timed on the same box's host cores in the
+    # same run"): rank 0, after the timed region and the final barrier -- at N > 1 too, when every rank's device work
+    # is done and the host cores are free -- on rank 0's own sample, cross-checked against rank 0's device CRCs
+    if rank == 0 and not args.no_cpu_baseline and w.sample is not None and args.engine == "device":
         result["cpu_baseline"] = cpu_baseline(entry.load_oracle(), m, w.sample, args.mode, args.cpu_seconds, w.crcs)
+        if world > 1:
+            result["cpu_baseline"]["ranks_note"] = (f"timed on rank 0 after all {world} ranks' timed regions ended "
+                                                    "(barrier), on rank 0's sample")
     else:
         result["cpu_baseline"] = None
     if rank == 0:

@@ -131,6 +131,18 @@ typedef struct lcrc_wal_rec {
  * context per engine). Different contexts never share workspace. */
 int lcrc_device_count(int* n);
 int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags);
+/* Kernel-selection and grid overrides for tests and measurement (production callers use lcrc_ctx_create, which is
+ * lcrc_ctx_create_ex with every option at its default). Zero-initialise, set size = sizeof(lcrc_ctx_options); a
+ * field left 0 keeps the default. The library reads no environment variable. */
+typedef struct lcrc_ctx_options {
+  uint32_t size;
+  int32_t general;        /* general path: 0 auto, 1 the one-pass k_ranges, 2 window pass + range pass always */
+  uint32_t batch_grid_b;  /* lcrc_batch's range-pass workgroups (0: 2 per CU) */
+  uint32_t wal_grid_b;    /* the WAL scan's range-pass workgroups (0: every resident one) */
+  uint32_t ts_grid;       /* the table scan's index/emit workgroup cap (0: 4096) */
+  uint32_t ts_blocks_div; /* divisor of the table scan's range-pass grid (0: 1) */
+} lcrc_ctx_options;
+int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, const lcrc_ctx_options* opt);
 int lcrc_ctx_destroy(lcrc_ctx* ctx);
 /* Pre-allocate the device workspace for spans up to max_span bytes (so later calls allocate nothing
  * and can be captured in a hipGraph). */

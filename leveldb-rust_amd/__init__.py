@@ -85,6 +85,14 @@ class _WJob(ctypes.Structure):
                 ("max_recs", ctypes.c_uint64), ("n_recs", ctypes.c_void_p)]
 
 
+class _CtxOptions(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_uint32), ("general", ctypes.c_int32), ("batch_grid_b", ctypes.c_uint32),
+                ("wal_grid_b", ctypes.c_uint32), ("ts_grid", ctypes.c_uint32), ("ts_blocks_div", ctypes.c_uint32)]
+
+
+GENERAL_PATHS = {"auto": 0, "ranges": 1, "blocks": 2}
+
+
 class _Hasher(ctypes.Structure):
     _fields_ = [("state", ctypes.c_uint32), ("mode", ctypes.c_int32), ("amount", ctypes.c_uint64)]
 
@@ -95,7 +103,7 @@ _lib = None
 ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
-    "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream", "lcrc_ctx_join",
+    "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_create_ex", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream", "lcrc_ctx_join",
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_multi", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
     "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
@@ -138,6 +146,7 @@ def lib():
     sig("lcrc_hasher_finalize", u32, ctypes.POINTER(_Hasher))
     sig("lcrc_device_count", i32, ctypes.POINTER(ctypes.c_int))
     sig("lcrc_ctx_create", i32, ctypes.POINTER(vp), i32, i32, u32)
+    sig("lcrc_ctx_create_ex", i32, ctypes.POINTER(vp), i32, i32, u32, ctypes.POINTER(_CtxOptions))
     sig("lcrc_ctx_destroy", i32, vp)
     sig("lcrc_ctx_reserve", i32, vp, u64)
     sig("lcrc_ctx_stream", vp, vp)
@@ -384,12 +393,27 @@ def _ptr(x):
 
 
 class Engine:
-    """One device + one CRC mode (``lcrc_ctx``). All batched calls are GPU-only."""
+    """One device + one CRC mode (``lcrc_ctx``). All batched calls are GPU-only.
 
-    def __init__(self, device=0, mode=MODE_C, flags=0):
+    Keyword options (``lcrc_ctx_create_ex``, tests and measurement only): ``general`` ("auto" | "ranges" |
+    "blocks"), ``batch_grid_b``, ``wal_grid_b``, ``ts_grid``, ``ts_blocks_div``; unset = the library default."""
+
+    def __init__(self, device=0, mode=MODE_C, flags=0, **options):
         self.device, self.mode, self.flags = device, mode, flags
         ctx = ctypes.c_void_p()
-        _check(lib().lcrc_ctx_create(ctypes.byref(ctx), device, mode, flags), "lcrc_ctx_create")
+        if options:
+            o = _CtxOptions()
+            o.size = ctypes.sizeof(_CtxOptions)
+            for k, v in options.items():
+                if k == "general":
+                    v = GENERAL_PATHS[v] if isinstance(v, str) else int(v)
+                elif k not in ("batch_grid_b", "wal_grid_b", "ts_grid", "ts_blocks_div"):
+                    raise TypeError(f"Engine: unknown option {k!r}")
+                setattr(o, k, int(v))
+            _check(lib().lcrc_ctx_create_ex(ctypes.byref(ctx), device, mode, flags, ctypes.byref(o)),
+                   "lcrc_ctx_create_ex")
+        else:
+            _check(lib().lcrc_ctx_create(ctypes.byref(ctx), device, mode, flags), "lcrc_ctx_create")
         self.ctx = ctx.value
 
     def close(self):

@@ -23,6 +23,8 @@
 extern "C" {
 void lcrc_launch_events_begin(hipEvent_t start, hipEvent_t stop);
 void lcrc_launch_events_end(bool* started, bool* stopped);
+hipEvent_t lcrc_launch_events_swap_stop(hipEvent_t ev);
+hipError_t lcrc_launch_events_record_stop(hipEvent_t ev, hipStream_t st);
 hipError_t lcrc_launch_windows(bool final_mode, int grid, const uint8_t* base, uint64_t span, const uint32_t* gtab,
                                uint32_t* out, uint64_t nblk, uint32_t fin, uint32_t flags,
                                const uint32_t* expected, uint32_t* mismatch, hipStream_t st,
@@ -61,12 +63,6 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t m, hipStream_t st);
-hipError_t lcrc_launch_wal_windows(int grid, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
-                                   const uint32_t* gtab, uint32_t* win, uint32_t* counts, uint2* slots, uint8_t* stops,
-                                   uint64_t* local, uint64_t* part, hipStream_t st);
-hipError_t lcrc_launch_wal_emit(const uint8_t* file, uint64_t nblocks, uint32_t* counts, uint2* slots, uint8_t* stops,
-                                uint64_t* local, uint64_t* part, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
-                                uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
                                    uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
                                    hipStream_t st);
@@ -148,6 +144,7 @@ struct lcrc_ctx {
   hipEvent_t t0 = nullptr, t1 = nullptr;
   bool tk_start = false, tk_stop = false, tk_any = false;  // lcrc_timer_kernels: launches that record t0 / t1
   bool tk_end = false;  // a launch after edge 1 recorded t1
+  bool tk_armed0 = false;  // edge 0 armed since the last lcrc_timer_start: t0 is valid only once a launch recorded it
   uint32_t* d_tab = nullptr;
   uint32_t init = lcrc::CRC_INIT, xorout = lcrc::CRC_XOROUT, fin4096 = 0;
   uint32_t poly = 0, x4096 = 0;  // this mode's polynomial and x^(8*4096) mod P (k_ranges' chunk shift)
@@ -209,11 +206,12 @@ struct lcrc_ctx {
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
   void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
   uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
-  uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (LCRC_TS_GRID: tests reach the tile loops with it)
-  int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan (LCRC_TS_BLOCKS_DIV, measurement)
-  uint32_t batch_grid_b = 0;  // lcrc_batch's k_blocks grid (LCRC_BATCH_GRID_B, measurement; 0: 2 per CU)
-  uint32_t wal_grid_b = 0;    // the WAL scan's k_blocks grid (LCRC_WAL_GRID_B, measurement; 0: every resident workgroup)
-  bool wal_fused = false;  // WAL scan: header walk inside the window pass (LCRC_WAL_FUSED=1; measured slower, DESIGN)
+  uint64_t ts_out_cap = 0;  // the decode workspace: ts_decoded_cap + 32 per chunk (16-aligned chunks + stored CRCs)
+  // lcrc_ctx_options (lcrc_ctx_create_ex; tests and measurement only -- the library reads no environment variable)
+  uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (tests reach the tile loops with a small one)
+  int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan
+  uint32_t batch_grid_b = 0;  // lcrc_batch's k_blocks grid (0: 2 per CU)
+  uint32_t wal_grid_b = 0;    // the WAL scan's k_blocks grid (0: every resident workgroup)
 };
 
 namespace {
@@ -312,7 +310,12 @@ int lcrc_device_count(int* n) {
 }
 
 int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
+  return lcrc_ctx_create_ex(out, device, mode, flags, nullptr);
+}
+
+int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, const lcrc_ctx_options* opt) {
   if (!out || (mode != LCRC_MODE_REF && mode != LCRC_MODE_C)) return LCRC_EINVAL;
+  if (opt && (opt->size < sizeof(lcrc_ctx_options) || opt->general < 0 || opt->general > 2)) return LCRC_EINVAL;
   *out = nullptr;
   int ndev = 0;
   int rc = lcrc_device_count(&ndev);
@@ -369,12 +372,13 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   ctx->fin4096 = lcrc::zshift(ctx->init, 4096, poly) ^ ctx->xorout;
   ctx->poly = poly;
   ctx->x4096 = lcrc::x8n(4096, poly);
-  if (const char* g = getenv("LCRC_GENERAL")) ctx->general = !strcmp(g, "ranges") ? 1 : !strcmp(g, "blocks") ? 2 : 0;
-  if (const char* g = getenv("LCRC_TS_BLOCKS_DIV")) ctx->ts_blocks_div = std::max(1, atoi(g));
-  if (const char* g = getenv("LCRC_BATCH_GRID_B")) ctx->batch_grid_b = (uint32_t)std::max(0, atoi(g));
-  if (const char* g = getenv("LCRC_WAL_GRID_B")) ctx->wal_grid_b = (uint32_t)std::max(0, atoi(g));
-  if (const char* g = getenv("LCRC_TS_GRID")) ctx->ts_grid = (uint32_t)std::max(1, atoi(g));
-  if (const char* g = getenv("LCRC_WAL_FUSED")) ctx->wal_fused = strcmp(g, "1") == 0;
+  if (opt) {
+    ctx->general = opt->general;
+    ctx->batch_grid_b = opt->batch_grid_b;
+    ctx->wal_grid_b = opt->wal_grid_b;
+    if (opt->ts_grid) ctx->ts_grid = opt->ts_grid;
+    if (opt->ts_blocks_div) ctx->ts_blocks_div = (int)opt->ts_blocks_div;
+  }
   *out = ctx;
   return LCRC_OK;
 }
@@ -492,6 +496,17 @@ static int lanes_join(lcrc_ctx* ctx, hipStream_t st) {
   return LCRC_OK;
 }
 
+// `st` waits for both lanes; a timer stop event armed for the call (lcrc_timer_kernels edge 1) was taken from the
+// lane launches (held_stop, lcrc_launch_events_swap_stop) and is recorded here, after the join, so that it closes
+// over whichever lane ends last
+static int lanes_join_timed(lcrc_ctx* ctx, hipStream_t st, hipEvent_t held_stop) {
+  int rc = lanes_join(ctx, st);
+  lcrc_launch_events_swap_stop(held_stop);
+  if (rc) return rc;
+  if (held_stop) HIPCHK(lcrc_launch_events_record_stop(held_stop, st));
+  return LCRC_OK;
+}
+
 int lcrc_ctx_reserve(lcrc_ctx* ctx, uint64_t max_span) {
   if (!ctx) return LCRC_EINVAL;
   int rc = set_device(ctx);
@@ -570,6 +585,7 @@ int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* s
   const int grid_b = std::min(ctx->grid_b, ctx->grid_a * LCRC_BATCH_WG_PER_CU);
   HIPCHK(hipEventRecord(ctx->q_fork, st));
   for (hipStream_t l : lane) HIPCHK(hipStreamWaitEvent(l, ctx->q_fork, 0));
+  hipEvent_t held_stop = lcrc_launch_events_swap_stop(nullptr);  // recorded after the join (lanes_join_timed)
   for (size_t k = 0; k < njobs; ++k) {
     const lcrc_gjob& j = jobs[k];
     const int b = (int)(k & 1);
@@ -581,7 +597,7 @@ int lcrc_batch_queue(lcrc_ctx* ctx, const lcrc_gjob* jobs, size_t njobs, void* s
                               (ctx->flags & LCRC_FLAG_MASK) | LCRC_KFLAG_SETCLR, j.out_crc, j.out_mismatch, nullptr,
                               nullptr, lane[b]));
   }
-  return lanes_join(ctx, st);
+  return lanes_join_timed(ctx, st, held_stop);
 }
 
 int lcrc_batch_covered(lcrc_ctx* ctx, const uint8_t* base, uint64_t base_len, const lcrc_desc* descs, size_t n,
@@ -931,23 +947,7 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   uint64_t* n_total = ctx->wal_offsets.p;
   uint64_t* local = ctx->wal_offsets.p + 1;
   uint64_t* part = ctx->wal_offsets.p + 1 + nblocks;
-  // LCRC_WAL_FUSED=1: ONE streaming pass computes every 256 B window value AND walks the record headers on the data
-  // it holds (k_wal_windows + k_wal_part), then the records at their file-order positions (k_wal_emit), then one
-  // k_blocks over all records that also stores each record's crc and verdict. Measured slower than the default
-  // below (k_wal_windows 57-59 us alone vs 45 for the plain window pass: the scalar header walk lengthens every
-  // wave; and on two streams the separate header walk already hides behind the other scan's window pass), so it
-  // is opt-in; both forms pass the same parity tests.
-  if (max_recs && ctx->general != 1 && ctx->wal_fused) {
-    HIPCHK(lcrc_launch_wal_windows(ctx->grid_a, file, file_len, nblocks, ctx->d_tab, ctx->win.p, ctx->wal_counts.p,
-                                   ctx->wal_slots.p, ctx->wal_stops.p, local, part, st));
-    HIPCHK(lcrc_launch_wal_emit(file, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local, part,
-                                (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p, max_recs, n_total, n_recs, st));
-    HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / LCRC_WAL_GRID_DIV, file, file_len, ctx->wal_descs.p, max_recs, 0, 0,
-                              nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, 0, ctx->wal_crcs.p, nullptr,
-                              n_total, (lcrc_wal_rec_dev*)recs, st));
-    return LCRC_OK;
-  }
-  // The default: one stream, the header walk (k_wal_parse, one lane per 32 KiB block following the 7-byte headers,
+  // One stream: the header walk (k_wal_parse, one lane per 32 KiB block following the 7-byte headers,
   // then k_wal_emit), the window pass over the whole file, then one k_blocks over all records (the log format stores
   // the raw crc: no mask) that also stores each record's crc and verdict.
   HIPCHK(lcrc_launch_wal_parse(file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local,
@@ -1016,6 +1016,7 @@ int lcrc_wal_scan_queue(lcrc_ctx* ctx, const lcrc_wjob* jobs, size_t njobs, void
     HIPCHK(hipEventRecord(ctx->q_fork, st));
     hipStream_t lane[2] = {ctx->side, ctx->side2};
     for (hipStream_t l : lane) HIPCHK(hipStreamWaitEvent(l, ctx->q_fork, 0));
+    hipEvent_t held_stop = lcrc_launch_events_swap_stop(nullptr);  // recorded after the join (lanes_join_timed)
     for (uint32_t k = 0; k < m; ++k) {
       const lcrc_wjob& j = jobs[k0 + k];
       if (!j.max_recs) continue;
@@ -1027,7 +1028,7 @@ int lcrc_wal_scan_queue(lcrc_ctx* ctx, const lcrc_wjob* jobs, size_t njobs, void
                                 w.descs.p, j.max_recs, 0, 0, nullptr, w.win.p, ctx->d_tab, ctx->init, ctx->xorout, 0,
                                 w.crcs.p, nullptr, h[k].n_total, (lcrc_wal_rec_dev*)j.recs, l));
     }
-    if ((rc = lanes_join(ctx, st))) return rc;
+    if ((rc = lanes_join_timed(ctx, st, held_stop))) return rc;
   }
   return LCRC_OK;
 }
@@ -1340,12 +1341,15 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
       (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) || (rc = ctx->sn_status.ensure(nb)) ||
       (rc = ctx->sn_max.ensure(2)) || (rc = ctx->sn_cdesc.ensure(cc)) || (rc = ctx->sn_cexp.ensure(cc)) ||
       (rc = ctx->sn_cframe.ensure(cc)) || (rc = ctx->sn_ccrc.ensure(cc)) || (rc = ctx->sn_cmm.ensure(cc / 32 + 1)) ||
-      (rc = ctx->sn_out.ensure(decoded_cap + 16)) ||
+      (rc = ctx->sn_out.ensure(decoded_cap + 32 * cc + 16)) ||
       (rc = ctx->win.ensure(window_words(max_file_len))))
     return rc;
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   ctx->ts_decoded_cap = decoded_cap;
   ctx->ts_chunk_cap = cc;
+  // the decode lands every chunk 16-aligned with its stored CRC in the 16 B after it: up to 31 B per chunk past the
+  // decoded bytes themselves, so a caller reserving the exact decoded total still scans on the device
+  ctx->ts_out_cap = decoded_cap + 32 * cc;
   return LCRC_OK;
 }
 
@@ -1388,7 +1392,7 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   const uint64_t* ntot = &S->n_total;
   const uint64_t* nver = &S->n_verify;
   if (cap) {
-    if (ctx->general == 1) {  // LCRC_GENERAL=ranges: the one-pass kernel
+    if (ctx->general == 1) {  // options.general = 1: the one-pass kernel
       HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, file, file_len, ctx->tbl_descs.p, vcap, 0, 0, nullptr, ctx->d_tab,
                                 ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
@@ -1407,9 +1411,9 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
                                  ctx->flags, st));
     HIPCHK(lcrc_launch_snappy_decode(file, ctx->tbl_frames.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_out.p,
                                      ctx->sn_status.p, ctx->sn_cdesc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, 8192, 8192,
-                                     ntot, S, ctx->ts_decoded_cap, ctx->ts_chunk_cap, 1, ctx->sn_part.p, ctx->sn_nch.p,
+                                     ntot, S, ctx->ts_out_cap, ctx->ts_chunk_cap, 1, ctx->sn_part.p, ctx->sn_nch.p,
                                      st));  // 8 KiB LDS staging each way; the frame-offset scan finished inside
-    HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, ctx->sn_out.p, ctx->ts_decoded_cap, ctx->sn_cdesc.p, ctx->ts_chunk_cap,
+    HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, ctx->sn_out.p, ctx->ts_out_cap, ctx->sn_cdesc.p, ctx->ts_chunk_cap,
                               0, 0, nullptr, tab_c, x4096_c, lcrc::POLY_C, lcrc::CRC_INIT, lcrc::CRC_XOROUT,
                               LCRC_FLAG_MASK | LCRC_KFLAG_SETCLR, ctx->sn_ccrc.p, ctx->sn_cmm.p, &S->n_chunks, nullptr,
                               st));
@@ -1459,7 +1463,7 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
       if (!rc)
         rc = lcrc_table_scan_async(ctx, file, file_len, filter_name, (lcrc_tblk*)ctx->ts_blocks.p, cap,
                                    ctx->ts_count.p, ctx->ts_count_status, nullptr);
-      if (rc == LCRC_ENOMEM || rc == LCRC_EINVAL) {  // no device-only scan for this table: the paths below
+      if (rc == LCRC_ENOMEM) {  // no workspace for the device-only scan: the paths below (other errors propagate)
         ran = false;
         break;
       }
@@ -1717,6 +1721,7 @@ int lcrc_graph_destroy(void* graph_exec) {
 
 int lcrc_timer_start(lcrc_ctx* ctx) {
   if (!ctx) return LCRC_EINVAL;
+  ctx->tk_armed0 = false;
   HIPCHK(hipEventRecord(ctx->t0, ctx->stream));
   return LCRC_OK;
 }
@@ -1724,9 +1729,16 @@ int lcrc_timer_stop(lcrc_ctx* ctx, float* ms) {
   if (!ctx || !ms) return LCRC_EINVAL;
   if (ctx->tk_stop) {  // kernel-carried: the events are the first and last launches' own start and end
     const bool any = ctx->tk_any && ctx->tk_end;
-    ctx->tk_start = ctx->tk_stop = ctx->tk_any = ctx->tk_end = false;
+    ctx->tk_start = ctx->tk_stop = ctx->tk_any = ctx->tk_end = ctx->tk_armed0 = false;
     if (!any) return LCRC_EINVAL;
   } else {
+    // start carried by a launch (edge 0), stop recorded here: a start that no launch recorded leaves t0 stale
+    const bool stale = ctx->tk_armed0 && !ctx->tk_any;
+    ctx->tk_start = ctx->tk_any = ctx->tk_armed0 = false;
+    if (stale) {
+      g_last_error = "lcrc_timer_stop: edge 0 was armed but no launch recorded the start event";
+      return LCRC_EINVAL;
+    }
     HIPCHK(hipEventRecord(ctx->t1, ctx->stream));
   }
   HIPCHK(hipEventSynchronize(ctx->t1));
@@ -1740,10 +1752,11 @@ int lcrc_timer_stop(lcrc_ctx* ctx, float* ms) {
 int lcrc_timer_kernels(lcrc_ctx* ctx, int edge) {
   if (!ctx || edge < 0 || edge > 2) return LCRC_EINVAL;
   if (edge == 2) {  // disarm
-    ctx->tk_start = ctx->tk_stop = ctx->tk_any = ctx->tk_end = false;
+    ctx->tk_start = ctx->tk_stop = ctx->tk_any = ctx->tk_end = ctx->tk_armed0 = false;
   } else if (edge == 0) {
     ctx->tk_start = true;
     ctx->tk_any = false;
+    ctx->tk_armed0 = true;
   } else {
     ctx->tk_stop = true;
     ctx->tk_end = false;

@@ -1544,14 +1544,9 @@ __device__ __forceinline__ void wal_header(const uint8_t* __restrict__ blk, uint
 // per workgroup, so the waves spread over the CUs instead of sharing one CU's address units four apiece.
 //
 // The walk is one dependent memory round trip per record, so the block with the most records sets the
-// kernel's time. With WIN > 0 each lane stages WIN bytes of its block at the current header into its own
-// LDS window (one round trip) and follows the chain inside the window at LDS latency, refilling only when
-// the next header lies past it. Header bytes the window loads cannot return (the file's last partial
-// dword: buffer loads are range-checked per dword) come from direct byte loads.
+// kernel's time. (Staging a window of the block in LDS per lane and following the chain there measured slower
+// alone and beside a window pass)
 constexpr uint32_t WAL_PARTB = 64;  // blocks per parse workgroup (= per part total)
-#ifndef LCRC_WAL_WIN
-#define LCRC_WAL_WIN 0
-#endif
 
 // The WAL scan orders its record descriptors for k_blocks with the records whose covered bytes
 // [h + 6, h + 7 + len) lie in one 256 B window of the file first (about half of the reference's random-read
@@ -1561,93 +1556,43 @@ __device__ __forceinline__ uint32_t wal_single(uint64_t b, uint32_t at, uint32_t
   return (s >> 8) == ((s + length) >> 8) ? 1u : 0u;  // last covered byte s + length
 }
 
-template <uint32_t WIN>
 __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file, uint64_t file_len,
                                                uint64_t nblocks, uint32_t* __restrict__ counts,
                                                uint2* __restrict__ slots, uint8_t* __restrict__ stops,
                                                uint64_t* __restrict__ local, uint64_t* __restrict__ part,
                                                uint32_t bx) {
-  __shared__ u32x4 wwin[WIN ? 64 * (WIN / 16) : 1];
   const uint64_t b = (uint64_t)bx * 64 + threadIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint8_t* blk = file + b * 32768ull;
   const uint64_t rem = b < nblocks ? file_len - b * 32768ull : 0;
   const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
   uint32_t consumed = 0, nrec = 0, nsingle = 0, stop = LCRC_WAL_STOP_TRAILER_DEV;
-  if constexpr (WIN == 0) {
-    while (cap - consumed >= 7) {
-      uint32_t length, type;
-      // bytes 4..7 at the header inside the block: ONE dword load per hop (the length and type bytes), instead of
-      // three byte loads -- beside another scan's window pass a CU's address units are shared, and every lane's
-      // hop is its own cache line (measured: WAL on two streams 3,494 vs 3,469 GiB/s, 6 alternated runs)
-      if (cap - consumed >= 8) {
-        typedef uint32_t u32_ua __attribute__((aligned(1)));
-        const uint32_t v = *(const u32_ua*)(blk + consumed + 4);
-        length = v & 0xFFFFu;
-        type = (v >> 16) & 0xFFu;
-      } else {
-        wal_header(blk, consumed, length, type);
-      }
-      if (7 + length > cap - consumed) {
-        stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
-        break;
-      }
-      if (type == 0 && length == 0) {
-        stop = LCRC_WAL_STOP_ZERO_DEV;
-        break;
-      }
-      const uint32_t one = wal_single(b, consumed, length);
-      if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | (one << 8));
-      ++nrec;
-      nsingle += one;
-      consumed += 7 + length;
+  while (cap - consumed >= 7) {
+    uint32_t length, type;
+    // bytes 4..7 at the header inside the block: ONE dword load per hop (the length and type bytes), instead of
+    // three byte loads -- beside another scan's window pass a CU's address units are shared, and every lane's
+    // hop is its own cache line (measured: WAL on two streams 3,494 vs 3,469 GiB/s, 6 alternated runs)
+    if (cap - consumed >= 8) {
+      typedef uint32_t u32_ua __attribute__((aligned(1)));
+      const uint32_t v = *(const u32_ua*)(blk + consumed + 4);
+      length = v & 0xFFFFu;
+      type = (v >> 16) & 0xFFu;
+    } else {
+      wal_header(blk, consumed, length, type);
     }
-  } else {
-    // the wave's 64 blocks (2 MiB) through one wave-uniform buffer descriptor
-    const uint64_t wbase = (b - lane) * 32768ull;
-    const uint64_t wrem = wbase < file_len ? file_len - wbase : 0;
-    const uint32_t wn = wrem < (64ull << 15) ? (uint32_t)wrem : (64u << 15);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(file + wbase), (short)0, (int)wn,
-                                                                        0x00020000);
-    const uint32_t rel = lane << 15, safe = wn & ~3u;
-    u32x4* mine = wwin + lane * (WIN / 16);
-    const uint8_t* wb = (const uint8_t*)mine;
-    bool more = cap >= 7;
-    while (more) {
-      const uint32_t wlo = consumed & ~15u;
-#pragma unroll
-      for (uint32_t k = 0; k < WIN / 16; ++k)
-        mine[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, rel + wlo + 16 * k, 0, 0);
-      do {
-        uint32_t length, type;
-        if (rel + consumed + 7 <= safe) {
-          const uint32_t at = consumed - wlo;
-          length = wb[at + 4] | ((uint32_t)wb[at + 5] << 8);
-          type = wb[at + 6];
-        } else {
-          wal_header(blk, consumed, length, type);
-        }
-        if (7 + length > cap - consumed) {
-          stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
-          more = false;
-          break;
-        }
-        if (type == 0 && length == 0) {
-          stop = LCRC_WAL_STOP_ZERO_DEV;
-          more = false;
-          break;
-        }
-        const uint32_t one = wal_single(b, consumed, length);
-        if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | (one << 8));
-        ++nrec;
-        nsingle += one;
-        consumed += 7 + length;
-        if (cap - consumed < 7) {
-          more = false;
-          break;
-        }
-      } while (consumed + 7 <= wlo + WIN);
+    if (7 + length > cap - consumed) {
+      stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
+      break;
     }
+    if (type == 0 && length == 0) {
+      stop = LCRC_WAL_STOP_ZERO_DEV;
+      break;
+    }
+    const uint32_t one = wal_single(b, consumed, length);
+    if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | (one << 8));
+    ++nrec;
+    nsingle += one;
+    consumed += 7 + length;
   }
   // wave exclusive scan by shuffles of (records | one-window records << 32)
   const uint64_t mine = (uint64_t)nrec | ((uint64_t)nsingle << 32);
@@ -1665,12 +1610,11 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
   if (lane == 63) part[bx] = inc;
 }
 
-template <uint32_t WIN>
 __global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
                                                   uint64_t nblocks, uint32_t* __restrict__ counts,
                                                   uint2* __restrict__ slots, uint8_t* __restrict__ stops,
                                                   uint64_t* __restrict__ local, uint64_t* __restrict__ part) {
-  wal_parse_body<WIN>(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x);
+  wal_parse_body(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x);
 }
 
 // several logs in one launch (lcrc_wal_scan_queue): log blockIdx.y, its parse workgroups blockIdx.x
@@ -1693,11 +1637,10 @@ struct WalJobsArg {
   WalJobDev j[MAX_WJOBS];
 };
 
-template <uint32_t WIN>
 __global__ void __launch_bounds__(64) k_wal_parse_q(const WalJobsArg jobs) {
   const WalJobDev& J = jobs.j[blockIdx.y];
   if ((uint64_t)blockIdx.x * WAL_PARTB >= J.nblocks) return;  // past this log's blocks (workgroup-uniform)
-  wal_parse_body<WIN>(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
+  wal_parse_body(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
 }
 
 // record o (file order) and its verify descriptor at position pos of k_blocks' order. The descriptor's
@@ -1817,220 +1760,6 @@ __global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
   wal_emit_body(J.file, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, J.recs, J.descs, J.max_recs, J.n_total,
                 J.n_out, blockIdx.x);
 }
-
-// ---------------------------------------------------------------------------------------------------
-// k_wal_windows: the WAL scan's window pass and its header walk in ONE streaming pass. Every byte of the log is
-// loaded once for the window values anyway, so the header walk of LogReader::read_physical_record
-// (src/db/log.rs:204-279) runs on the region data already in registers instead of as a chain of dependent memory
-// round trips (k_wal_parse: ~20 us alone, ~50 us beside another scan's window pass). A wave takes a whole 32 KiB log
-// block at a time -- its two 16 KiB regions one after the other, so the chain carries from the first into the
-// second -- and walks, per region, the headers that lie in it: a header byte at a (wave-uniform) offset sits in a
-// known lane and register of the pre-transpose LX half-tiles, read by M0-relative register indexing and v_readlane
-// (a few scalar instructions per byte, no memory access). Three half-tile buffers rotate so that both halves of the
-// region are resident when the walk starts while the next half-tile's loads stay in flight (the walk of the
-// second-to-last loaded half refills one buffer, the last one the other). Outputs exactly k_wal_parse's per-block
-// record slots, counts and stop reasons; k_wal_part then forms k_wal_emit's per-part offsets.
-// ---------------------------------------------------------------------------------------------------
-struct WalWalk {
-  uint32_t consumed, nrec, nsingle, stop, saved;
-  bool done;
-  uint32_t sx, sy;  // the block's first WAL_SLOTS record slots, slot i in lane i (stored once, at the block's end)
-};
-
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
-}
-
-// The aligned dword at region offset o (wave-uniform, o % 4 == 0) of a region held in two pre-transpose LX
-// half-tiles (A: bytes [0, 128) of every 256 B window, B: [128, 256)): lane k + 8 c2 + 16 c0 + 32 c1, register
-// 4 j + dword, j = pi(window >> 3). Each half-tile is read as one 32-register vector at the uniform index (M0-relative:
-// s_set_gpr_idx_on + v_mov), then v_readlane. (The compiler cannot tell which register such a read touches: its
-// caller waits for A and B explicitly before it, see wal_phase.)
-__device__ __forceinline__ uint32_t lx_dword(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t o) {
-  const uint32_t w = o >> 8, x = o & 255u, c = (x >> 4) & 7u;
-  const uint32_t lane = (w & 7u) | (((c >> 2) & 1u) << 3) | ((c & 1u) << 4) | (((c >> 1) & 1u) << 5);
-  const uint32_t J = w >> 3;
-  const uint32_t j = ((J & 1u) << 2) | (J & 2u) | ((J >> 2) & 1u);
-  const uint32_t R = 4u * j + ((x >> 2) & 3u);
-  typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
-  u32x32 fa, fb;
-#pragma unroll
-  for (int k = 0; k < 32; ++k) fa[k] = A[k >> 2][k & 3];
-#pragma unroll
-  for (int k = 0; k < 32; ++k) fb[k] = B[k >> 2][k & 3];
-  const uint32_t va = fa[R], vb = fb[R];
-  const uint32_t v = (x & 128u) ? vb : va;
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
-}
-
-// region h (0: block bytes [0, 16 KiB), 1: [16 KiB, 32 KiB)) of log block b's header walk, exactly as k_wal_parse
-// (log.rs:229-258): the headers whose 7 bytes lie below this region's end (region 1 reads a header straddling the
-// two from the last dword of region 0, kept in W.saved). cap: the block's bytes.
-__device__ __forceinline__ void wal_walk_region(const u32x4 (&A)[8], const u32x4 (&B)[8], uint32_t h, uint64_t b,
-                                                uint32_t cap, WalWalk& W, uint32_t lane) {
-  const uint32_t lo = 16384u * h;
-  const uint32_t hi = (h == 0 && cap > 16384u) ? 16384u : cap;
-  while (!W.done && W.consumed + 7 <= hi) {  // (implies cap - consumed >= 7)
-    const uint32_t p = W.consumed;
-    // header bytes 4..6 from the dwords at q0 and q0 + 4 (block offsets; below lo: the saved dword of region 0)
-    const uint32_t q0 = (p + 4) & ~3u, sh = (p + 4) & 3u;
-    const uint32_t d0 = q0 < lo ? W.saved : lx_dword(A, B, q0 - lo);
-    const uint32_t d1 = sh <= 1 ? 0u : lx_dword(A, B, q0 + 4 - lo);  // (q0 + 4 >= lo: q0 >= lo - 4)
-    const uint64_t hb = (((uint64_t)d1 << 32) | d0) >> (8 * sh);
-    const uint32_t length = (uint32_t)hb & 0xFFFFu, type = (uint32_t)(hb >> 16) & 0xFFu;
-    if (7 + length > cap - p) {
-      W.stop = LCRC_WAL_STOP_BAD_LENGTH_DEV;
-      W.done = true;
-      break;
-    }
-    if (type == 0 && length == 0) {
-      W.stop = LCRC_WAL_STOP_ZERO_DEV;
-      W.done = true;
-      break;
-    }
-    const uint32_t one = wal_single(b, p, length);
-    // slot nrec kept in lane nrec (a select): no memory store inside the walk -- a store there made the compiler
-    // drain every load in flight before the loop
-    const bool mine = lane == W.nrec;
-    W.sx = mine ? (p | (length << 16)) : W.sx;
-    W.sy = mine ? (type | (one << 8)) : W.sy;
-    ++W.nrec;
-    W.nsingle += one;
-    W.consumed = p + 7 + length;
-  }
-  if (h == 0 && cap > 16384u) W.saved = lx_dword(A, B, 16380u);  // for a header straddling the two regions
-}
-
-struct WalSched {  // a wave's position: block cur (region h of it), the next block (ticket taken at h == 0)
-  uint64_t cur, next;
-  uint32_t h;
-};
-
-// One region of the fused pass. A, B: both half-tiles of region r_i = 2 cur + h (loaded one region earlier); C, D:
-// free. Once A and B are in, the next region's two half-tiles are issued into C, D (they have this region's header
-// walk and walk to arrive), the headers are walked on A, B, then A and B are walked (no refills). The next region's
-// call takes (C, D, A, B). Returns true when the wave has no block left.
-__device__ __forceinline__ bool wal_phase(u32x4 (&A)[8], u32x4 (&B)[8], u32x4 (&C)[8], u32x4 (&D)[8],
-                                          const uint8_t* __restrict__ file, uint64_t file_len, uint64_t nblocks,
-                                          uint64_t nreg, const void* L, const Rot& R, WalSched& S, WalWalk& W,
-                                          uint32_t* wg_ticket, uint32_t* __restrict__ win, uint32_t* __restrict__ counts,
-                                          uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                          uint64_t* __restrict__ packed, uint32_t lane, uint32_t voff_a, uint32_t voff_b) {
-  // the schedule is wave-uniform; say so (left to itself the compiler kept it in VGPRs and wrapped every load of
-  // the pass in a waterfall loop over its buffer descriptor)
-  S.cur = uniform64(S.cur);
-  S.next = uniform64(S.next);
-  S.h = __builtin_amdgcn_readfirstlane(S.h);
-  if (S.cur == NO_REGION) return true;
-  if (S.h == 0) {
-    uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(wg_ticket, 1u);
-    v = __builtin_amdgcn_readfirstlane(v);
-    const uint64_t nb = blockIdx.x + (uint64_t)v * gridDim.x;
-    S.next = nb < nblocks ? nb : NO_REGION;
-    W.consumed = W.nrec = W.nsingle = W.saved = 0;
-    W.stop = LCRC_WAL_STOP_TRAILER_DEV;
-    W.done = false;
-  }
-  const uint64_t t = 2 * S.cur + S.h;
-  // r_{i+1} = (cur, 1) or (next, 0)
-  const uint64_t b1 = S.h == 0 ? S.cur : S.next;
-  const uint64_t t1 = b1 == NO_REGION ? nreg : 2 * b1 + (S.h ^ 1u);
-  const __amdgpu_buffer_rsrc_t rs1 = region_rsrc(file, file_len, t1, nreg);
-  const uint64_t rem = file_len - S.cur * 32768ull;
-  const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
-  // A and B are all this wave has in flight: wait for them HERE, explicitly -- the compiler then knows they are in
-  // registers and inserts no wait of its own before the header walk's M0-relative reads (it cannot tell which
-  // register those touch, and would otherwise drain the next region's loads too) -- then issue the next region,
-  // which stays in flight during the header walk and the two half walks
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __builtin_amdgcn_sched_barrier(0);
-  load_half<KW_LAY>(C, rs1, voff_a);
-  __builtin_amdgcn_sched_barrier(0);
-  load_half<KW_LAY>(D, rs1, voff_b);
-  __builtin_amdgcn_sched_barrier(0);
-  if (t < nreg) wal_walk_region(A, B, S.h, S.cur, cap, W, lane);
-  __builtin_amdgcn_sched_barrier(0);
-  const uint32_t x = walk_half<false, KW_LAY, false>(L, R, A, 0u, rs1, voff_a);
-  __builtin_amdgcn_sched_barrier(0);
-  const uint32_t p = walk_half<false, KW_LAY>(L, R, B, x, rs1, voff_b);
-  if (t < nreg) win[t * 64 + window_of_lane<KW_LAY>(lane)] = p;
-  if (S.h == 1) {
-    if (lane < W.nrec && lane < WAL_SLOTS) slots[S.cur * WAL_SLOTS + lane] = make_uint2(W.sx, W.sy);
-    if (lane == 0) {
-      counts[S.cur] = W.nrec;
-      stops[S.cur] = (uint8_t)W.stop;
-      packed[S.cur] = (uint64_t)W.nrec | ((uint64_t)W.nsingle << 32);
-    }
-    S.cur = S.next;
-    S.h = 0;
-  } else {
-    S.h = 1;
-  }
-  return false;
-}
-
-__global__ void __launch_bounds__(A_THREADS) k_wal_windows(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                          uint64_t nblocks, const uint32_t* __restrict__ gtab,
-                                                          uint32_t* __restrict__ win, uint32_t* __restrict__ counts,
-                                                          uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                                          uint64_t* __restrict__ packed) {
-  __shared__ __attribute__((aligned(16))) uint32_t L[A_ZT / 4];  // the slice sets only (no block tree)
-  __shared__ uint32_t wg_ticket;
-  const uint32_t lane = __lane_id();
-  const uint32_t tid = threadIdx.x;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t nreg = (file_len + REGION - 1) / REGION;
-  const uint32_t voff_a = lane_voff<KW_LAY>(lane, 0), voff_b = lane_voff<KW_LAY>(lane, 1);
-  // log blocks dealt round-robin over the workgroups; a wave's first one static, then tickets
-  WalSched S;
-  {
-    const uint64_t b0 = blockIdx.x + (uint64_t)wv * gridDim.x;
-    S.cur = b0 < nblocks ? b0 : NO_REGION;
-    S.next = NO_REGION;
-    S.h = 0;
-  }
-  u32x4 X[8], Y[8], Z[8], Q[8];
-  {
-    const __amdgpu_buffer_rsrc_t r0 = region_rsrc(file, file_len, S.cur == NO_REGION ? nreg : 2 * S.cur, nreg);
-    __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_LAY>(X, r0, voff_a);
-    __builtin_amdgcn_sched_barrier(0);
-    load_half<KW_LAY>(Y, r0, voff_b);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  build_tables<false>(L, gtab, wv, lane);
-  if (tid == 0) wg_ticket = A_THREADS / 64;  // tickets 0 .. waves-1 were the static first blocks
-  lds_barrier();
-  const Rot R = make_rot(lane);
-  WalWalk W{};
-  for (;;) {
-    if (wal_phase(X, Y, Z, Q, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed,
-                  lane, voff_a, voff_b))
-      break;
-    if (wal_phase(Z, Q, X, Y, file, file_len, nblocks, nreg, L, R, S, W, &wg_ticket, win, counts, slots, stops, packed,
-                  lane, voff_a, voff_b))
-      break;
-  }
-}
-
-// k_wal_windows' per-block packed counts (records | one-window records << 32) -> k_wal_emit's inputs, as k_wal_parse
-// leaves them: the exclusive offsets inside each part of WAL_PARTB blocks (in place) and the part totals
-__global__ void __launch_bounds__(64) k_wal_part(uint64_t nblocks, uint64_t* __restrict__ local,
-                                                 uint64_t* __restrict__ part) {
-  static_assert(WAL_PARTB == 64, "one wave per part");
-  const uint64_t b = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-  const uint64_t mine = b < nblocks ? local[b] : 0;
-  uint64_t inc = mine;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t v = __shfl_up(inc, d, 64);
-    if (threadIdx.x >= (uint32_t)d) inc += v;
-  }
-  if (b < nblocks) local[b] = inc - mine;
-  if (threadIdx.x == 63) part[blockIdx.x] = inc;
-}
-
 
 // ---------------------------------------------------------------------------------------------------
 // Snappy framing (the `snap` crate's FrameEncoder / FrameDecoder used for compressed SSTable blocks,
@@ -3299,6 +3028,19 @@ void lcrc_launch_events_begin(hipEvent_t start, hipEvent_t stop) {
   lcrc_tl_ev_stop = stop;
   lcrc_tl_ev_started = lcrc_tl_ev_stopped = false;
 }
+// the stop event the launches carry, replaced by `ev` (nullptr: none); returns the previous one. A call whose
+// launches fork over several streams takes it away from them and records it after the join itself
+// (lcrc_launch_events_record_stop): the last launch issued need not be the last to end.
+hipEvent_t lcrc_launch_events_swap_stop(hipEvent_t ev) {
+  hipEvent_t old = lcrc_tl_ev_stop;
+  lcrc_tl_ev_stop = ev;
+  return old;
+}
+hipError_t lcrc_launch_events_record_stop(hipEvent_t ev, hipStream_t st) {
+  hipError_t e = hipEventRecord(ev, st);
+  if (e == hipSuccess) lcrc_tl_ev_stopped = true;
+  return e;
+}
 // clears them; *started / *stopped: whether a launch recorded the start / the stop
 void lcrc_launch_events_end(bool* started, bool* stopped) {
   *started = lcrc_tl_ev_started;
@@ -3488,38 +3230,12 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  uint64_t* n_out, hipStream_t st) {
   const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
   if (nparts)
-    LCRC_LAUNCH(lcrc_dev::k_wal_parse<LCRC_WAL_WIN>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
+    LCRC_LAUNCH(lcrc_dev::k_wal_parse, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
                        slots, stops, local, part);
   const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
   const uint64_t g = (nt + 255) / 256;
   LCRC_LAUNCH(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
                      stops, local, part, recs, descs, max_recs, n_total, n_out);
-  return hipGetLastError();
-}
-
-// the fused WAL window pass + header walk (k_wal_windows), then the per-part offsets (k_wal_part); `grid` = CUs.
-// local: k_wal_emit's per-block offsets (nblocks words), part: its per-64-block totals
-hipError_t lcrc_launch_wal_windows(int grid, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
-                                   const uint32_t* gtab, uint32_t* win, uint32_t* counts, uint2* slots, uint8_t* stops,
-                                   uint64_t* local, uint64_t* part, hipStream_t st) {
-  if (nblocks == 0) return hipSuccess;
-  const uint64_t need = (nblocks + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
-  const int g = (int)(need < (uint64_t)grid ? need : (uint64_t)grid);
-  LCRC_LAUNCH(lcrc_dev::k_wal_windows, dim3(g), dim3(lcrc_dev::A_THREADS), 0, st, file, file_len, nblocks, gtab, win,
-              counts, slots, stops, local);
-  const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
-  LCRC_LAUNCH(lcrc_dev::k_wal_part, dim3((unsigned)nparts), dim3(64), 0, st, nblocks, local, part);
-  return hipGetLastError();
-}
-
-// the record emit alone (after lcrc_launch_wal_windows)
-hipError_t lcrc_launch_wal_emit(const uint8_t* file, uint64_t nblocks, uint32_t* counts, uint2* slots, uint8_t* stops,
-                                uint64_t* local, uint64_t* part, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
-                                uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, hipStream_t st) {
-  const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
-  const uint64_t g = (nt + 255) / 256;
-  LCRC_LAUNCH(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots, stops,
-              local, part, recs, descs, max_recs, n_total, n_out);
   return hipGetLastError();
 }
 
@@ -3538,7 +3254,7 @@ hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t 
     gp = std::max<uint64_t>(gp, (j.nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB);
     ge = std::max<uint64_t>(ge, (j.nblocks * lcrc_dev::WAL_SLOTS + 255) / 256);
   }
-  LCRC_LAUNCH(lcrc_dev::k_wal_parse_q<LCRC_WAL_WIN>, dim3((unsigned)gp, m), dim3(64), 0, st, a);
+  LCRC_LAUNCH(lcrc_dev::k_wal_parse_q, dim3((unsigned)gp, m), dim3(64), 0, st, a);
   LCRC_LAUNCH(lcrc_dev::k_wal_emit_q, dim3((unsigned)ge, m), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -366,11 +366,10 @@ def test_graph_replay_general_path_and_wal(lcrc, orc):
 
 
 @pytest.mark.parametrize("path", ["ranges", "blocks"])
-def test_general_path_variants(lcrc, orc, path, monkeypatch):
-    """Both general-path kernels, forced through LCRC_GENERAL (read at context creation): k_ranges (one
+def test_general_path_variants(lcrc, orc, path):
+    """Both general-path kernels, forced through the context option `general` (lcrc_ctx_create_ex): k_ranges (one
     streaming pass in 4 KiB chunks) and k_windows + k_blocks, on random ranges (empty, 1-3 bytes, unaligned,
     multi-chunk, long), uniform layouts, and a WAL scan -- bit-exact against the oracle."""
-    monkeypatch.setenv("LCRC_GENERAL", path)
     rng = np.random.default_rng(4242)
     data = rng.integers(0, 256, 6 << 20, dtype=np.uint8)
     n = 3000
@@ -378,7 +377,7 @@ def test_general_path_variants(lcrc, orc, path, monkeypatch):
                            rng.integers(0, 70000, n - 13)]).astype(np.uint32)
     offs = np.array([int(rng.integers(0, len(data) - int(L))) for L in lens], np.uint64)
     for mode in MODES:
-        eng = lcrc.Engine(0, mode, lcrc.FLAG_MASK if mode else 0)
+        eng = lcrc.Engine(0, mode, lcrc.FLAG_MASK if mode else 0, general=path)
         crcs, _ = eng.crc_ranges(data, offs, lens)
         want = orc.crc_ranges(data.tobytes(), offs, lens, mode)
         if mode:
@@ -395,7 +394,7 @@ def test_general_path_variants(lcrc, orc, path, monkeypatch):
     recs = [rng.integers(0, 256, int(rng.integers(0, 1 << int(rng.integers(1, 16)))), dtype=np.uint8).tobytes()
             for _ in range(300)]
     log = orc.log_write(recs)
-    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    eng = lcrc.Engine(0, lcrc.MODE_REF, general=path)
     got = eng.wal_scan(lcrc.DeviceBuffer.from_host(np.frombuffer(log, np.uint8)), len(log))
     want = _wal_expect(orc, log)
     assert [(int(r["header"]), int(r["length"]), int(r["type"])) for r in got] == want
@@ -405,16 +404,15 @@ def test_general_path_variants(lcrc, orc, path, monkeypatch):
 
 
 @pytest.mark.parametrize("path", ["ranges", "blocks"])
-def test_out_of_bounds_descriptors(lcrc, orc, path, monkeypatch):
+def test_out_of_bounds_descriptors(lcrc, orc, path):
     """A range outside [0, base_len) is never read: CRC 0 and its mismatch bit set; in-bounds neighbours are
     unaffected. The in-place store of lcrc_batch_seal never writes outside the buffer either."""
-    monkeypatch.setenv("LCRC_GENERAL", path)
     data = bytes(orc.splitmix_bytes(99, 1 << 20))
     n0 = len(data)
     offs = np.array([0, 100, n0 - 10, n0, n0 + 5, 2 ** 40, 5000], np.uint64)
     lens = np.array([4096, 300, 10, 0, 1, 16, 70000], np.uint32)
     ok = (offs <= n0) & (lens.astype(np.uint64) <= n0 - np.minimum(offs, n0))
-    eng = lcrc.Engine(0, lcrc.MODE_C)
+    eng = lcrc.Engine(0, lcrc.MODE_C, general=path)
     crcs, mm = eng.crc_ranges(data, offs, lens)
     want = orc.crc_ranges(data, offs[ok], lens[ok], 1)
     assert np.array_equal(crcs[ok], want)
@@ -434,12 +432,11 @@ def test_out_of_bounds_descriptors(lcrc, orc, path, monkeypatch):
 
 
 @pytest.mark.parametrize("path", ["ranges", "blocks", "covered", "direct"])
-def test_mismatch_bitmap_not_prefilled(lcrc, orc, path, monkeypatch):
+def test_mismatch_bitmap_not_prefilled(lcrc, orc, path):
     """lcrc_batch / lcrc_batch_covered fill no bitmap before the kernel: every range sets or clears its own
     bit and the last range clears the bits past n. A bitmap full of ones comes back exact (bad ranges only,
     zero past n) and the word after it is untouched, twice in a row."""
-    if path in ("ranges", "blocks"):
-        monkeypatch.setenv("LCRC_GENERAL", path)
+    opts = {"general": path} if path in ("ranges", "blocks") else {}
     rng = np.random.default_rng(77)
     for n in (77, 64, 1):
         # ranges back to back, each followed by its 4-byte expected slot; ~70 % hold the right CRC
@@ -454,7 +451,7 @@ def test_mismatch_bitmap_not_prefilled(lcrc, orc, path, monkeypatch):
             host[int(o) + int(L):int(o) + int(L) + 4] = np.frombuffer(v.to_bytes(4, "little"), np.uint8)
         d = np.zeros(n, lcrc.DESC_DTYPE)
         d["offset"], d["length"], d["expect_rel"] = offs, lens, lens.astype(np.int64)
-        eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_DIRECT if path == "direct" else 0)
+        eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_DIRECT if path == "direct" else 0, **opts)
         base = lcrc.DeviceBuffer.from_host(host)
         dd = lcrc.DeviceBuffer.from_host(d.view(np.uint8))
         words = (n + 31) // 32
@@ -475,13 +472,12 @@ def test_mismatch_bitmap_not_prefilled(lcrc, orc, path, monkeypatch):
 
 # ---- round 2: BASELINE configs[2] at full size, the queue API, unaligned bases, large logs ------------------
 @pytest.mark.parametrize("path", ["blocks", "ranges"])
-def test_config3_mixed_sstable_full_size(lcrc, orc, synth, path, monkeypatch):
+def test_config3_mixed_sstable_full_size(lcrc, orc, synth, path):
     """BASELINE configs[2] exactly as bench.py's mixed leg builds it: synth.mixed_sizes(256 MiB) (zipf 1.1 over
     256 B-64 KiB) laid out by synth.sstable_layout, every block's trailer sealed with the oracle's CRC (REF:
     the reference's crc32fast bytes; C: masked CRC-32C), a few blocks corrupted, then ONE lcrc_batch with
     {off, n + 1, expect n + 1} (format.rs:162-171): every CRC equals the oracle's and exactly the corrupted
     blocks are flagged. Both general paths (k_windows + k_blocks, k_ranges)."""
-    monkeypatch.setenv("LCRC_GENERAL", path)
     sizes = synth.mixed_sizes(256 << 20)
     offs, total = synth.sstable_layout(sizes)
     lens = sizes.astype(np.uint64) + 1
@@ -497,7 +493,7 @@ def test_config3_mixed_sstable_full_size(lcrc, orc, synth, path, monkeypatch):
             f[slot + k] = ((want >> np.uint32(8 * k)) & 0xFF).astype(np.uint8)
         for i in bad:
             f[int(offs[i] + lens[i] // 2)] ^= 0x40
-        eng = lcrc.Engine(0, mode, flags)
+        eng = lcrc.Engine(0, mode, flags, general=path)
         crcs, mm = eng.crc_ranges(f, offs, lens, expect_rel=lens.astype(np.int64))
         eng.close()
         got_want, _ = orc.crc_ranges_mt(f, offs, lens, 8, algo)
@@ -633,16 +629,14 @@ def test_sparse_verify_in_a_large_file(lcrc, orc):
 
 
 @pytest.mark.parametrize("path", ["auto", "ranges"])
-def test_general_queue_matches_batches(lcrc, orc, path, monkeypatch):
+def test_general_queue_matches_batches(lcrc, orc, path):
     """lcrc_batch_queue: 7 independent descriptor batches (different file sizes, an empty batch, a batch of
     zero-length file, expected values with injected mismatches, out-of-bounds descriptors) in one call, the
     window pass of each batch beside the previous batch's range pass on the context's second stream: the CRCs
     and mismatch bits of 7 separate lcrc_batch calls and of the oracle; then the same queue captured in a HIP
     graph (a fork and a join) and replayed twice."""
-    if path != "auto":
-        monkeypatch.setenv("LCRC_GENERAL", path)
     rng = np.random.default_rng(0x9E)
-    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
+    eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK, general=path)
     jobs, want, keep = [], [], []
     for k, size in enumerate([3 << 20, 1 << 20, 5 << 20, 0, 2 << 20, 777_777, 4 << 20]):
         data = rng.integers(0, 256, max(size, 1), dtype=np.uint8)[:size]
@@ -929,67 +923,14 @@ def test_first_queued_call_inside_a_graph_capture(lcrc, orc):
         eng.close()
 
 
-@pytest.mark.parametrize("blocks", [8195, 4161])
-def test_wal_fused_window_pass(lcrc, orc, synth, blocks, monkeypatch):
-    """LCRC_WAL_FUSED=1: the record headers walked inside the window pass (k_wal_windows, the region data read from
-    the wave's registers) instead of by k_wal_parse -- every record, crc and verdict the same as the oracle's walk,
-    on the full-size configs[3] log and on the corrupted 4,161-block log (a header straddling the two 16 KiB regions
-    of a block is read from the saved last dword of the first)."""
-    monkeypatch.setenv("LCRC_WAL_FUSED", "1")
-    engs = {m: lcrc.Engine(0, m) for m in MODES}
-    try:
-        if blocks == 8195:
-            data = _wal_file(lcrc, synth, 256 << 20, synth.SEED_WAL)
-        else:
-            data = _wal_file(lcrc, synth, 4161 * 32768, 0x5EED0013)[:4160 * 32768 + 1000]
-            rng = np.random.default_rng(0x65)
-            want = _wal_expect(orc, data)
-            for k in rng.choice(len(want), 40, replace=False):
-                h, n, _ = want[int(k)]
-                data[h + 6 + int(rng.integers(0, n + 1))] ^= 1 << int(rng.integers(0, 8))
-            h, n, _ = want[len(want) // 3]
-            data[h + 5] ^= 0x80
-        for mode in MODES:
-            _wal_check_scan(lcrc, orc, engs[mode], data, mode)
-    finally:
-        for e in engs.values():
-            e.close()
-
-
-def test_wal_fused_headers_straddling_regions(lcrc, orc, monkeypatch):
-    """k_wal_windows walks a 32 KiB block as two 16 KiB regions: logs whose blocks put a header at every offset
-    16372..16389 around the boundary (its length and type bytes in the first region, the second, or both) parse
-    and verify exactly as the oracle's walk (log.rs:204-279)."""
-    monkeypatch.setenv("LCRC_WAL_FUSED", "1")
-    eng = lcrc.Engine(0, lcrc.MODE_REF)
-    try:
-        recs = []
-        for at in range(16372, 16390):
-            # first record fills the block up to `at` (header 7 + payload), then short records
-            recs.append(b"\xab" * (at - 7))
-            recs += [bytes([at & 0xFF]) * 5, b"", b"\x01" * 300]
-            # pad the rest of the block with one record so the next logical record starts a fresh block
-            used = at + (7 + 5) + 7 + (7 + 300)
-            recs.append(b"\x02" * (32768 - used - 7))
-        data = orc.log_write(recs)
-        got = _wal_check_scan(lcrc, orc, eng, bytearray(data), 0)
-        assert (got["status"] == 0).all()
-        starts = set(int(h) % 32768 for h in got["header"])
-        assert set(range(16372, 16390)) <= starts
-    finally:
-        eng.close()
-
-
 # ---- round 3: the range pass's per-row loop far past its usual ~3 iterations ---------------------------------
 @pytest.mark.parametrize("grid", [1, 7])
-def test_range_pass_small_grid(lcrc, orc, synth, grid, monkeypatch):
-    """k_blocks with a grid of 1 or 7 workgroups (LCRC_BATCH_GRID_B, a measurement knob) over a 24 MiB slice of
+def test_range_pass_small_grid(lcrc, orc, synth, grid):
+    """k_blocks with a grid of 1 or 7 workgroups (context option batch_grid_b, a measurement knob) over a 24 MiB slice of
     BASELINE configs[2]'s zipf SSTable layout (~4,100 blocks): each 16-lane row walks 130 or 18 ranges in turn, so
     the descriptor prefetch, the mismatch-bit set/clear of words shared across iterations and the last range's
     clear of the bits past n all run far beyond the bench's ~3 iterations per row. Every CRC and mismatch bit
     equals the oracle's, both modes (format.rs:162-171)."""
-    monkeypatch.setenv("LCRC_BATCH_GRID_B", str(grid))
-    monkeypatch.setenv("LCRC_GENERAL", "blocks")
     sizes = synth.mixed_sizes(24 << 20, seed=synth.SEED_MIXED + 7)
     offs, total = synth.sstable_layout(sizes)
     lens = sizes.astype(np.uint64) + 1
@@ -1006,7 +947,7 @@ def test_range_pass_small_grid(lcrc, orc, synth, grid, monkeypatch):
             f[slot + k] = ((want >> np.uint32(8 * k)) & 0xFF).astype(np.uint8)
         for i in bad:
             f[int(offs[i] + lens[i] // 2)] ^= 0x10
-        eng = lcrc.Engine(0, mode, flags)
+        eng = lcrc.Engine(0, mode, flags, general="blocks", batch_grid_b=grid)
         crcs, mm = eng.crc_ranges(f, offs, lens, expect_rel=lens.astype(np.int64))
         eng.close()
         got_want, _ = orc.crc_ranges_mt(f, offs, lens, 8, algo)
@@ -1017,11 +958,10 @@ def test_range_pass_small_grid(lcrc, orc, synth, grid, monkeypatch):
 
 
 @pytest.mark.parametrize("grid", [1, 5])
-def test_wal_range_pass_small_grid(lcrc, orc, synth, grid, monkeypatch):
-    """The WAL scan's range pass with 1 or 5 workgroups (LCRC_WAL_GRID_B): a 40 MiB log's ~11,000 records, the
+def test_wal_range_pass_small_grid(lcrc, orc, synth, grid):
+    """The WAL scan's range pass with 1 or 5 workgroups (context option wal_grid_b): a 40 MiB log's ~11,000 records, the
     one-window records first, walked ~350 or ~70 per row, with corrupted records; every record, crc and verdict
     against the oracle's walk (log.rs:204-279)."""
-    monkeypatch.setenv("LCRC_WAL_GRID_B", str(grid))
     data = _wal_file(lcrc, synth, 40 << 20, 0x5EED0021 + grid)
     rng = np.random.default_rng(0x77 + grid)
     want = _wal_expect(orc, data)
@@ -1029,7 +969,7 @@ def test_wal_range_pass_small_grid(lcrc, orc, synth, grid, monkeypatch):
         h, n, _ = want[int(k)]
         data[h + 6 + int(rng.integers(0, n + 1))] ^= 1 << int(rng.integers(0, 8))
     for mode in MODES:
-        eng = lcrc.Engine(0, mode)
+        eng = lcrc.Engine(0, mode, wal_grid_b=grid)
         got = _wal_check_scan(lcrc, orc, eng, data, mode)
         eng.close()
         if mode == 0:

@@ -13,20 +13,23 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NBLK = 4096
 
 
-def test_bench_two_device_ranks(orc, synth):
+# 4,096 blocks: the launcher; 65,536: BASELINE configs[4]'s per-GPU batch (64K x 4 KiB, 4 rotated 256 MiB buffers per
+# rank) -- the size the driver's N-GPU run allocates and streams in every rank -- with rank 0's CPU baseline after the
+# timed region, cross-checked against its device CRCs
+@pytest.mark.parametrize("NBLK", [4096, 65536])
+def test_bench_two_device_ranks(orc, synth, NBLK):
     world = 2
     env = dict(os.environ, LCRC_RANK_DEVICE_MOD="1", OMP_NUM_THREADS="1")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--blocks", str(NBLK),
-           "--steps", "3", "--warmup", "1"]
+           "--steps", "5" if NBLK == 65536 else "3", "--warmup", "2" if NBLK == 65536 else "1", "--cpu-seconds", "0.5"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     rows = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(rows) == 1, r.stdout  # ONE line, from rank 0 only
     res = json.loads(rows[0])
-    print(json.dumps({k: res[k] for k in ("value", "n_gpus", "ms_per_step", "per_gpu")}))
+    print(json.dumps({k: res[k] for k in ("value", "n_gpus", "ms_per_step", "per_gpu", "cpu_baseline")}))
     assert res["n_gpus"] == world and res["scaling"] == "weak"
     assert [g["rank"] for g in res["per_gpu"]] == list(range(world))
     assert [g["device"] for g in res["per_gpu"]] == [0] * world  # rank r on device r % 1
@@ -38,5 +41,8 @@ def test_bench_two_device_ranks(orc, synth):
         assert g["crc_xor"] == f"{int(np.bitwise_xor.reduce(want)):08x}"
         assert g["launch_us"] > 0 and 0 < g["frac"] < 1.2  # each rank's own launch-carried HIP events
     assert len({g["crc_xor"] for g in res["per_gpu"]}) == world
+    cb = res["cpu_baseline"]
+    assert cb is not None and cb["matches_device"] is True and cb["cores"] >= 1 and cb["value"] > 0
+    assert cb["kind"] == "port" and "cpu_model" in cb
     # the aggregate is all ranks' bytes over the slowest rank's time
     assert abs(res["value"] - world * NBLK * 4096 / (res["ms_per_step"] / 1e3) / 2 ** 30) <= 0.01 * res["value"] + 0.02

@@ -73,6 +73,26 @@ def test_async_clean(lcrc, orc, engines, compression, filt, block_size):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("block_size", [256, 4096])
+def test_async_exact_decoded_reservation(lcrc, orc, block_size):
+    """lcrc_table_scan_reserve's decoded_cap is the Snappy frames' decoded bytes (lcrc.h): a caller reserving
+    exactly the oracle's decoded total of a compressed table (small blocks: the per-chunk alignment and stored CRCs
+    the device adds are a large fraction of it) gets the device scan (LCRC_TSCAN_OK), not LCRC_TSCAN_HOST."""
+    f, blocks = orc.table_build(_kvs(3000, 23 + block_size), block_size=block_size, compression=1,
+                                filter_name=FILTER, filter_block=b"f" * 80)
+    decoded = 0
+    for off, n, kind in blocks:
+        if f[off + n] == 1:  # a Snappy-framed block (format.rs:194-206)
+            decoded += len(orc.snappy_frame_decode(f[off:off + n]))
+    assert decoded > 0
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    try:
+        assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks) + 4, decoded=decoded) == OK
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_async_masked_c(lcrc, orc):
     eng = lcrc.Engine(0, lcrc.MODE_C, lcrc.FLAG_MASK)
     try:
@@ -252,11 +272,10 @@ def test_async_long_meta_blocks(lcrc, orc, mode, masked):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("grid", [1, 3])
-def test_async_tile_loops(lcrc, orc, grid, monkeypatch):
-    """k_ts_index / k_ts_emit with fewer workgroups than 256-segment tiles (LCRC_TS_GRID caps their grid): a
-    workgroup scans several tiles and emit adds the totals of every tile before each one."""
-    monkeypatch.setenv("LCRC_TS_GRID", str(grid))
-    eng = lcrc.Engine(0, lcrc.MODE_REF)
+def test_async_tile_loops(lcrc, orc, grid):
+    """k_ts_index / k_ts_emit with fewer workgroups than 256-segment tiles (the context option ts_grid caps their
+    grid): a workgroup scans several tiles and emit adds the totals of every tile before each one."""
+    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_grid=grid)
     try:
         f, blocks = orc.table_build(_kvs(6000, 41), block_size=256, compression=1, index_restart_interval=1,
                                     filter_name=FILTER, filter_block=b"z" * 100)

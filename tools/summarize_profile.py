@@ -1,5 +1,7 @@
 """Summarize a tools/profile_round.sh output directory into profiles/ (committed evidence).
 
+Usage: summarize_profile.py OUTDIR ROUND CONFIG MODE [COMMITTED_LINE_JSON]
+
 Writes:
   profiles/<round>_<config>_<mode>_kernel_stats.csv   (rocprofv3 --stats table, verbatim)
   profiles/<round>_<config>_<mode>_summary.json       (per-kernel avg duration, HBM bytes per launch)
@@ -33,7 +35,7 @@ def counters(d, name):
     return per
 
 
-def main(outdir, rnd, config, mode):
+def main(outdir, rnd, config, mode, committed=None):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     tag = f"{rnd}_{config}_{mode}"
@@ -117,11 +119,26 @@ def main(outdir, rnd, config, mode):
                     summary["trace_gap_us"] = round(span - summary["avg_us"], 3)
                     summary["frac_from_trace"] = round(bpl / (span * 1e3) / 8000.0, 4)
                     summary["kernels_per_step"] = kps or 1
-                    summary["agreement"] = round(summary["frac_from_trace"] / line["roofline"]["frac"], 4)
+                    # against the profiled run's own line (the same process the trace comes from)
+                    summary["agreement_profiled_run"] = round(summary["frac_from_trace"] / line["roofline"]["frac"], 4)
+            # against the COMMITTED line: the un-profiled bench run of the same command that DESIGN.md quotes
+            # (tools/gpu_round.sh runs it right after the profile and re-summarizes with it)
+            if committed and os.path.exists(committed) and "trace_launch_us" in summary:
+                with open(committed) as f:
+                    cl = json.load(f)
+                cr = cl.get("roofline") or {}
+                summary["committed_line"] = {"file": os.path.relpath(committed, ROOT), "value": cl["value"],
+                                             "ms_per_step": cl["ms_per_step"], "launch_us": cr.get("launch_us"),
+                                             "frac": cr.get("frac")}
+                if cr.get("launch_us"):
+                    summary["agreement"] = round(cr["launch_us"] / summary["trace_launch_us"], 4)
+                summary["agreement_wall"] = round(cl["ms_per_step"] * 1e3 / summary["trace_launch_us"], 4)
             summary["note"] = ("frac: the dominant kernel's average duration alone (rocprofv3 kernel trace); "
                                "frac_from_trace: the bench line's measure (its timed launches, first to last, per "
-                               "launch) on the same trace -- the difference is the dispatch "
-                               "gap between two in-order launches; agreement = frac_from_trace / line frac")
+                               "launch) on the same trace -- the difference is the dispatch gap between two in-order "
+                               "launches. agreement = the committed line's GPU time per launch / the trace's "
+                               "(1.0: the trace reproduces the committed line); agreement_wall = its wall time per step / "
+                               "the trace's; agreement_profiled_run = frac_from_trace / the profiled run's own line frac")
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     # the dominant kernel's traffic for bench.py
@@ -148,4 +165,4 @@ def main(outdir, rnd, config, mode):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
