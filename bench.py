@@ -70,6 +70,9 @@ def parse(argv=None):
     p.add_argument("--table-sync", action="store_true",
                    help="table config: time the synchronous lcrc_table_scan (results to pinned host memory)")
     p.add_argument("--mode", choices=["c", "ref"], default="c")
+    p.add_argument("--compression", type=int, choices=[0, 1], default=0,
+                   help="table config: 1 = a Snappy-compressed table (the reference's default, option.rs:127) written "
+                        "by the TableBuilder restatement from db_bench-style values; 0 = raw blocks")
     p.add_argument("--queue", type=int, default=None,
                    help="fixed config: 1 (default): one lcrc_batch_uniform launch per step; Q > 1: steps per "
                         "lcrc_batch_uniform_queue submission (<= 32 per launch, launches balanced); 0: all timed "
@@ -526,17 +529,30 @@ def workload_table(m, synth, engs, rank, device, args):
     """Whole-table verify scan of a 64K x 4 KiB-block SSTable: footer, index parse on
     the device, one device verify of every trailer. The trailers are sealed once by the device writer path."""
     nblk, blen = 65536, 4096
-    f, blocks = synth.table_layout(nblk, blen, seed=synth.SEED_TABLE + rank)
-    dev = m.DeviceBuffer.from_host(f, device)
-    d = np.zeros(len(blocks), m.DESC_DTYPE)
-    d["offset"] = [b[0] for b in blocks]
-    d["length"] = [b[1] + 1 for b in blocks]
-    d["expect_rel"] = [b[1] + 1 for b in blocks]
-    dd = m.DeviceBuffer.from_host(d.view(np.uint8), device)
-    seal = m.Engine(device, m.MODE_REF)  # the reference's trailers: crc32fast, unmasked
-    seal.batch_seal(dev, len(f), dd, len(blocks))
-    seal.sync()
-    seal.close()
+    decoded = 0
+    if args.compression:
+        # every compressible data block a Snappy frame (write_block keeps it: < raw - raw/8, table.rs:489), trailers
+        # sealed on the host by the writer (crc32fast over the stored bytes, table.rs:519-522)
+        f, tb = synth.compressed_table(m, nblk)
+        blocks = [(int(b["offset"]), int(b["size"])) for b in tb]
+        dev = m.DeviceBuffer.from_host(f, device)
+        for b in tb:
+            if b["kind"] == m.TBLK_DATA and f[int(b["offset"] + b["size"])] == 1:
+                decoded += 1
+        kinds = np.asarray(tb["kind"])
+        framed = f[(tb["offset"] + tb["size"]).astype(np.int64)] == 1
+    else:
+        f, blocks = synth.table_layout(nblk, blen, seed=synth.SEED_TABLE + rank)
+        dev = m.DeviceBuffer.from_host(f, device)
+        d = np.zeros(len(blocks), m.DESC_DTYPE)
+        d["offset"] = [b[0] for b in blocks]
+        d["length"] = [b[1] + 1 for b in blocks]
+        d["expect_rel"] = [b[1] + 1 for b in blocks]
+        dd = m.DeviceBuffer.from_host(d.view(np.uint8), device)
+        seal = m.Engine(device, m.MODE_REF)  # the reference's trailers: crc32fast, unmasked
+        seal.batch_seal(dev, len(f), dd, len(blocks))
+        seal.sync()
+        seal.close()
     # two copies of the table, alternated per step (2 x 269 MB > the 256 MiB Infinity Cache)
     devs = [dev, m.DeviceBuffer.from_host(dev.download(np.uint8, len(f)), device)]
     # the synchronous form's results land in pinned host memory (lcrc_host_alloc_pinned), as a caller that scans
@@ -557,8 +573,13 @@ def workload_table(m, synth, engs, rank, device, args):
     cap = len(blocks) + 8
     res = [(m.DeviceBuffer(cap * m.TBLK_DTYPE.itemsize, device), m.DeviceBuffer(8, device), m.DeviceBuffer(8, device))
            for _ in scanners]
+    dec_bytes = 0
+    if args.compression:  # the decoded bytes of every frame (the decode workspace the scan reserves)
+        for (off, size), fr in zip(blocks, framed):
+            if fr:
+                dec_bytes += len(m.snappy_frame_decode(f[off:off + size]))
     for e in scanners:
-        e.table_scan_reserve(len(f), cap)
+        e.table_scan_reserve(len(f), cap, dec_bytes)
     # the async form (lcrc_table_scan_async) must agree with the synchronous one before it is timed
     scanners[0].table_scan_async(dev, len(f), res[0][0], cap, res[0][1], res[0][2])
     scanners[0].sync()
@@ -588,7 +609,12 @@ def workload_table(m, synth, engs, rank, device, args):
                 scanners[k].table_scan_async(devs[i % 2], len(f), res[k][0], cap, res[k][1], res[k][2])
 
     run.keep = (pinned, scanners, res, devs)  # (a graph holds raw pointers: the files must outlive it)
-    cfg = {"workload": "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)",
+    cfg = {"workload": ("whole-table verify scan: ~64K Snappy-compressed data blocks (4 KiB raw, db_bench values) + "
+                        "index: block crc32fast trailers, frames decoded, every chunk's masked CRC-32C"
+                        if args.compression else
+                        "whole-table verify scan: 64K x 4 KiB data blocks + index (crc32fast trailers)"),
+           "compression": args.compression, "decoded_bytes": int(dec_bytes), "snappy_frames": int(decoded),
+           "bytes_counted": "sum(stored block + type byte): the block checksums' bytes",
            "blocks": len(blocks), "file_bytes": int(len(f)), "crc": "crc-32/iso-hdlc (crc32fast), the reference's trailers",
            "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else
            "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async"}
@@ -836,6 +862,7 @@ def main(argv=None):
         "pct_hbm_peak": round(100.0 * (w.nbytes * args.steps * world / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
         "per_gpu": per_gpu,
     }
+    prof_config = args.config + ("z" if args.compression else "")  # profiles/ tag (tablez: the compressed table)
     if timers and gpu_ms:
         one_stream = len(timers) == 1 and not w.per_step_sync
         launch_s = gpu_ms / 1e3 / cov_launches
@@ -843,13 +870,13 @@ def main(argv=None):
         achieved = bytes_per_launch / launch_s / 1e9
         result["roofline"] = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(args.config, args.mode),
+            "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(prof_config, args.mode),
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
             "timing": timing_text(w, timers, one_stream),
             "clock": ("marker" if not w.kernel_events else
                       "carried" if w.cfg.get("kernels_per_step", 1) == 1 else "start"),
-            "profile": load_profile(args.config, args.mode, len(engs)),
+            "profile": load_profile(prof_config, args.mode, len(engs)),
         }
         if single:
             one = single

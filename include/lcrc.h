@@ -327,6 +327,8 @@ void* lcrc_tb_create(uint32_t block_size, int restart_interval, uint8_t compress
                      int host_seal);
 void lcrc_tb_destroy(void* tb);
 int lcrc_tb_add(void* tb, const uint8_t* key, size_t klen, const uint8_t* val, size_t vlen); /* keys ascending */
+/* n entries at once: keys[i * klen], vals[i * vlen] (fixed sizes, keys ascending) */
+int lcrc_tb_add_many(void* tb, const uint8_t* keys, size_t klen, const uint8_t* vals, size_t vlen, size_t n);
 void lcrc_tb_flush(void* tb);                                                                 /* end a data block */
 int lcrc_tb_finish(void* tb, const char* filter_name, const uint8_t* filter, size_t filter_len);
 size_t lcrc_tb_size(void* tb);

@@ -107,7 +107,7 @@ ABI_SYMBOLS = [
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_multi", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
     "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
-    "lcrc_tb_create", "lcrc_tb_destroy", "lcrc_tb_add", "lcrc_tb_flush", "lcrc_tb_finish", "lcrc_tb_size",
+    "lcrc_tb_create", "lcrc_tb_destroy", "lcrc_tb_add", "lcrc_tb_add_many", "lcrc_tb_flush", "lcrc_tb_finish", "lcrc_tb_size",
     "lcrc_tb_data", "lcrc_tb_blocks", "lcrc_tb_seal_descs",
     "lcrc_dev_alloc", "lcrc_dev_free", "lcrc_host_alloc_pinned", "lcrc_host_free_pinned", "lcrc_memcpy_h2d",
     "lcrc_memcpy_d2h", "lcrc_memset_d", "lcrc_device_sync", "lcrc_timer_start", "lcrc_timer_kernels", "lcrc_timer_stop",
@@ -214,6 +214,7 @@ def lib():
     sig("lcrc_tb_create", vp, u32, i32, ctypes.c_uint8, i32, u32, i32)
     sig("lcrc_tb_destroy", None, vp)
     sig("lcrc_tb_add", i32, vp, vp, sz, vp, sz)
+    sig("lcrc_tb_add_many", i32, vp, vp, sz, vp, sz, sz)
     sig("lcrc_tb_flush", None, vp)
     sig("lcrc_tb_finish", i32, vp, cp, vp, sz)
     sig("lcrc_tb_size", sz, vp)
@@ -874,6 +875,15 @@ class TableBuilder:
         kp, kn, _k1 = _buf(key)
         vp, vn, _k2 = _buf(value)
         _check(lib().lcrc_tb_add(self._t, kp, kn, vp, vn), "TableBuilder.add (keys must increase)")
+
+    def add_many(self, keys, values):
+        """keys: (n, klen) u8 array, values: (n, vlen) u8 array -- n entries in one call (keys ascending)."""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        values = np.ascontiguousarray(values, np.uint8)
+        assert keys.ndim == 2 and values.ndim == 2 and len(keys) == len(values)
+        _check(lib().lcrc_tb_add_many(self._t, keys.ctypes.data_as(ctypes.c_void_p), keys.shape[1],
+                                      values.ctypes.data_as(ctypes.c_void_p), values.shape[1], len(keys)),
+               "TableBuilder.add_many (keys must increase)")
 
     def flush(self):
         lib().lcrc_tb_flush(self._t)

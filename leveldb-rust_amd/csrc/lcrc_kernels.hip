@@ -2099,7 +2099,11 @@ __device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, u
   return w0 == ulen;
 }
 
-__global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __restrict__ base,
+// One wave per frame. Table scan (tparts): one workgroup of SN_TS_WAVES waves per 256-frame tile of k_ts_finish -- the
+// workgroup sums the tile totals once (the gate's grand totals and the base of its own tile: O(tiles) loads per
+// workgroup, not per wave), then its waves take the tile's frames in turn. Otherwise one-wave workgroups, grid-stride.
+constexpr uint32_t SN_TS_WAVES = 8;
+__global__ void __launch_bounds__(64 * SN_TS_WAVES) k_snappy_decode_wave(const uint8_t* __restrict__ base,
                                                            const lcrc_desc_dev* __restrict__ frames, uint64_t n,
                                                            const uint64_t* __restrict__ out_off,
                                                            uint64_t* __restrict__ chunk_off,  // (table scan: each frame's final offset written back)
@@ -2115,9 +2119,10 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
   extern __shared__ __attribute__((aligned(16))) uint8_t sn_lds[];
   if (n_dev) n = *n_dev < n ? *n_dev : n;
   const uint32_t lane = __lane_id();
+  const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   // tparts (table scan): out_off / chunk_off are exclusive scans WITHIN 256-frame tiles (k_ts_finish), the tile
-  // totals in tparts[2 t], tparts[2 t + 1]; a wave adds the tiles before its frame itself (no scan launch) and
-  // writes the frame's final chunk offset back for k_ts_close
+  // totals in tparts[2 t], tparts[2 t + 1]; the workgroup of tile t adds the tiles before it and writes each frame's
+  // final chunk offset back for k_ts_close
   auto tile_sum = [&](uint64_t lo, uint64_t hi, uint64_t& so, uint64_t& sc) {
     unsigned long long xo = 0, xc = 0;
     for (uint64_t w = lo + lane; w < hi; w += 64) {
@@ -2131,17 +2136,22 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
     so += xo;
     sc += xc;
   };
+  uint64_t before_o = 0, before_c = 0;  // tparts: the totals of the tiles before this workgroup's tile
   if (ts) {
     // async table scan: the decoded total and the chunk count against the workspace, decided alike by every
-    // workgroup from the scans; workgroup 0 records it (over: the host path; no chunk: nothing to decode). A table
-    // without Snappy frames (any_frame 0) needs no sums: both are 0.
+    // workgroup; workgroup 0 records it (over: the host path; no chunk: nothing to decode). A table without Snappy
+    // frames (any_frame 0) needs no sums: both are 0.
     const uint64_t m = ts->status == 0 ? n : 0;
     uint64_t total = 0, chunks = 0;
     if (!tparts) {
       total = m ? out_off[m] : 0;
       chunks = m ? chunk_off[m] : 0;
     } else if (m && ts->any_frame) {
-      tile_sum(0, (m + 255) / 256, total, chunks);
+      const uint64_t tiles = (m + 255) / 256, mine = blockIdx.x < tiles ? blockIdx.x : tiles;
+      tile_sum(0, mine, before_o, before_c);
+      total = before_o;
+      chunks = before_c;
+      tile_sum(mine, tiles, total, chunks);
     }
     const bool over = total > ts_out_cap || chunks > ts_chunk_cap;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2153,14 +2163,12 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
     }
     if (over || chunks == 0) return;
   }
-  uint8_t* const lin = sn_lds;
-  uint8_t* const lout = sn_lds + in_lim + SN_SLACK;
-  uint64_t before_o = 0, before_c = 0, tiles_done = 0;  // tparts: the totals of the tiles before tiles_done
-  for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
-    if (tparts && f / 256 > tiles_done) {
-      tile_sum(tiles_done, f / 256, before_o, before_c);
-      tiles_done = f / 256;
-    }
+  uint8_t* const lin = sn_lds + (size_t)wv * (in_lim + SN_SLACK + out_cap);
+  uint8_t* const lout = lin + in_lim + SN_SLACK;
+  const uint64_t f0 = tparts ? (uint64_t)blockIdx.x * 256 + wv : (uint64_t)blockIdx.x * nwv + wv;
+  const uint64_t fstep = tparts ? nwv : (uint64_t)gridDim.x * nwv;
+  const uint64_t fend = tparts ? ((uint64_t)blockIdx.x * 256 + 256 < n ? (uint64_t)blockIdx.x * 256 + 256 : n) : n;
+  for (uint64_t f = f0; f < fend; f += fstep) {
     if (status[f]) continue;
     const uint8_t* p = base + frames[f].offset;
     const uint32_t len = frames[f].length;
@@ -3295,12 +3303,21 @@ hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* f
                                      const uint64_t* tnch, hipStream_t st) {
   using lcrc_dev::SN_MAX;
   if (n == 0) return hipSuccess;
-  const uint64_t g = n < 16384 ? n : 16384;  // one wave per frame, grid-stride
+  // table scan (tparts): one workgroup of SN_TS_WAVES waves per 256-frame tile; otherwise one wave per workgroup,
+  // grid-stride
+  const uint32_t waves = tparts ? lcrc_dev::SN_TS_WAVES : 1;
+  const uint64_t g = tparts ? (n + 255) / 256 : (n < 16384 ? n : 16384);
   // LDS sized to the batch's largest chunk (bigger ones take the lane-serial path): small staging, many waves
   const uint32_t in_lim = max_in + 4 < SN_MAX ? (max_in + 4 + 15) & ~15u : SN_MAX;
   const uint32_t out_cap = max_out < SN_MAX ? (max_out + 15) & ~15u : SN_MAX;
-  const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
-  LCRC_LAUNCH(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
+  const size_t lds = ((size_t)in_lim + lcrc_dev::SN_SLACK + out_cap) * waves;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {  // more than the default dynamic LDS: raise the kernel's limit (once per process)
+    static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_snappy_decode_wave,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+  }
+  LCRC_LAUNCH(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64 * waves), lds, st, base, frames, n, out_off,
                      chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, ts, ts_out_cap,
                      ts_chunk_cap, inline_exp, tparts, tnch);
   return hipGetLastError();

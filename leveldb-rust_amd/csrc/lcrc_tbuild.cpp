@@ -324,6 +324,14 @@ void lcrc_tb_destroy(void* t) { delete (TableBuilder*)t; }
 int lcrc_tb_add(void* t, const uint8_t* key, size_t klen, const uint8_t* val, size_t vlen) {
   return ((TableBuilder*)t)->add(key, klen, val, vlen);
 }
+// n entries of fixed-size keys and values laid out back to back (keys[i * klen], vals[i * vlen]), in order
+int lcrc_tb_add_many(void* t, const uint8_t* keys, size_t klen, const uint8_t* vals, size_t vlen, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    const int rc = ((TableBuilder*)t)->add(keys + i * klen, klen, vals + i * vlen, vlen);
+    if (rc) return rc;
+  }
+  return 0;
+}
 void lcrc_tb_flush(void* t) { ((TableBuilder*)t)->flush(); }
 int lcrc_tb_finish(void* t, const char* filter_name, const uint8_t* filter, size_t filter_len) {
   return ((TableBuilder*)t)->finish(filter_name, filter, filter_len);

@@ -150,3 +150,32 @@ def snappy_frame_synthetic(seed=SEED_SNAPPY, unit=64, reps=64):
     body = bytes(4) + bytes(z)
     frame = b"\xff\x06\x00\x00sNaPpY" + bytes([0]) + len(body).to_bytes(3, "little") + body
     return frame, raw, 14
+
+
+SEED_TEXT = 0x5EED0006
+
+
+def compressible_values(n, vlen, fraction=0.5, seed=SEED_TEXT):
+    """n values of vlen bytes as LevelDB's db_bench makes them (CompressibleString: a random printable string of
+    vlen * fraction bytes, repeated to fill vlen), so Snappy keeps about `fraction` of each."""
+    k = max(1, int(vlen * fraction))
+    rng = np.random.default_rng(seed)
+    raw = rng.integers(ord(" "), ord("~") + 1, (n, k)).astype(np.uint8)
+    reps = -(-vlen // k)
+    return np.tile(raw, (1, reps))[:, :vlen]
+
+
+def compressed_table(m, nblk, block_size=4096, vlen=100):
+    """A Snappy-compressed SSTable written by the TableBuilder restatement (table.rs:268-468, compression type 1 =
+    the reference's default, option.rs:127): keys k%015d, db_bench-style values (half compressible), about nblk data
+    blocks. Returns (file bytes as numpy u8, the builder's block list)."""
+    # entries per data block: the index-shared key prefix leaves ~vlen + 6 bytes per entry (flushed at >= block_size)
+    per = max(1, -(-block_size // (vlen + 6)))
+    n = nblk * per
+    vals = compressible_values(n, vlen)
+    tb = m.TableBuilder(block_size=block_size, compression=1, mode=m.MODE_REF, host_seal=True)
+    digits = np.arange(n, dtype=np.int64)[:, None] // (10 ** np.arange(14, -1, -1, dtype=np.int64))[None, :] % 10
+    keys = np.concatenate([np.full((n, 1), ord("k"), np.uint8), (digits + ord("0")).astype(np.uint8)], axis=1)
+    tb.add_many(keys, vals)
+    f = tb.finish()
+    return np.frombuffer(f, np.uint8), tb.blocks()

@@ -13,7 +13,8 @@ timeout -k 10 120 python -u __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
 tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_fixed.json 2> gpurun_out/bench_fixed.err || { tail -20 gpurun_out/bench_fixed.err; exit 1; }
 cat gpurun_out/bench_fixed.json
-for c in mixed wal; do
-  timeout -k 10 300 python -u bench.py --config $c > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || { tail -20 gpurun_out/bench_$c.err; exit 1; }
-  cat gpurun_out/bench_$c.json
+for c in ${CONFIGS:-mixed wal table tablez}; do
+  BC="--config $c"; [ "$c" = tablez ] && BC="--config table --compression 1"
+  timeout -k 10 300 python -u bench.py $BC > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || { tail -20 gpurun_out/bench_$c.err; exit 1; }
+  cut -c1-1500 gpurun_out/bench_$c.json
 done

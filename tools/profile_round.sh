@@ -15,7 +15,10 @@ OUT=gpurun_out/prof_${ROUND}_${CONFIG}_${MODE}
 rm -rf "$OUT"
 mkdir -p "$OUT" profiles
 # the driver's command (bench.py --gpus 1 --steps 20 --warmup 5) for this config, without the CPU leg
-BENCH="bench.py --gpus 1 --config $CONFIG --mode $MODE --steps 20 --warmup 5 --no-cpu-baseline $EXTRA"
+# tablez: the Snappy-compressed table (bench.py --config table --compression 1)
+BCONF="--config $CONFIG"
+[ "$CONFIG" = tablez ] && BCONF="--config table --compression 1"
+BENCH="bench.py --gpus 1 $BCONF --mode $MODE --steps 20 --warmup 5 --no-cpu-baseline $EXTRA"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH --extra-out "$OUT/bench.json" > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH > "$OUT/write.log" 2>&1
