@@ -53,7 +53,7 @@ QMAX = 32  # batches per queued launch (MAX_QJOBS in lcrc_kernels.hip)
 MIXED_QUEUE = 1  # mixed config: steps per lcrc_batch_queue submission (1: one lcrc_batch per step)
 WAL_QUEUE = 1  # wal config: scans per lcrc_wal_scan_queue submission (1: one lcrc_wal_scan_async per step)
 WAL_KERNELS = 4  # lcrc_wal_scan_async: header walk, record emit, window pass, range pass
-TABLE_KERNELS = 8  # lcrc_table_scan_async: index, emit, windows, blocks, finish, decode, chunk crcs, close
+TABLE_KERNELS = 6  # lcrc_table_scan_async: index, emit, windows, blocks, finish, decode + chunk checks + close
 
 
 def parse(argv=None):

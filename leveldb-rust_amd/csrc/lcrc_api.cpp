@@ -50,6 +50,10 @@ hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t*
 hipError_t lcrc_launch_ts_close(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t bound, const uint8_t* fstatus,
                                const uint64_t* choff, const uint64_t* nch, const uint32_t* cmm, uint64_t* n_out,
                                uint32_t* status_out, hipStream_t s);
+hipError_t lcrc_launch_ts_decode(const uint8_t* file, const lcrc_desc_dev* frames, const uint64_t* out_off, uint8_t* out,
+                                 const uint8_t* fstatus, lcrc_tscan_dev* st, lcrc_tblk_dev* blk, const uint32_t* tab_c,
+                                 uint64_t ts_out_cap, const uint64_t* tparts, uint64_t bound, uint64_t* n_out,
+                                 uint32_t* status_out, hipStream_t s);
 hipError_t lcrc_launch_scan2_add(uint64_t n, uint64_t* out_a, uint64_t* out_b, const uint64_t* part,
                                  const uint64_t* n_dev, hipStream_t st);
 int lcrc_blocks_per_cu();
@@ -1379,8 +1383,7 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   lcrc_tblk_dev* blk = (lcrc_tblk_dev*)blocks;
   const uint64_t cap = max_blocks;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
-  static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);
-  // Eight dependent launches. The footer, the index block header and the metaindex filter entry (optimistic:
+  // Six dependent launches. The footer, the index block header and the metaindex filter entry (optimistic:
   // checksums come with the batch) with the index block's restart segments: entry counts, scanned per tile
   const uint64_t vcap = ts_verify_cap(cap, file_len);
   HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
@@ -1389,7 +1392,6 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_count.p, ctx->sn_part.p, blk, ctx->tbl_descs.p, cap, vcap, cap,
                              ctx->ts_grid, st));
   // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
-  const uint64_t* ntot = &S->n_total;
   const uint64_t* nver = &S->n_verify;
   if (cap) {
     if (ctx->general == 1) {  // options.general = 1: the one-pass kernel
@@ -1403,24 +1405,16 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
                                 nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     }
-    // read_block_from_file's type dispatch and the Snappy framing walk (the frames' sizes scanned per workgroup,
-    // the scan finished inside the decode); the frames decoded (the decoded total checked against the workspace on the
-    // device), each chunk followed by its stored CRC, which the CRC pass compares
+    // read_block_from_file's type dispatch and the Snappy framing walk (the frames' padded decoded sizes scanned per
+    // 256-block tile)
     HIPCHK(lcrc_launch_ts_finish(blk, cap, ctx->tbl_crcs.p, ctx->tbl_mm.p, file, ctx->tbl_frames.p, ctx->sn_out_off.p,
                                  ctx->sn_choff.p, ctx->sn_part.p, ctx->sn_nch.p, ctx->sn_status.p, S, ctx->d_tab,
                                  ctx->flags, st));
-    HIPCHK(lcrc_launch_snappy_decode(file, ctx->tbl_frames.p, cap, ctx->sn_out_off.p, ctx->sn_choff.p, ctx->sn_out.p,
-                                     ctx->sn_status.p, ctx->sn_cdesc.p, ctx->sn_cexp.p, ctx->sn_cframe.p, 8192, 8192,
-                                     ntot, S, ctx->ts_out_cap, ctx->ts_chunk_cap, 1, ctx->sn_part.p, ctx->sn_nch.p,
-                                     st));  // 8 KiB LDS staging each way; the frame-offset scan finished inside
-    HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, ctx->sn_out.p, ctx->ts_out_cap, ctx->sn_cdesc.p, ctx->ts_chunk_cap,
-                              0, 0, nullptr, tab_c, x4096_c, lcrc::POLY_C, lcrc::CRC_INIT, lcrc::CRC_XOROUT,
-                              LCRC_FLAG_MASK | LCRC_KFLAG_SETCLR, ctx->sn_ccrc.p, ctx->sn_cmm.p, &S->n_chunks, nullptr,
-                              st));
   }
-  // the content verdicts and the reference's order of outcomes; the count and the status for the caller
-  HIPCHK(lcrc_launch_ts_close(S, blk, cap, ctx->sn_status.p, ctx->sn_choff.p, ctx->sn_nch.p, ctx->sn_cmm.p, n_blocks,
-                              status, st));
+  // the frames decoded and every chunk's masked CRC-32C checked in the decoding wave, the content verdicts and the
+  // reference's order of outcomes; the count and the status for the caller
+  HIPCHK(lcrc_launch_ts_decode(file, ctx->tbl_frames.p, ctx->sn_out_off.p, ctx->sn_out.p, ctx->sn_status.p, S, blk, tab_c,
+                               ctx->ts_out_cap, ctx->sn_part.p, cap, n_blocks, status, st));
   return LCRC_OK;
 }
 

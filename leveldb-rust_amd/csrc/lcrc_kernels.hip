@@ -2099,6 +2099,52 @@ __device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, u
   return w0 == ulen;
 }
 
+// One Snappy chunk's elements qp[0, qe - qp) decoded lane-serially into out[o, lim) (global memory; chunks too large
+// for the LDS staging); o advances. False when malformed or the output does not end exactly at lim.
+__device__ bool sn_serial_decode(const uint8_t* qp, const uint8_t* qe, uint8_t* __restrict__ out, uint64_t& o,
+                                 uint64_t lim) {
+  const uint64_t start = o;
+  bool ok = true;
+  while (ok && qp < qe) {
+    const uint32_t tag = *qp++;
+    uint32_t ln, off;
+    if ((tag & 3) == 0) {
+      ln = tag >> 2;
+      if (ln >= 60) {
+        const uint32_t nb = ln - 59;
+        if ((uint64_t)(qe - qp) < nb) { ok = false; break; }
+        ln = 0;
+        for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)qp[k] << (8 * k);
+        qp += nb;
+      }
+      ln += 1;
+      if ((uint64_t)(qe - qp) < ln || o + ln > lim) { ok = false; break; }
+      for (uint32_t k = 0; k < ln; ++k) out[o + k] = qp[k];
+      o += ln;
+      qp += ln;
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (qp >= qe) { ok = false; break; }
+      ln = 4 + ((tag >> 2) & 7);
+      off = ((tag >> 5) << 8) | *qp++;
+    } else if ((tag & 3) == 2) {
+      if (qe - qp < 2) { ok = false; break; }
+      ln = 1 + (tag >> 2);
+      off = qp[0] | ((uint32_t)qp[1] << 8);
+      qp += 2;
+    } else {
+      if (qe - qp < 4) { ok = false; break; }
+      ln = 1 + (tag >> 2);
+      off = qp[0] | ((uint32_t)qp[1] << 8) | ((uint32_t)qp[2] << 16) | ((uint32_t)qp[3] << 24);
+      qp += 4;
+    }
+    if (off == 0 || off > o - start || o + ln > lim) { ok = false; break; }
+    for (uint32_t k = 0; k < ln; ++k, ++o) out[o] = out[o - off];
+  }
+  return ok && o == lim;
+}
+
 // One wave per frame. Table scan (tparts): one workgroup of SN_TS_WAVES waves per 256-frame tile of k_ts_finish -- the
 // workgroup sums the tile totals once (the gate's grand totals and the base of its own tile: O(tiles) loads per
 // workgroup, not per wave), then its waves take the tile's frames in turn. Otherwise one-wave workgroups, grid-stride.
@@ -2226,47 +2272,7 @@ __global__ void __launch_bounds__(64 * SN_TS_WAVES) k_snappy_decode_wave(const u
             o += ulen;
           }
         } else if (lane == 0) {  // too large for the staging: lane-serial, from and to global memory
-          const uint8_t* qp = rd.a + q;
-          const uint8_t* qe = rd.a + at;
-          const uint64_t lim = start + ulen;
-          while (ok && qp < qe) {
-            const uint32_t tag = *qp++;
-            uint32_t ln, off;
-            if ((tag & 3) == 0) {
-              ln = tag >> 2;
-              if (ln >= 60) {
-                const uint32_t nb = ln - 59;
-                if ((uint64_t)(qe - qp) < nb) { ok = false; break; }
-                ln = 0;
-                for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)qp[k] << (8 * k);
-                qp += nb;
-              }
-              ln += 1;
-              if ((uint64_t)(qe - qp) < ln || o + ln > lim) { ok = false; break; }
-              for (uint32_t k = 0; k < ln; ++k) out[o + k] = qp[k];
-              o += ln;
-              qp += ln;
-              continue;
-            }
-            if ((tag & 3) == 1) {
-              if (qp >= qe) { ok = false; break; }
-              ln = 4 + ((tag >> 2) & 7);
-              off = ((tag >> 5) << 8) | *qp++;
-            } else if ((tag & 3) == 2) {
-              if (qe - qp < 2) { ok = false; break; }
-              ln = 1 + (tag >> 2);
-              off = qp[0] | ((uint32_t)qp[1] << 8);
-              qp += 2;
-            } else {
-              if (qe - qp < 4) { ok = false; break; }
-              ln = 1 + (tag >> 2);
-              off = qp[0] | ((uint32_t)qp[1] << 8) | ((uint32_t)qp[2] << 16) | ((uint32_t)qp[3] << 24);
-              qp += 4;
-            }
-            if (off == 0 || off > o - start || o + ln > lim) { ok = false; break; }
-            for (uint32_t k = 0; k < ln; ++k, ++o) out[o] = out[o - off];
-          }
-          if (ok && o != lim) ok = false;
+          ok = sn_serial_decode(rd.a + q, rd.a + at, out, o, start + ulen);
         }
         ok = bcast(ok ? 1u : 0u) != 0;
         o = ((uint64_t)bcast((uint32_t)(o >> 32)) << 32) | bcast((uint32_t)o);
@@ -3004,6 +3010,230 @@ __global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, u
   p[3] = (uint8_t)(c >> 24);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// k_ts_decode: the table scan's last launch -- the Snappy frames decoded, every chunk's masked CRC-32C computed in
+// the decoding wave and compared with the stored one, every block's content verdict, and the reference's order of
+// outcomes (ts_final). It replaces three launches (the decode, a CRC pass over the decoded bytes, the close) and the
+// decoded bytes' round trip through HBM: a chunk decoded in LDS is checksummed there and never written out
+// (format.rs:194-206; the snap crate's FrameDecoder checks each chunk's masked CRC-32C).
+//
+// One workgroup of TD_WAVES waves per 256-block tile of k_ts_finish (its in-tile scans of the frames' padded decoded
+// sizes give each frame's global-memory workspace for the lane-serial path; the workgroup adds the tiles before its
+// own once). The last three blocks (filter, metaindex, index: whatever ts_final may move) are the last tile's.
+//
+// Chunk CRC (td_chunk_crc): the chunk M is read as V = 0^pad || M, |V| = 1024 np (leading zeros walked from register
+// 0 stay 0, so walk(0, V) = walk(0, M)); per 1 KiB pass each lane walks 16 B (slice-by-4), the 16-lane rows join with
+// Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- a 32 KiB table copy in LDS. The init register
+// is injected into the first min(4, |M|) bytes: walk(R, M) = walk(0, M ^ LE(R)) ^ (R >> 8 |M|) for |M| < 4.
+// ---------------------------------------------------------------------------------------------------
+constexpr uint32_t TD_WAVES = 8;
+constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
+constexpr uint32_t TD_IN = 6144 + 16;   // LDS staging per wave: compressed bytes (+ 4 for the tail dword)
+constexpr uint32_t TD_OUT = 7168;       // decoded bytes (a multiple of 1 KiB: V fits as is)
+constexpr uint32_t TD_WAVE_LDS = TD_IN + SN_SLACK + TD_OUT;
+constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
+
+// the piece of pass k of lane `lane`: V[1024 k + 16 lane, +16), init injected into V[pad, pad + q)
+__device__ __forceinline__ u32x4 td_inject(u32x4 w, uint32_t x0, uint32_t pad, uint32_t q) {
+  if (x0 < pad + q && x0 + 16 > pad) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t x = x0 + 4 * d + b;
+        if (x >= pad && x < pad + q) w[d] ^= 0xFFu << (8 * b);  // CRC-32C init 0xFFFFFFFF
+      }
+  }
+  return w;
+}
+
+template <bool FROM_LDS>
+__device__ uint32_t td_chunk_crc(const uint32_t* T, const uint8_t* src, uint32_t len, uint32_t lane) {
+  const uint32_t np = (len + 1023) >> 10, pad = (np << 10) - len, q = len < 4 ? len : 4u;
+  const uint32_t g = lane & 15;
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < np; ++k) {
+    const uint32_t x0 = 1024 * k + 16 * lane;
+    u32x4 w;
+    if constexpr (FROM_LDS) {
+      w = *(const u32x4*)(src + x0);  // src = V (the chunk decoded at V + pad, V[0, pad) zeroed)
+    } else {  // src = M in global memory, any alignment
+      if (x0 >= pad) {
+        w = *(const u32x4_ua*)(src + (x0 - pad));
+      } else {
+        w = u32x4{0, 0, 0, 0};
+        if (x0 + 16 > pad)
+          for (uint32_t b = pad - x0; b < 16; ++b) w[b >> 2] |= (uint32_t)src[x0 + b - pad] << (8 * (b & 3));
+      }
+    }
+    w = td_inject(w, x0, pad, q);
+    uint32_t cv = step4(T, 0u, w.x);
+    cv = step4(T, cv, w.y);
+    cv = step4(T, cv, w.z);
+    cv = step4(T, cv, w.w);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {  // row tree: 16 pieces of 16 B -> one 256 B value in lane 0 of the row
+      const uint32_t pn = row_down(cv, m);
+      if ((g & ((2u << m) - 1)) == 0) cv = zl(T, TAB_ZPIECE + m * 1024, cv) ^ pn;
+    }
+    const uint32_t r0 = __builtin_amdgcn_readlane(cv, 0), r1 = __builtin_amdgcn_readlane(cv, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(cv, 32), r3 = __builtin_amdgcn_readlane(cv, 48);
+    const uint32_t a = zl(T, TAB_ZWIN, r0) ^ r1, b = zl(T, TAB_ZWIN, r2) ^ r3;
+    const uint32_t pass = zl(T, TAB_ZWIN + 1024, a) ^ b;
+    acc = k ? zl(T, TAB_ZWIN + 2048, acc) ^ pass : pass;
+  }
+  if (len < 4) acc ^= len ? 0xFFFFFFFFu >> (8 * len) : 0xFFFFFFFFu;
+  return __builtin_amdgcn_readfirstlane(acc ^ 0xFFFFFFFFu);  // raw CRC-32C (xorout)
+}
+
+// frame f decoded chunk by chunk, every chunk's masked CRC-32C checked: true when the frame is good (format.rs:194-206)
+__device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint32_t* T, uint8_t* lin, uint8_t* lout,
+                         uint8_t* __restrict__ out, uint64_t o, uint32_t lane) {
+  sn_reader rd;
+  rd.init(p, len, lane);
+  const uint32_t end = rd.lim;
+  bool ok = true;
+  uint32_t at = (uint32_t)(p - rd.a);
+  // the framing was validated by k_ts_finish: chunk headers and lengths are in bounds, preambles are sane
+  while (ok && at < end) {
+    rd.ensure(at, lane);
+    const uint32_t type = rd.byte(at);
+    const uint32_t cl = rd.le(at + 1, 3);
+    const uint32_t body = at + 4;
+    at = body + cl;
+    if (type > 1) continue;  // stream identifiers and skippable chunks
+    rd.ensure(body, lane);
+    const uint32_t want = rd.le(body, 4);
+    uint32_t crc;
+    if (type == 1) {  // uncompressed: checksummed where it lies
+      crc = td_chunk_crc<false>(T, rd.a + body + 4, cl - 4, lane);
+    } else {
+      uint32_t ulen = 0, q = body + 4;  // preamble = uncompressed length
+      for (uint32_t i = 0, sh = 0; i < 5 && q < at; ++i, sh += 7) {
+        const uint32_t b = rd.byte(q++);
+        ulen |= (b & 127u) << sh;
+        if (!(b & 128)) break;
+      }
+      if (ulen <= TD_OUT && at - q + 4 <= TD_IN) {
+        // decoded at V + pad of the output staging, V[0, pad) zeroed: the CRC reads whole aligned 16 B pieces
+        const uint32_t pad = ((ulen + 1023) & ~1023u) - ulen;
+        for (uint32_t k = 16 * lane; k < pad; k += 1024) *(u32x4*)(lout + k) = u32x4{0, 0, 0, 0};
+        const uint8_t* zs = rd.a + q;
+        const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
+        const uint32_t* za = (const uint32_t*)(zs - d);
+        const uint32_t ndw = (d + (at - q) + 3) >> 2;
+        for (uint32_t k = lane; k < ndw; k += 64) ((uint32_t*)lin)[k] = za[k];
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        ok = snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane);
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        crc = ok ? td_chunk_crc<true>(T, lout, ulen, lane) : 0u;
+      } else {  // too large for the staging: lane-serial into this frame's workspace, checksummed there
+        uint64_t oo = o;
+        if (lane == 0) ok = sn_serial_decode(rd.a + q, rd.a + at, out, oo, o + ulen);
+        ok = bcast(ok ? 1u : 0u) != 0;
+        __threadfence_block();
+        crc = ok ? td_chunk_crc<false>(T, out + o, ulen, lane) : 0u;
+        o += (ulen + 15) & ~15u;
+      }
+    }
+    ok = ok && mask32c(crc) == want;
+  }
+  return ok;
+}
+
+__global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __restrict__ file,
+                                                            const lcrc_desc_dev* __restrict__ frames,
+                                                            const uint64_t* __restrict__ out_off, uint8_t* __restrict__ out,
+                                                            const uint8_t* __restrict__ fstatus,
+                                                            lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
+                                                            const uint32_t* __restrict__ tab_c, uint64_t ts_out_cap,
+                                                            const uint64_t* __restrict__ tparts,
+                                                            uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t td_lds[];
+  uint32_t* const T = (uint32_t*)td_lds;
+  uint8_t* const bad = td_lds + TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // 256 tile flags + the last three
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+  // the block count from fields ts_final leaves alone (it may shrink n_total while later workgroups start)
+  const bool live = st->status == TS_OK && !st->idx_only;
+  const uint64_t n = live ? st->n_data + (st->has_filter ? 3 : 2) : 0;
+  const uint64_t tiles = (n + 255) / 256, tail = n > 3 ? n - 3 : 0, t = blockIdx.x;
+  const bool last = n && t == (n - 1) / 256;
+  if (t >= tiles && t != 0) return;  // (workgroup 0 runs ts_final when nothing is live)
+  // the gate: the decoded total and the chunk count the frames need against the workspace (decided alike by every
+  // workgroup from the tile totals; workgroup 0 records it -- over: the host path). No frames: no sums.
+  uint64_t before = 0, total = 0, chunks = 0;
+  if (n && st->any_frame) {
+    unsigned long long xb = 0, xo = 0, xc = 0;
+    for (uint64_t w = lane; w < tiles; w += 64) {
+      const uint64_t v = tparts[2 * w];
+      xo += v;
+      xc += tparts[2 * w + 1];
+      if (w < t) xb += v;
+    }
+    for (int d = 1; d < 64; d <<= 1) {
+      xo += __shfl_xor(xo, d, 64);
+      xc += __shfl_xor(xc, d, 64);
+      xb += __shfl_xor(xb, d, 64);
+    }
+    before = xb;
+    total = xo;
+    chunks = xc;
+  }
+  const bool over = total > ts_out_cap;
+  if (t == 0 && threadIdx.x == 0) {
+    st->need_out = total;
+    st->need_chunks = chunks;
+    st->gate = over ? 1u : chunks == 0 ? 2u : 0u;
+    st->n_chunks = over ? 0 : chunks;
+  }
+  const bool dec = !over && chunks;
+  for (uint32_t i = threadIdx.x; i < 256 + 16; i += blockDim.x) bad[i] = 0;
+  if (dec)
+    for (uint32_t i = threadIdx.x; i < TD_TAB_WORDS / 4; i += blockDim.x) ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i];
+  __syncthreads();
+  if (dec) {
+    uint8_t* const lin = td_lds + TD_TAB_WORDS * 4 + wv * TD_WAVE_LDS;
+    uint8_t* const lout = lin + TD_IN + SN_SLACK;
+    // this tile's frames (the last three blocks excluded), then the last workgroup's wave 0 the last three
+    const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
+    for (uint64_t f = lo + wv; f < hi; f += TD_WAVES)
+      if (frames[f].length && !fstatus[f] &&
+          !td_frame(file + frames[f].offset, frames[f].length, T, lin, lout, out, out_off[f] + before, lane) && lane == 0)
+        bad[f - lo] = 1;
+    if (last && wv == 0)
+      for (uint64_t f = tail; f < n; ++f) {
+        const uint64_t tb = (f / 256 == t) ? before : 0;  // (a frame among the last three in an earlier tile: its
+        // workspace offset is that tile's; the tiles before it are summed here)
+        uint64_t base_o = tb;
+        if (f / 256 != t) {
+          unsigned long long xb = 0;
+          for (uint64_t w = lane; w < f / 256; w += 64) xb += tparts[2 * w];
+          for (int d = 1; d < 64; d <<= 1) xb += __shfl_xor(xb, d, 64);
+          base_o = xb;
+        }
+        if (frames[f].length && !fstatus[f] &&
+            !td_frame(file + frames[f].offset, frames[f].length, T, lin, lout, out, out_off[f] + base_o, lane) &&
+            lane == 0)
+          bad[256 + (f - tail)] = 1;
+      }
+  }
+  __syncthreads();
+  // content verdicts (k_ts_finish left fstatus = 1 for a frame whose framing walk failed)
+  auto content = [&](uint64_t j, bool fb) {
+    if (fstatus[j] || fb) blk[j].status = 3;  // LCRC_TBLK_BAD_CONTENT
+    if (j > 0 && blk[j - 1].offset > blk[j].offset) st->unsorted = 1;
+  };
+  const uint64_t j = t * 256 + threadIdx.x;
+  if (threadIdx.x < 256 && j < tail) content(j, bad[threadIdx.x] != 0);
+  if (threadIdx.x == 0 && (last || (n == 0 && t == 0))) {
+    for (uint64_t k = tail; k < n; ++k) content(k, bad[256 + (k - tail)] != 0);
+    if (over && st->status == TS_OK) st->status = TS_HOST;
+    ts_final(st, blk, n_out, status_out);
+  }
+}
+
 }  // namespace lcrc_dev
 
 // ---------------------------------------------------------------------------------------------------
@@ -3181,6 +3411,20 @@ hipError_t lcrc_launch_ts_close(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t
                                uint32_t* status_out, hipStream_t s) {
   LCRC_LAUNCH(lcrc_dev::k_ts_close, dim3((unsigned)(bound / 256 + 1)), dim3(256), 0, s, st, blk, fstatus, choff, nch,
               cmm, n_out, status_out);
+  return hipGetLastError();
+}
+
+// the table scan's decode, chunk checks and close in one launch (k_ts_decode); bound: the result capacity
+hipError_t lcrc_launch_ts_decode(const uint8_t* file, const lcrc_desc_dev* frames, const uint64_t* out_off, uint8_t* out,
+                                 const uint8_t* fstatus, lcrc_tscan_dev* st, lcrc_tblk_dev* blk, const uint32_t* tab_c,
+                                 uint64_t ts_out_cap, const uint64_t* tparts, uint64_t bound, uint64_t* n_out,
+                                 uint32_t* status_out, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_decode,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::TD_LDS);
+  if (attr != hipSuccess) return attr;
+  const uint64_t g = (bound + 255) / 256;
+  LCRC_LAUNCH(lcrc_dev::k_ts_decode, dim3((unsigned)(g ? g : 1)), dim3(64 * lcrc_dev::TD_WAVES), lcrc_dev::TD_LDS, s,
+              file, frames, out_off, out, fstatus, st, blk, tab_c, ts_out_cap, tparts, n_out, status_out);
   return hipGetLastError();
 }
 
