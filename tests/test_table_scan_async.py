@@ -82,7 +82,8 @@ def test_async_exact_decoded_reservation(lcrc, orc, block_size):
                                 filter_name=FILTER, filter_block=b"f" * 80)
     decoded = 0
     for off, n, kind in blocks:
-        if f[off + n] == 1:  # a Snappy-framed block (format.rs:194-206)
+        if kind == 0 and f[off + n] == 1:  # a Snappy-framed data block (format.rs:194-206; the filter block carries
+            # type 1 over raw bytes, table.rs:383-391)
             decoded += len(orc.snappy_frame_decode(f[off:off + n]))
     assert decoded > 0
     eng = lcrc.Engine(0, lcrc.MODE_REF)

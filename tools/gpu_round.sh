@@ -10,7 +10,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 R=${1:-r03}
 shift || true
-CONFIGS=${@:-fixed mixed wal table}
+CONFIGS=${@:-fixed mixed wal table tablez}
 OUT=gpurun_out/round_$R
 mkdir -p "$OUT/profiles" profiles
 if [ -z "$SKIP_TESTS" ]; then
