@@ -47,9 +47,6 @@ hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t*
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
                                  uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, lcrc_tscan_dev* st,
                                  const uint32_t* gtab, uint32_t flags, hipStream_t s);
-hipError_t lcrc_launch_ts_close(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t bound, const uint8_t* fstatus,
-                               const uint64_t* choff, const uint64_t* nch, const uint32_t* cmm, uint64_t* n_out,
-                               uint32_t* status_out, hipStream_t s);
 hipError_t lcrc_launch_ts_decode(const uint8_t* file, const lcrc_desc_dev* frames, const uint64_t* out_off, uint8_t* out,
                                  const uint8_t* fstatus, lcrc_tscan_dev* st, lcrc_tblk_dev* blk, const uint32_t* tab_c,
                                  uint64_t ts_out_cap, const uint64_t* tparts, uint64_t bound, uint64_t* n_out,
@@ -73,11 +70,9 @@ hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* fra
 hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* out_a, uint64_t* out_b,
                              uint64_t* part, const uint64_t* n_dev, hipStream_t st);
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
-                                     const uint64_t* out_off, uint64_t* chunk_off, uint8_t* out, uint8_t* status,
+                                     const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
-                                     uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
-                                     uint64_t ts_chunk_cap, uint32_t inline_exp, const uint64_t* tparts,
-                                     const uint64_t* tnch, hipStream_t st);
+                                     uint32_t max_out, hipStream_t st);
 hipError_t lcrc_launch_snappy_check(const uint32_t* crc, const uint32_t* cexp, const uint32_t* cframe,
                                     const uint64_t* nch, uint64_t nch_bound, uint8_t* status, hipStream_t st);
 hipError_t lcrc_launch_idx_parse(bool pass2, const uint8_t* d, uint32_t len, uint32_t nres, uint64_t file_len,
@@ -1087,8 +1082,7 @@ static int snappy_run(lcrc_ctx* ctx, const uint8_t* base, const lcrc_desc_dev* f
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
   HIPCHK(lcrc_launch_snappy_decode(base, frames, n, out_off, ctx->sn_choff.p, out, status, ctx->sn_cdesc.p,
-                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], nullptr, nullptr, 0, 0, 0, nullptr,
-                                   nullptr, st));
+                                   ctx->sn_cexp.p, ctx->sn_cframe.p, mx[0], mx[1], st));
   // masked CRC-32C of every decoded chunk: the general path over the decoded bytes
   if (ctx->general == 1) {
     static const uint32_t x4096_c = lcrc::x8n(4096, lcrc::POLY_C);

@@ -17,7 +17,7 @@
 //     loads and walk, zero-padded by the buffer range check, the padding undone by one GF(2) multiply.
 //   * Snappy framing: k_snappy_size (framing walk), k_snappy_decode_wave (one wave per frame, LDS-staged,
 //     data-parallel element parse), k_snappy_check; table scan: k_idx_parse, k_tbl_finish, k_tbl_content
-//     (host-walked index), and the device-only scan k_ts_index, k_ts_emit, k_ts_finish, k_ts_close.
+//     (host-walked index), and the device-only scan k_ts_index, k_ts_emit, k_ts_finish, k_ts_decode.
 //   * k_wal_parse walks the 7-byte headers of every 32 KiB log block (src/db/log.rs:204-279) into
 //     record descriptors for k_blocks.
 #include <hip/hip_runtime.h>
@@ -2032,8 +2032,13 @@ __device__ __forceinline__ uint32_t small_mod(uint32_t x, uint32_t a) {
   return x - (uint32_t)q * a;
 }
 
-__device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, uint8_t* o, uint32_t ulen,
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ bool snappy_wave_decode(const uint8_t* in_g, uint32_t q, uint32_t qe, uint8_t* o_g, uint32_t ulen,
                                    uint32_t lane) {
+  // both staging buffers are LDS: say so, so that every access is a ds_ op (a generic pointer picked between them at
+  // run time would become a flat access waiting on the vector memory counter too)
+  const lds_u8* const in = (const lds_u8*)in_g;
+  lds_u8* const o = (lds_u8*)o_g;
   uint32_t w0 = 0;  // bytes written before this window
   for (uint32_t base = q; base < qe;) {
     const uint32_t i = base + lane;  // candidate start (reads stay inside the staging's slack)
@@ -2073,26 +2078,93 @@ __device__ bool snappy_wave_decode(const uint8_t* in, uint32_t q, uint32_t qe, u
     const uint32_t w = w0 + incl - v;
     const bool bad = sel && (!good || w > ulen || outlen > ulen - w || (typ != 0 && (a == 0 || a > w)));
     if (__builtin_amdgcn_ballot_w64(bad)) return false;
-    const uint32_t pw = (w & 0xFFFFu) | ((outlen - 1) << 16);   // w < ulen <= SN_MAX, outlen <= SN_MAX
-    const uint32_t pa = typ == 0 ? (0x80000000u | a) : a;       // valid offsets are <= w
-    // execute in order: a literal is an LDS -> LDS copy, a copy moves its <= 64 bytes in one pass
-    for (uint64_t m = mask; m; m &= m - 1) {
-      const int j = (int)__builtin_ctzll(m);
-      const uint32_t ew = (uint32_t)__builtin_amdgcn_readlane((int)pw, j);
-      const uint32_t ea = (uint32_t)__builtin_amdgcn_readlane((int)pa, j);
-      const uint32_t eo = ew & 0xFFFFu, eln = (ew >> 16) + 1;
-      if (ea & 0x80000000u) {
-        const uint32_t a = ea & 0x7FFFFFFFu;
-        for (uint32_t k = lane; k < eln; k += 64) o[eo + k] = in[a + k];
-      } else if (lane < eln) {  // the source byte of lane k is always already written
-        const uint32_t src = eo - ea + (ea >= eln ? lane : small_mod(lane, ea));
-        const uint8_t b = o[src];
-        __builtin_amdgcn_wave_barrier();
-        o[eo + lane] = b;
-      } else {
-        __builtin_amdgcn_wave_barrier();
+    // Each element's source: in[sa + f(i)] (a literal's bytes, or a copy whose whole source lies in the literal just
+    // before it -- the usual Snappy shape of repeated text -- read from that literal's input bytes instead), or
+    // o[sa + f(i)]; f(i) = i, or i mod `per` for a copy shorter-offset than it is long (it repeats its last `per` bytes).
+    const int pj = 63 - __builtin_clzll((mask & ((1ull << lane) - 1)) | 1ull);  // the previous element's lane
+    const bool has_prev = (mask & ((1ull << lane) - 1)) != 0;
+    const uint32_t pw_ = (uint32_t)__builtin_amdgcn_ds_bpermute(pj * 4, (int)w);
+    const uint32_t pl_ = (uint32_t)__builtin_amdgcn_ds_bpermute(pj * 4, (int)(typ == 0 ? outlen : 0u));  // 0: not a literal
+    const uint32_t pa_ = (uint32_t)__builtin_amdgcn_ds_bpermute(pj * 4, (int)a);
+    uint32_t sa = a, per = 0, from_in = 1;
+    if (typ != 0) {
+      per = a < outlen ? a : 0u;
+      sa = w - a;
+      from_in = 0;
+      const uint32_t s_hi = per ? w : w - a + outlen;  // end of the output bytes the copy reads
+      if (has_prev && pl_ && sa >= pw_ && s_hi <= pw_ + pl_) {
+        sa = pa_ + (sa - pw_);
+        from_in = 1;
       }
     }
+    const uint32_t pw = (w & 0xFFFFu) | ((outlen - 1) << 16);  // w < ulen <= SN_MAX, outlen <= SN_MAX
+    const uint32_t ps = sa | (from_in << 31);
+    // Execute in order, in batches of up to four elements: the batch's bytes are all read, then all written (one LDS
+    // round trip per batch instead of one per element). An element joins the batch only when its source lies outside
+    // the batch's own output (a literal, a copy resolved to its literal's input bytes, or a copy of earlier output);
+    // a literal over 64 bytes runs alone, pass by pass.
+    uint64_t m = mask;
+    while (m) {
+      // the batch, chosen with scalar work only (no loaded value crosses a branch: the reads below are unconditional)
+      uint32_t eo[4], eln[4], esa[4], eper[4];
+      bool ein[4];
+      uint32_t cnt = 0, bo = 0;
+      bool long_lit = false;
+      uint64_t mm = m;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        eo[k] = 0;
+        eln[k] = 0;
+        esa[k] = 0;
+        eper[k] = 0;
+        ein[k] = true;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (mm == 0 || cnt < (uint32_t)k) continue;
+        const int j = (int)__builtin_ctzll(mm);
+        const uint32_t ew = (uint32_t)__builtin_amdgcn_readlane((int)pw, j);
+        const uint32_t es = (uint32_t)__builtin_amdgcn_readlane((int)ps, j);
+        const uint32_t ep = (uint32_t)__builtin_amdgcn_readlane((int)per, j);
+        const uint32_t o_ = ew & 0xFFFFu, n_ = (ew >> 16) + 1;
+        const bool in_ = (es >> 31) != 0;
+        const uint32_t sa_ = es & 0x7FFFFFFFu;
+        if (n_ > 64) {  // a long literal (a copy is at most 64 bytes) runs alone
+          if (k == 0) {
+            long_lit = true;
+            eo[0] = o_;
+            eln[0] = n_;
+            esa[0] = sa_;
+          }
+          continue;
+        }
+        if (k > 0 && !in_ && (ep ? o_ : sa_ + n_) > bo) continue;  // reads this batch's output: the next batch
+        if (k == 0) bo = o_;
+        mm &= mm - 1;
+        eo[k] = o_;
+        eln[k] = n_;
+        esa[k] = sa_;
+        eper[k] = ep;
+        ein[k] = in_;
+        cnt = k + 1;
+      }
+      if (long_lit) {
+        m &= m - 1;
+        for (uint32_t q2 = lane; q2 < eln[0]; q2 += 64) o[eo[0] + q2] = in[esa[0] + q2];
+        continue;
+      }
+      m = mm;
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t idx = lane < eln[k] ? esa[k] + small_mod(lane, eper[k] ? eper[k] : 64u) : esa[k];
+        v[k] = ein[k] ? in[idx] : o[idx];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (lane < eln[k]) o[eo[k] + lane] = (uint8_t)v[k];
+    }
+    __builtin_amdgcn_wave_barrier();
     w0 += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     base += cur;
   }
@@ -2145,83 +2217,27 @@ __device__ bool sn_serial_decode(const uint8_t* qp, const uint8_t* qe, uint8_t* 
   return ok && o == lim;
 }
 
-// One wave per frame. Table scan (tparts): one workgroup of SN_TS_WAVES waves per 256-frame tile of k_ts_finish -- the
-// workgroup sums the tile totals once (the gate's grand totals and the base of its own tile: O(tiles) loads per
-// workgroup, not per wave), then its waves take the tile's frames in turn. Otherwise one-wave workgroups, grid-stride.
-constexpr uint32_t SN_TS_WAVES = 8;
-__global__ void __launch_bounds__(64 * SN_TS_WAVES) k_snappy_decode_wave(const uint8_t* __restrict__ base,
+// One wave per frame (lcrc_snappy_frames), grid-stride; each chunk's descriptor for the CRC pass over the decoded
+// bytes (the whole-table scan decodes and checks its frames in k_ts_decode instead).
+__global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __restrict__ base,
                                                            const lcrc_desc_dev* __restrict__ frames, uint64_t n,
                                                            const uint64_t* __restrict__ out_off,
-                                                           uint64_t* __restrict__ chunk_off,  // (table scan: each frame's final offset written back)
+                                                           const uint64_t* __restrict__ chunk_off,
                                                            uint8_t* __restrict__ out, uint8_t* __restrict__ status,
                                                            lcrc_desc_dev* __restrict__ cdesc,
                                                            uint32_t* __restrict__ cexp, uint32_t* __restrict__ cframe,
-                                                           uint32_t in_lim, uint32_t out_cap,
-                                                           const uint64_t* __restrict__ n_dev,
-                                                           lcrc_tscan_dev* __restrict__ ts, uint64_t ts_out_cap,
-                                                           uint64_t ts_chunk_cap, uint32_t inline_exp,
-                                                           const uint64_t* __restrict__ tparts,
-                                                           const uint64_t* __restrict__ tnch) {
+                                                           uint32_t in_lim, uint32_t out_cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sn_lds[];
-  if (n_dev) n = *n_dev < n ? *n_dev : n;
   const uint32_t lane = __lane_id();
-  const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  // tparts (table scan): out_off / chunk_off are exclusive scans WITHIN 256-frame tiles (k_ts_finish), the tile
-  // totals in tparts[2 t], tparts[2 t + 1]; the workgroup of tile t adds the tiles before it and writes each frame's
-  // final chunk offset back for k_ts_close
-  auto tile_sum = [&](uint64_t lo, uint64_t hi, uint64_t& so, uint64_t& sc) {
-    unsigned long long xo = 0, xc = 0;
-    for (uint64_t w = lo + lane; w < hi; w += 64) {
-      xo += tparts[2 * w];
-      xc += tparts[2 * w + 1];
-    }
-    for (int d = 1; d < 64; d <<= 1) {
-      xo += __shfl_xor(xo, d, 64);
-      xc += __shfl_xor(xc, d, 64);
-    }
-    so += xo;
-    sc += xc;
-  };
-  uint64_t before_o = 0, before_c = 0;  // tparts: the totals of the tiles before this workgroup's tile
-  if (ts) {
-    // async table scan: the decoded total and the chunk count against the workspace, decided alike by every
-    // workgroup; workgroup 0 records it (over: the host path; no chunk: nothing to decode). A table without Snappy
-    // frames (any_frame 0) needs no sums: both are 0.
-    const uint64_t m = ts->status == 0 ? n : 0;
-    uint64_t total = 0, chunks = 0;
-    if (!tparts) {
-      total = m ? out_off[m] : 0;
-      chunks = m ? chunk_off[m] : 0;
-    } else if (m && ts->any_frame) {
-      const uint64_t tiles = (m + 255) / 256, mine = blockIdx.x < tiles ? blockIdx.x : tiles;
-      tile_sum(0, mine, before_o, before_c);
-      total = before_o;
-      chunks = before_c;
-      tile_sum(mine, tiles, total, chunks);
-    }
-    const bool over = total > ts_out_cap || chunks > ts_chunk_cap;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      ts->need_out = total;
-      ts->need_chunks = chunks;
-      ts->gate = over ? 1u : chunks == 0 ? 2u : 0u;
-      ts->n_chunks = over ? 0 : chunks;  // the chunk count the CRC pass and the check read
-      if (over && ts->status == 0) ts->status = 2;  // TS_HOST
-    }
-    if (over || chunks == 0) return;
-  }
-  uint8_t* const lin = sn_lds + (size_t)wv * (in_lim + SN_SLACK + out_cap);
-  uint8_t* const lout = lin + in_lim + SN_SLACK;
-  const uint64_t f0 = tparts ? (uint64_t)blockIdx.x * 256 + wv : (uint64_t)blockIdx.x * nwv + wv;
-  const uint64_t fstep = tparts ? nwv : (uint64_t)gridDim.x * nwv;
-  const uint64_t fend = tparts ? ((uint64_t)blockIdx.x * 256 + 256 < n ? (uint64_t)blockIdx.x * 256 + 256 : n) : n;
-  for (uint64_t f = f0; f < fend; f += fstep) {
+  uint8_t* const lin = sn_lds;
+  uint8_t* const lout = sn_lds + in_lim + SN_SLACK;
+  for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
     if (status[f]) continue;
     const uint8_t* p = base + frames[f].offset;
     const uint32_t len = frames[f].length;
-    uint64_t o = out_off[f] + before_o;
-    uint64_t c = chunk_off[f] + before_c;
-    const uint64_t c_end = tparts ? c + tnch[f] : chunk_off[f + 1];
-    if (tparts && lane == 0) chunk_off[f] = c;  // k_ts_close reads the frame's chunk range
+    uint64_t o = out_off[f];
+    uint64_t c = chunk_off[f];
+    const uint64_t c_end = chunk_off[f + 1];
     sn_reader rd;
     rd.init(p, len, lane);
     const uint32_t end = rd.lim;
@@ -2278,20 +2294,15 @@ __global__ void __launch_bounds__(64 * SN_TS_WAVES) k_snappy_decode_wave(const u
         o = ((uint64_t)bcast((uint32_t)(o >> 32)) << 32) | bcast((uint32_t)o);
       }
       if (!ok) break;
-      // inline_exp (table scan): the stored CRC goes into the 16 B after the 16-aligned chunk, where the CRC pass
-      // compares it (expect_rel) -- no separate check launch; the next chunk starts 16-aligned
-      const uint32_t clen = (uint32_t)(o - start), pad = (clen + 15) & ~15u;
       if (lane == 0) {
         lcrc_desc_dev d;
         d.offset = start;
-        d.length = clen;
-        d.expect_rel = inline_exp ? (int32_t)pad : LCRC_NO_EXPECT_DEV;
+        d.length = (uint32_t)(o - start);
+        d.expect_rel = LCRC_NO_EXPECT_DEV;
         cdesc[c] = d;
         cexp[c] = want;
         cframe[c] = (uint32_t)f;
-        if (inline_exp) *(uint32_t*)(out + start + pad) = want;
       }
-      if (inline_exp) o = start + pad + 16;
       ++c;
     }
     if (!ok && lane == 0) {
@@ -2940,7 +2951,7 @@ __device__ void ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restr
       s.n_total = n - 1;
     }
   }
-  // only the fields decided here (k_ts_close's other threads may be setting st->unsorted)
+  // only the fields decided here (k_ts_decode's other workgroups may be setting st->unsorted)
   st->status = s.status;
   st->code = s.code;
   st->n_total = s.n_total;
@@ -2954,32 +2965,6 @@ __device__ void ts_final(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restr
 // mismatch bits cmm; not read when the gate sent the frames to the host) -- and the order check of the
 // offsets, then the reference's order of outcomes (ts_final). The last three blocks (filter, metaindex,
 // index), which ts_final may move, are thread 0 of workgroup 0's alone.
-__global__ void __launch_bounds__(256) k_ts_close(lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
-                                                  const uint8_t* __restrict__ fstatus,
-                                                  const uint64_t* __restrict__ choff, const uint64_t* __restrict__ nch,
-                                                  const uint32_t* __restrict__ cmm, uint64_t* __restrict__ n_out,
-                                                  uint32_t* __restrict__ status_out) {
-  // the block count k_ts_emit set, from fields ts_final leaves alone (it may shrink n_total, and workgroups of this
-  // launch may start after workgroup 0 is done); not OK / index-only: only thread 0's three blocks matter
-  const bool live = st->status == TS_OK && !st->idx_only;
-  const uint64_t n = live ? st->n_data + (st->has_filter ? 3 : 2) : 0;
-  const bool bits = st->gate == 0;
-  auto content = [&](uint64_t j) {
-    bool bad = fstatus[j] != 0;
-    if (bits)
-      for (uint64_t c = choff[j], ce = c + nch[j]; !bad && c < ce; ++c) bad = (cmm[c >> 5] >> (c & 31)) & 1;
-    if (bad) blk[j].status = 3;  // LCRC_TBLK_BAD_CONTENT
-    if (j > 0 && blk[j - 1].offset > blk[j].offset) st->unsorted = 1;
-  };
-  const uint64_t tail = n > 3 ? n - 3 : 0;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < tail) content(i);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint64_t n0 = st->n_total;  // = n when live
-    for (uint64_t j = n0 > 3 ? n0 - 3 : 0; j < n0; ++j) content(j);
-    ts_final(st, blk, n_out, status_out);
-  }
-}
 
 // ---------------------------------------------------------------------------------------------------
 // small helpers of the table scan and the writer-side seal
@@ -3406,13 +3391,6 @@ hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t*
   return hipGetLastError();
 }
 // grid: a bound on the blocks
-hipError_t lcrc_launch_ts_close(lcrc_tscan_dev* st, lcrc_tblk_dev* blk, uint64_t bound, const uint8_t* fstatus,
-                               const uint64_t* choff, const uint64_t* nch, const uint32_t* cmm, uint64_t* n_out,
-                               uint32_t* status_out, hipStream_t s) {
-  LCRC_LAUNCH(lcrc_dev::k_ts_close, dim3((unsigned)(bound / 256 + 1)), dim3(256), 0, s, st, blk, fstatus, choff, nch,
-              cmm, n_out, status_out);
-  return hipGetLastError();
-}
 
 // the table scan's decode, chunk checks and close in one launch (k_ts_decode); bound: the result capacity
 hipError_t lcrc_launch_ts_decode(const uint8_t* file, const lcrc_desc_dev* frames, const uint64_t* out_off, uint8_t* out,
@@ -3540,30 +3518,18 @@ hipError_t lcrc_launch_scan2(const uint64_t* a, const uint64_t* b, uint64_t n, u
 }
 
 hipError_t lcrc_launch_snappy_decode(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n,
-                                     const uint64_t* out_off, uint64_t* chunk_off, uint8_t* out, uint8_t* status,
+                                     const uint64_t* out_off, const uint64_t* chunk_off, uint8_t* out, uint8_t* status,
                                      lcrc_desc_dev* cdesc, uint32_t* cexp, uint32_t* cframe, uint32_t max_in,
-                                     uint32_t max_out, const uint64_t* n_dev, lcrc_tscan_dev* ts, uint64_t ts_out_cap,
-                                     uint64_t ts_chunk_cap, uint32_t inline_exp, const uint64_t* tparts,
-                                     const uint64_t* tnch, hipStream_t st) {
+                                     uint32_t max_out, hipStream_t st) {
   using lcrc_dev::SN_MAX;
   if (n == 0) return hipSuccess;
-  // table scan (tparts): one workgroup of SN_TS_WAVES waves per 256-frame tile; otherwise one wave per workgroup,
-  // grid-stride
-  const uint32_t waves = tparts ? lcrc_dev::SN_TS_WAVES : 1;
-  const uint64_t g = tparts ? (n + 255) / 256 : (n < 16384 ? n : 16384);
+  const uint64_t g = n < 16384 ? n : 16384;  // one wave per frame, grid-stride
   // LDS sized to the batch's largest chunk (bigger ones take the lane-serial path): small staging, many waves
   const uint32_t in_lim = max_in + 4 < SN_MAX ? (max_in + 4 + 15) & ~15u : SN_MAX;
   const uint32_t out_cap = max_out < SN_MAX ? (max_out + 15) & ~15u : SN_MAX;
-  const size_t lds = ((size_t)in_lim + lcrc_dev::SN_SLACK + out_cap) * waves;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (lds > 64 * 1024) {  // more than the default dynamic LDS: raise the kernel's limit (once per process)
-    static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_snappy_decode_wave,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (attr != hipSuccess) return attr;
-  }
-  LCRC_LAUNCH(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64 * waves), lds, st, base, frames, n, out_off,
-                     chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap, n_dev, ts, ts_out_cap,
-                     ts_chunk_cap, inline_exp, tparts, tnch);
+  const size_t lds = (size_t)in_lim + lcrc_dev::SN_SLACK + out_cap;
+  LCRC_LAUNCH(lcrc_dev::k_snappy_decode_wave, dim3((unsigned)g), dim3(64), lds, st, base, frames, n, out_off,
+              chunk_off, out, status, cdesc, cexp, cframe, in_lim, out_cap);
   return hipGetLastError();
 }
 
