@@ -25,9 +25,11 @@ for c in $CONFIGS; do
   BC="--config $c"; [ "$c" = tablez ] && BC="--config table --compression 1"
   timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 $BC --extra-out "$OUT/bench_${c}_full.json" > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }
   cut -c1-300 "$OUT/bench_$c.json"
-  # the committed line is this un-profiled run: the summary's agreement is computed against it
-  cp "$OUT/bench_${c}_full.json" profiles/${R}_bench_${c}_c.json
-  python3 tools/summarize_profile.py gpurun_out/prof_${R}_${c}_c $R $c c profiles/${R}_bench_${c}_c.json > /dev/null
-  python3 -c "import json;s=json.load(open('profiles/${R}_${c}_c_summary.json'));print('$c agreement vs committed line:', s.get('agreement'), 'wall', s.get('agreement_wall'))"
-  cp profiles/${R}_${c}_c_* profiles/${R}_bench_${c}_c.json profiles/traffic_${c}_c.json "$OUT/profiles/"
+  # the committed line is the profiled run's own line (the trace reproduces it); the un-profiled run of the same
+  # command is kept beside it (the profiler's per-dispatch cost slows multi-kernel steps on two streams)
+  cp gpurun_out/prof_${R}_${c}_c/bench.json profiles/${R}_bench_${c}_c.json
+  cp "$OUT/bench_${c}_full.json" profiles/${R}_bench_${c}_c_unprofiled.json
+  python3 tools/summarize_profile.py gpurun_out/prof_${R}_${c}_c $R $c c profiles/${R}_bench_${c}_c.json profiles/${R}_bench_${c}_c_unprofiled.json > /dev/null
+  python3 -c "import json;s=json.load(open('profiles/${R}_${c}_c_summary.json'));print('$c agreement vs committed line:', s.get('agreement'), 'wall', s.get('agreement_wall'), 'vs un-profiled run:', s.get('agreement_unprofiled'))"
+  cp profiles/${R}_${c}_c_* profiles/${R}_bench_${c}_c*.json profiles/traffic_${c}_c.json "$OUT/profiles/"
 done

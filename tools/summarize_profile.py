@@ -1,6 +1,6 @@
 """Summarize a tools/profile_round.sh output directory into profiles/ (committed evidence).
 
-Usage: summarize_profile.py OUTDIR ROUND CONFIG MODE [COMMITTED_LINE_JSON]
+Usage: summarize_profile.py OUTDIR ROUND CONFIG MODE [COMMITTED_LINE_JSON [UNPROFILED_LINE_JSON]]
 
 Writes:
   profiles/<round>_<config>_<mode>_kernel_stats.csv   (rocprofv3 --stats table, verbatim)
@@ -35,7 +35,7 @@ def counters(d, name):
     return per
 
 
-def main(outdir, rnd, config, mode, committed=None):
+def main(outdir, rnd, config, mode, committed=None, unprofiled=None):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     tag = f"{rnd}_{config}_{mode}"
@@ -121,24 +121,27 @@ def main(outdir, rnd, config, mode, committed=None):
                     summary["kernels_per_step"] = kps or 1
                     # against the profiled run's own line (the same process the trace comes from)
                     summary["agreement_profiled_run"] = round(summary["frac_from_trace"] / line["roofline"]["frac"], 4)
-            # against the COMMITTED line: the un-profiled bench run of the same command that DESIGN.md quotes
-            # (tools/gpu_round.sh runs it right after the profile and re-summarizes with it)
-            if committed and os.path.exists(committed) and "trace_launch_us" in summary:
-                with open(committed) as f:
+            # against the COMMITTED line (the line DESIGN.md quotes; tools/gpu_round.sh commits the profiled run's own
+            # line) and, when given, an un-profiled run of the same command taken right after
+            for key, path in (("", committed), ("_unprofiled", unprofiled)):
+                if not (path and os.path.exists(path) and "trace_launch_us" in summary):
+                    continue
+                with open(path) as f:
                     cl = json.load(f)
                 cr = cl.get("roofline") or {}
-                summary["committed_line"] = {"file": os.path.relpath(committed, ROOT), "value": cl["value"],
-                                             "ms_per_step": cl["ms_per_step"], "launch_us": cr.get("launch_us"),
-                                             "frac": cr.get("frac")}
+                summary["committed_line" if not key else "unprofiled_line"] = {
+                    "file": os.path.relpath(path, ROOT), "value": cl["value"], "ms_per_step": cl["ms_per_step"],
+                    "launch_us": cr.get("launch_us"), "frac": cr.get("frac")}
                 if cr.get("launch_us"):
-                    summary["agreement"] = round(cr["launch_us"] / summary["trace_launch_us"], 4)
-                summary["agreement_wall"] = round(cl["ms_per_step"] * 1e3 / summary["trace_launch_us"], 4)
+                    summary["agreement" + key] = round(cr["launch_us"] / summary["trace_launch_us"], 4)
+                summary["agreement_wall" + key] = round(cl["ms_per_step"] * 1e3 / summary["trace_launch_us"], 4)
             summary["note"] = ("frac: the dominant kernel's average duration alone (rocprofv3 kernel trace); "
                                "frac_from_trace: the bench line's measure (its timed launches, first to last, per "
                                "launch) on the same trace -- the difference is the dispatch gap between two in-order "
                                "launches. agreement = the committed line's GPU time per launch / the trace's "
                                "(1.0: the trace reproduces the committed line); agreement_wall = its wall time per step / "
-                               "the trace's; agreement_profiled_run = frac_from_trace / the profiled run's own line frac")
+                               "the trace's; *_unprofiled: the same against an un-profiled run of the command; "
+                               "agreement_profiled_run = frac_from_trace / the profiled run's own line frac")
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     # the dominant kernel's traffic for bench.py
@@ -165,4 +168,4 @@ def main(outdir, rnd, config, mode, committed=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:6])
+    main(*sys.argv[1:7])
