@@ -1788,11 +1788,26 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
 // the framing walk of one frame p[0, len): decoded size, data-chunk count, largest compressed data (after the
 // crc) and decoded chunk; false when the framing is malformed
 // padded: the bytes the table scan's decode takes, each chunk 16-aligned with its stored CRC in the 16 B after it
+// LDS staging of the wave decoders: compressed bytes + SN_SLACK for the parse windows' header reads, then the decoded
+// bytes, each at most SN_MAX (k_snappy_decode_wave sizes them from the batch's largest chunk)
+constexpr uint32_t SN_SLACK = 128;
+constexpr uint32_t SN_MAX = 16384;
+// k_ts_decode (the whole-table scan's decode): 8 waves per 256-block tile, each with this LDS staging
+constexpr uint32_t TD_WAVES = 8;
+constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
+constexpr uint32_t TD_IN = 6144 + 16;   // LDS staging per wave: compressed bytes (+ 4 for the tail dword)
+constexpr uint32_t TD_OUT = 7168;       // decoded bytes (a multiple of 1 KiB: V fits as is)
+constexpr uint32_t TD_WAVE_LDS = TD_IN + SN_SLACK + TD_OUT;
+constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
+
+// `slow`: the decoded bytes (16-aligned) of the compressed chunks too large for k_ts_decode's LDS staging (TD_IN
+// compressed, TD_OUT decoded), which it decodes lane-serially into the table scan's workspace
 __device__ __forceinline__ bool snappy_frame_size(const uint8_t* __restrict__ p, uint32_t len, uint64_t& total,
                                                   uint64_t& chunks, uint32_t& max_in, uint32_t& max_out,
-                                                  uint64_t& padded) {
+                                                  uint64_t& padded, uint64_t* slow = nullptr) {
   total = 0;
   padded = 0;
+  if (slow) *slow = 0;
   chunks = 0;
   max_in = 0;
   max_out = 0;
@@ -1825,6 +1840,7 @@ __device__ __forceinline__ bool snappy_frame_size(const uint8_t* __restrict__ p,
       if (ulen > max_out) max_out = ulen;
       total += ulen;
       padded += ((ulen + 15) & ~15u) + 16;
+      if (slow && type == 0 && (ulen > TD_OUT || cl - used + 4 > TD_IN + 4)) *slow += (ulen + 15) & ~15u;
       ++chunks;
     } else if (type <= 0x7f) {
       ok = false;  // reserved unskippable
@@ -1957,10 +1973,6 @@ __global__ void __launch_bounds__(256) k_scan2_add(uint64_t n, uint64_t* __restr
 // v_readlane with a scalar index). A compressed chunk is staged into LDS with dword loads, decoded in LDS
 // (snappy_wave_decode) and leaves LDS with 16 B per lane. Chunks over the LDS staging take a lane-serial
 // path from and to global memory.
-// LDS staging per wave (dynamic, sized by the launcher from the batch's largest chunk): in_lim compressed
-// bytes + SN_SLACK for the parse windows' header reads, then out_cap decoded bytes; each at most SN_MAX
-constexpr uint32_t SN_SLACK = 128;
-constexpr uint32_t SN_MAX = 16384;
 
 __device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -2835,10 +2847,11 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
 
 // read_block_from_file's type dispatch for every block (k_tbl_finish) and, in the same thread, the framing
 // walk of the block's Snappy frame (k_snappy_size)
-// The frames' decoded sizes (padded, see snappy_frame_size) and chunk counts are scanned within the workgroup
-// (out_off, choff) with the workgroup totals in part[2 b], part[2 b + 1]: k_snappy_decode_wave adds the totals of
-// the tiles before each frame itself (no scan launch between), and sums them all for its gate only when a tile
-// had frames (any_frame).
+// The frames' workspace sizes (the decoded bytes of chunks too large for k_ts_decode's LDS staging, see
+// snappy_frame_size) and chunk counts are scanned within the workgroup
+// (out_off, choff) with the workgroup totals in part[2 b], part[2 b + 1]: k_ts_decode's workgroup of a tile adds the
+// totals of the tiles before it (no scan launch between), and sums them all for its gate only when a tile had frames
+// (any_frame).
 __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
                                                    const uint32_t* __restrict__ crc,
                                                    const uint32_t* __restrict__ mismatch,
@@ -2902,10 +2915,10 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
     f.expect_rel = LCRC_NO_EXPECT_DEV;
     blk[i] = b;
     frames[i] = f;
-    uint64_t total, chunks, padded;
+    uint64_t total, chunks, padded, slow;
     uint32_t mi, mo;
-    const bool ok = snappy_frame_size(file + f.offset, flen, total, chunks, mi, mo, padded);
-    fsize = ok ? padded : 0;
+    const bool ok = snappy_frame_size(file + f.offset, flen, total, chunks, mi, mo, padded, &slow);
+    fsize = ok ? slow : 0;  // k_ts_decode's workspace: only the chunks it cannot decode in LDS
     fch = ok ? chunks : 0;
     nchunks[i] = fch;
     fstatus[i] = ok ? 0 : 1;
@@ -3011,12 +3024,6 @@ __global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, u
 // Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- a 32 KiB table copy in LDS. The init register
 // is injected into the first min(4, |M|) bytes: walk(R, M) = walk(0, M ^ LE(R)) ^ (R >> 8 |M|) for |M| < 4.
 // ---------------------------------------------------------------------------------------------------
-constexpr uint32_t TD_WAVES = 8;
-constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
-constexpr uint32_t TD_IN = 6144 + 16;   // LDS staging per wave: compressed bytes (+ 4 for the tail dword)
-constexpr uint32_t TD_OUT = 7168;       // decoded bytes (a multiple of 1 KiB: V fits as is)
-constexpr uint32_t TD_WAVE_LDS = TD_IN + SN_SLACK + TD_OUT;
-constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
 
 // the piece of pass k of lane `lane`: V[1024 k + 16 lane, +16), init injected into V[pad, pad + q)
 __device__ __forceinline__ u32x4 td_inject(u32x4 w, uint32_t x0, uint32_t pad, uint32_t q) {
