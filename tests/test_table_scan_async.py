@@ -180,13 +180,18 @@ def test_async_capacity_and_workspace(lcrc, orc, engines):
                                 filter_block=b"k" * 30)
     assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks) - 1) == CAPACITY
     assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks)) == OK
-    # decoded frames over the reserved workspace: handed to the host, and the sync wrapper grows it
+    # chunks the decoder's LDS staging holds need no workspace (k_ts_decode checksums them in LDS): OK even with a
+    # 16-byte reservation. 64 KiB blocks' chunks are decoded lane-serially into the workspace: over the reservation
+    # they are handed to the host, and the sync wrapper grows it
     eng2 = lcrc.Engine(0, lcrc.MODE_REF)
     try:
-        assert _expect_async(lcrc, eng2, orc, f, FILTER, decoded=16) == HOST
-        got, err = _sync(lcrc, eng2, f, FILTER)
-        assert err is None and _as_tuples(got) == orc.table_scan_expect(f, FILTER)[0]
-        assert _expect_async(lcrc, eng2, orc, f, FILTER, decoded=0) == OK  # the grown workspace stays
+        assert _expect_async(lcrc, eng2, orc, f, FILTER, decoded=16) == OK
+        g, _ = orc.table_build(_kvs(3000, 13 + 65536), block_size=65536, compression=1, filter_name=FILTER,
+                               filter_block=b"k" * 30)
+        assert _expect_async(lcrc, eng2, orc, g, FILTER, decoded=16) == HOST
+        got, err = _sync(lcrc, eng2, g, FILTER)
+        assert err is None and _as_tuples(got) == orc.table_scan_expect(g, FILTER)[0]
+        assert _expect_async(lcrc, eng2, orc, g, FILTER, decoded=0) == OK  # the grown workspace stays
     finally:
         eng2.close()
 
