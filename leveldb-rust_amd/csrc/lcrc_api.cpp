@@ -205,7 +205,7 @@ struct lcrc_ctx {
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
   void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
   uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
-  uint64_t ts_out_cap = 0;  // the decode workspace: ts_decoded_cap + 32 per chunk (16-aligned chunks + stored CRCs)
+  uint64_t ts_out_cap = 0;  // the decode workspace: ts_decoded_cap + the 16-alignment of its (large) chunks
   // lcrc_ctx_options (lcrc_ctx_create_ex; tests and measurement only -- the library reads no environment variable)
   uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (tests reach the tile loops with a small one)
   int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan
@@ -1339,15 +1339,15 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
       (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) || (rc = ctx->sn_status.ensure(nb)) ||
       (rc = ctx->sn_max.ensure(2)) || (rc = ctx->sn_cdesc.ensure(cc)) || (rc = ctx->sn_cexp.ensure(cc)) ||
       (rc = ctx->sn_cframe.ensure(cc)) || (rc = ctx->sn_ccrc.ensure(cc)) || (rc = ctx->sn_cmm.ensure(cc / 32 + 1)) ||
-      (rc = ctx->sn_out.ensure(decoded_cap + 32 * cc + 16)) ||
+      (rc = ctx->sn_out.ensure(decoded_cap + 16 * (decoded_cap / 4096 + 1) + 16)) ||
       (rc = ctx->win.ensure(window_words(max_file_len))))
     return rc;
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   ctx->ts_decoded_cap = decoded_cap;
   ctx->ts_chunk_cap = cc;
-  // the decode lands every chunk 16-aligned with its stored CRC in the 16 B after it: up to 31 B per chunk past the
-  // decoded bytes themselves, so a caller reserving the exact decoded total still scans on the device
-  ctx->ts_out_cap = decoded_cap + 32 * cc;
+  // the workspace holds only the chunks k_ts_decode cannot decode in LDS (over 6 KiB compressed or 7 KiB decoded),
+  // each 16-aligned: a caller reserving the exact decoded total still scans on the device
+  ctx->ts_out_cap = decoded_cap + 16 * (decoded_cap / 4096 + 1);
   return LCRC_OK;
 }
 
