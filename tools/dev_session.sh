@@ -23,6 +23,7 @@ for s in ${STEPS:-fixed}; do
           python3 tools/probe/ab_many_summary.py | tee $O/sens_summary.txt ;;
     *) c=${s%@*}; var=""; [ "$c" != "$s" ] && var=${s#*@}
        BC="--config $c"; [ "$c" = tablez ] && BC="--config table --compression 1"
+       [ "$c" = tablezsync ] && BC="--config table --compression 1 --table-sync"
        tag=$c${var:+_$var}
        ( [ -n "$var" ] && export LCRC_LIB_PATH=$PWD/tools/probe/variants/$var.so
          timeout -k 10 300 python -u bench.py $BC ${BENCH_ARGS} --extra-out $O/bench_${tag}_full.json > $O/bench_$tag.json 2> $O/bench_$tag.err ) || { tail -20 $O/bench_$tag.err; exit 1; }
