@@ -54,6 +54,7 @@ MIXED_QUEUE = 1  # mixed config: steps per lcrc_batch_queue submission (1: one l
 WAL_QUEUE = 1  # wal config: scans per lcrc_wal_scan_queue submission (1: one lcrc_wal_scan_async per step)
 WAL_KERNELS = 4  # lcrc_wal_scan_async: header walk, record emit, window pass, range pass
 TABLE_KERNELS = 6  # lcrc_table_scan_async: index, emit, windows, blocks, finish, decode + chunk checks + close
+# (+ 1 with LCRC_TSCAN_SNAPPY_INDEX: the compressed table's Snappy-framed index decoded first, k_ts_open)
 
 
 def parse(argv=None):
@@ -580,10 +581,11 @@ def workload_table(m, synth, engs, rank, device, args):
                 dec_bytes += len(m.snappy_frame_decode(f[off:off + size]))
     for e in scanners:
         e.table_scan_reserve(len(f), cap, dec_bytes)
-    # the async form (lcrc_table_scan_async) must agree with the synchronous one before it is timed (the synchronous
-    # form is what --table-sync times: a table the device-only walk hands to the host -- a Snappy-framed index block --
-    # is scanned through it)
-    scanners[0].table_scan_async(dev, len(f), res[0][0], cap, res[0][1], res[0][2])
+    # the async form (lcrc_table_scan_async) must agree with the synchronous one before it is timed. A table written
+    # with compression has a Snappy-framed index block (table.rs:430): the async scan is told so
+    # (lcrc_table_scan_async_ex, LCRC_TSCAN_SNAPPY_INDEX) and decodes it on the device
+    si = bool(args.compression)
+    scanners[0].table_scan_async(dev, len(f), res[0][0], cap, res[0][1], res[0][2], snappy_index=si)
     scanners[0].sync()
     st = res[0][2].download(np.uint32, 2)
     n = int(res[0][1].download(np.uint64, 1)[0])
@@ -599,7 +601,8 @@ def workload_table(m, synth, engs, rank, device, args):
     elif args.graph:
         # each scanner's whole scan (14 launches) captured once in a HIP graph and replayed per step
         # (graph k scans copy k % 2)
-        graphs = [e.graph_capture(lambda e=e, r=r, d=devs[k % 2]: e.table_scan_async(d, len(f), r[0], cap, r[1], r[2]))
+        graphs = [e.graph_capture(lambda e=e, r=r, d=devs[k % 2]: e.table_scan_async(d, len(f), r[0], cap, r[1], r[2],
+                                                                                     snappy_index=si))
                   for k, (e, r) in enumerate(zip(scanners, res))]
 
         def run(first, count):
@@ -610,7 +613,7 @@ def workload_table(m, synth, engs, rank, device, args):
         def run(first, count):  # device-only: enqueued, results, count and verdict stay on the device
             for i in range(first, first + count):
                 k = i % len(engs)
-                scanners[k].table_scan_async(devs[i % 2], len(f), res[k][0], cap, res[k][1], res[k][2])
+                scanners[k].table_scan_async(devs[i % 2], len(f), res[k][0], cap, res[k][1], res[k][2], snappy_index=si)
 
     run.keep = (pinned, scanners, res, devs)  # (a graph holds raw pointers: the files must outlive it)
     cfg = {"workload": ("whole-table verify scan: ~64K Snappy-compressed data blocks (4 KiB raw, db_bench values) + "
@@ -621,9 +624,10 @@ def workload_table(m, synth, engs, rank, device, args):
            "bytes_counted": "sum(stored block + type byte): the block checksums' bytes",
            "blocks": len(blocks), "file_bytes": int(len(f)), "crc": "crc-32/iso-hdlc (crc32fast), the reference's trailers",
            "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else
-           "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async"}
+           "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async",
+           "snappy_index": bool(args.compression and framed[kinds == m.TBLK_INDEX].any())}
     return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None,
-                    per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS,
+                    per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si),
                     kernel_events=not (args.table_sync or args.graph))
 
 

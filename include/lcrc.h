@@ -298,14 +298,24 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
  * blocks in index order (by offset for a well-formed table); *n_blocks (device or pinned) their count;
  * status[0..1] (device or pinned u32) the verdict: LCRC_TSCAN_OK, LCRC_TSCAN_CORRUPT with status[1] the
  * message (lcrc_table_scan_message), LCRC_TSCAN_HOST when the table needs the synchronous scan's host
- * walk (a Snappy-framed index or metaindex, a handle past the file, restart segments over 4 KiB, decoded
- * frames over the reserved workspace), or LCRC_TSCAN_CAPACITY with *n_blocks the capacity needed. */
+ * walk (a Snappy-framed index without LCRC_TSCAN_SNAPPY_INDEX or one that does not decode, a Snappy-framed
+ * metaindex, a handle past the file, restart segments over 4 KiB, decoded bytes over the reserved workspace), or
+ * LCRC_TSCAN_CAPACITY with *n_blocks the capacity needed. */
 #define LCRC_TSCAN_OK 0
 #define LCRC_TSCAN_CORRUPT 1
 #define LCRC_TSCAN_HOST 2
 #define LCRC_TSCAN_CAPACITY 3
 int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
                           lcrc_tblk* blocks, size_t max_blocks, uint64_t* n_blocks, uint32_t* status, void* stream);
+/* lcrc_table_scan_async with flags. LCRC_TSCAN_SNAPPY_INDEX: the table was written with Snappy compression (the
+ * reference's default, option.rs:127), so its index block is likely a Snappy frame (table.rs:430, write_block):
+ * one more launch decodes a framed index block on the device -- every chunk's masked CRC-32C checked -- and the walk
+ * reads the decoded contents (without the flag such a table is LCRC_TSCAN_HOST; with it a raw index costs that
+ * launch only). The decoded index takes workspace like the frames' (lcrc_table_scan_reserve's decoded_cap). */
+#define LCRC_TSCAN_SNAPPY_INDEX 0x1u
+int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
+                             lcrc_tblk* blocks, size_t max_blocks, uint64_t* n_blocks, uint32_t* status, uint32_t flags,
+                             void* stream);
 /* Workspace for lcrc_table_scan_async up to these sizes (decoded_cap: the Snappy frames' decoded bytes). */
 int lcrc_table_scan_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap);
 /* The reference's message for a LCRC_TSCAN_CORRUPT code ("" for none). */

@@ -27,6 +27,7 @@ MODE_REF = 0  # CRC-32/ISO-HDLC (crc32fast)
 MODE_C = 1  # CRC-32C
 FLAG_MASK = 0x1
 FLAG_DIRECT = 0x2
+TSCAN_SNAPPY_INDEX = 0x1  # lcrc_table_scan_async_ex: decode a Snappy-framed index block on the device
 NO_EXPECT = -0x80000000
 
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ECORRUPT, ERANGE = 0, -1, -2, -3, -4, -5, -6
@@ -105,7 +106,7 @@ ABI_SYMBOLS = [
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
     "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_create_ex", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream", "lcrc_ctx_join",
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_multi", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
-    "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
+    "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_async_ex", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
     "lcrc_tb_create", "lcrc_tb_destroy", "lcrc_tb_add", "lcrc_tb_add_many", "lcrc_tb_flush", "lcrc_tb_finish", "lcrc_tb_size",
     "lcrc_tb_data", "lcrc_tb_blocks", "lcrc_tb_seal_descs",
@@ -164,6 +165,7 @@ def lib():
     sig("lcrc_table_scan", i32, vp, vp, u64, cp, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp, sz)
     sig("lcrc_batch_seal", i32, vp, vp, u64, vp, sz, vp, vp)
     sig("lcrc_table_scan_async", i32, vp, vp, u64, cp, vp, sz, vp, vp, vp)
+    sig("lcrc_table_scan_async_ex", i32, vp, vp, u64, cp, vp, sz, vp, vp, u32, vp)
     sig("lcrc_table_scan_reserve", i32, vp, u64, sz, u64)
     sig("lcrc_table_scan_message", cp, u32)
     sig("lcrc_snappy_frames", i32, vp, vp, vp, sz, vp, u64, vp, vp, ctypes.POINTER(ctypes.c_uint64))
@@ -550,10 +552,16 @@ class Engine:
                "lcrc_table_scan_reserve")
 
     def table_scan_async(self, file_dev, file_len, blocks_dev, max_blocks, count_dev, status_dev, filter_name=None,
-                         stream=None):
+                         stream=None, snappy_index=False):
         """lcrc_table_scan_async: enqueued, device-only; results, count (u64) and status (2 x u32) stay where
-        the caller points them (device or pinned memory)."""
+        the caller points them (device or pinned memory). snappy_index: lcrc_table_scan_async_ex with
+        LCRC_TSCAN_SNAPPY_INDEX (a table written with compression: its Snappy-framed index decoded on the device)."""
         fname = filter_name.encode() if isinstance(filter_name, str) else filter_name
+        if snappy_index:
+            _check(lib().lcrc_table_scan_async_ex(self.ctx, _ptr(file_dev), int(file_len), fname, _ptr(blocks_dev),
+                                                  int(max_blocks), _ptr(count_dev), _ptr(status_dev),
+                                                  TSCAN_SNAPPY_INDEX, stream), "lcrc_table_scan_async_ex")
+            return
         _check(lib().lcrc_table_scan_async(self.ctx, _ptr(file_dev), int(file_len), fname, _ptr(blocks_dev),
                                            int(max_blocks), _ptr(count_dev), _ptr(status_dev), stream),
                "lcrc_table_scan_async")

@@ -39,10 +39,14 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
                                      hipEvent_t t_stop);
 hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                 lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
-                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, hipStream_t s);
+                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
+                                const uint64_t* iopen, hipStream_t s);
+hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uint32_t* tab_c, uint8_t* idec,
+                               uint64_t idec_cap, uint64_t* iopen, hipStream_t s);
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
                                const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t vcap, uint64_t bound, uint32_t gcap, hipStream_t s);
+                               uint64_t vcap, uint64_t bound, uint32_t gcap, const uint8_t* idec, uint64_t* iopen,
+                               hipStream_t s);
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
                                  uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, lcrc_tscan_dev* st,
@@ -200,6 +204,8 @@ struct lcrc_ctx {
   DevBuf<uint8_t> tbl_types;
   // asynchronous table scan: its device state, the result staging of the synchronous wrapper, capacities
   DevBuf<lcrc_tscan_dev> ts_state;
+  DevBuf<uint8_t> ts_idx;    // table scan: a Snappy-framed index block decoded on the device (k_ts_open)
+  DevBuf<uint64_t> ts_open;  // k_ts_open's verdict words (zeroed when allocated)
   DevBuf<lcrc_tblk_dev> ts_blocks;
   DevBuf<uint64_t> ts_count;
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
@@ -435,6 +441,8 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->tbl_pos.release();
   ctx->tbl_types.release();
   ctx->ts_state.release();
+  ctx->ts_idx.release();
+  ctx->ts_open.release();
   ctx->ts_blocks.release();
   ctx->ts_count.release();
   if (ctx->ts_host) (void)hipHostFree(ctx->ts_host);
@@ -1340,8 +1348,12 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
       (rc = ctx->sn_max.ensure(2)) || (rc = ctx->sn_cdesc.ensure(cc)) || (rc = ctx->sn_cexp.ensure(cc)) ||
       (rc = ctx->sn_cframe.ensure(cc)) || (rc = ctx->sn_ccrc.ensure(cc)) || (rc = ctx->sn_cmm.ensure(cc / 32 + 1)) ||
       (rc = ctx->sn_out.ensure(decoded_cap + 16 * (decoded_cap / 4096 + 1) + 16)) ||
-      (rc = ctx->win.ensure(window_words(max_file_len))))
+      (rc = ctx->win.ensure(window_words(max_file_len))) || (rc = ctx->ts_idx.ensure(decoded_cap)))
     return rc;
+  if (!ctx->ts_open.p) {
+    if ((rc = ctx->ts_open.ensure(4))) return rc;
+    HIPCHK(hipMemset(ctx->ts_open.p, 0, 4 * sizeof(uint64_t)));
+  }
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   ctx->ts_decoded_cap = decoded_cap;
   ctx->ts_chunk_cap = cc;
@@ -1358,8 +1370,16 @@ int lcrc_table_scan_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blo
 
 int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
                           lcrc_tblk* blocks, size_t max_blocks, uint64_t* n_blocks, uint32_t* status, void* stream) {
+  return lcrc_table_scan_async_ex(ctx, file, file_len, filter_name, blocks, max_blocks, n_blocks, status, 0, stream);
+}
+
+int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
+                             lcrc_tblk* blocks, size_t max_blocks, uint64_t* n_blocks, uint32_t* status, uint32_t flags,
+                             void* stream) {
   TkScope tk_scope(ctx);
-  if (!ctx || !n_blocks || !status || (file_len && !file) || (max_blocks && !blocks)) return LCRC_EINVAL;
+  if (!ctx || !n_blocks || !status || (file_len && !file) || (max_blocks && !blocks) ||
+      (flags & ~LCRC_TSCAN_SNAPPY_INDEX))
+    return LCRC_EINVAL;
   lcrc_tscan_key key;
   memset(&key, 0, sizeof(key));
   if (filter_name) {
@@ -1377,14 +1397,19 @@ int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len,
   lcrc_tblk_dev* blk = (lcrc_tblk_dev*)blocks;
   const uint64_t cap = max_blocks;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
-  // Six dependent launches. The footer, the index block header and the metaindex filter entry (optimistic:
-  // checksums come with the batch) with the index block's restart segments: entry counts, scanned per tile
+  // Six dependent launches (seven with LCRC_TSCAN_SNAPPY_INDEX: a Snappy-framed index block decoded first). The
+  // footer, the index block header and the metaindex filter entry (optimistic: checksums come with the batch) with
+  // the index block's restart segments: entry counts, scanned per tile
+  const bool sidx = flags & LCRC_TSCAN_SNAPPY_INDEX;
+  if (sidx)
+    HIPCHK(lcrc_launch_ts_open(file, file_len, tab_c, ctx->ts_idx.p, ctx->ts_idx.cap, ctx->ts_open.p, st));
   const uint64_t vcap = ts_verify_cap(cap, file_len);
   HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
-                              ctx->ts_grid, ctx->tbl_mm.p, vcap / 32 + 1, st));
+                              ctx->ts_grid, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p, sidx ? ctx->ts_open.p : nullptr,
+                              st));
   // the handles and the verify descriptors
   HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_count.p, ctx->sn_part.p, blk, ctx->tbl_descs.p, cap, vcap, cap,
-                             ctx->ts_grid, st));
+                             ctx->ts_grid, ctx->ts_idx.p, ctx->ts_open.p, st));
   // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
   const uint64_t* nver = &S->n_verify;
   if (cap) {
@@ -1449,8 +1474,8 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
       rc = ctx->ts_blocks.ensure(cap);
       if (!rc) rc = ctx->ts_count.ensure(1);
       if (!rc)
-        rc = lcrc_table_scan_async(ctx, file, file_len, filter_name, (lcrc_tblk*)ctx->ts_blocks.p, cap,
-                                   ctx->ts_count.p, ctx->ts_count_status, nullptr);
+        rc = lcrc_table_scan_async_ex(ctx, file, file_len, filter_name, (lcrc_tblk*)ctx->ts_blocks.p, cap,
+                                      ctx->ts_count.p, ctx->ts_count_status, LCRC_TSCAN_SNAPPY_INDEX, nullptr);
       if (rc == LCRC_ENOMEM) {  // no workspace for the device-only scan: the paths below (other errors propagate)
         ran = false;
         break;
@@ -1460,7 +1485,7 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
       HIPCHK(hipStreamSynchronize(st));
       if (hs->status == 3) {  // capacity: grow to what the table needs and scan again
         cap = std::max<uint64_t>(hs->n_data + 16, cap * 2);
-      } else if (hs->status == 2 && hs->gate == 1) {  // decoded frames over the workspace: grow it, scan again
+      } else if (hs->status == 2 && hs->gate == 1) {  // decoded frames or index over the workspace: grow it, scan again
         rc = ts_reserve(ctx, file_len, cap, hs->need_out + hs->need_out / 4 + 4096, hs->need_chunks + 64);
         if (rc == LCRC_ENOMEM) {
           ran = false;

@@ -102,6 +102,9 @@ struct lcrc_tscan_dev {
   // filter, metaindex, index: a block longer than LCRC_TS_PIECE is verified as pieces of that size (one row of
   // the batch kernel each, instead of one row folding thousands of windows), combined afterwards
   uint32_t pbase[3], pcnt[3];
+  // a Snappy-framed index block decoded on the device first (k_ts_open): the walk reads the decoded contents
+  uint32_t idx_dec, pad_;
+  uint64_t idx_clen;  // the index block's contents length (decoded when idx_dec, else idx_size)
 };
 #define LCRC_TS_PIECE 65536
 struct lcrc_tscan_key {  // the metaindex key read_meta looks for: "filter" + the policy name

@@ -2514,8 +2514,10 @@ enum { TS_OK = 0, TS_CORRUPT = 1, TS_HOST = 2, TS_CAPACITY = 3 };
 enum { TSM_SHORT = 1, TSM_MAGIC = 2, TSM_VARINT = 3, TSM_CHECKSUM = 4, TSM_TYPE = 5, TSM_SMALL = 6, TSM_CONTENTS = 7 };
 
 // footer, index block header and (meta) the metaindex filter entry, by one thread; key: 256 B of LDS
+// idec / iopen: k_ts_open's decoded index and its verdict (nullptr when the scan has no LCRC_TSCAN_SNAPPY_INDEX)
 __device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_len, const lcrc_tscan_key& fkey,
-                              uint64_t seg_cap, uint8_t* __restrict__ key, bool meta, lcrc_tscan_dev& s) {
+                              uint64_t seg_cap, uint8_t* __restrict__ key, bool meta, const uint8_t* __restrict__ idec,
+                              const uint64_t* __restrict__ iopen, lcrc_tscan_dev& s) {
   s = {};
   if (file_len < 48) {
     s.status = TS_CORRUPT;
@@ -2544,17 +2546,31 @@ __device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_le
     return;
   }
   const uint8_t itype = file[s.idx_off + s.idx_size];
-  const uint64_t clen = s.idx_size;
+  const uint8_t* ic = file + s.idx_off;  // the index block's contents
+  uint64_t clen = s.idx_size;
   if (itype == 1) {
-    s.status = TS_HOST;  // a Snappy-framed index block: decoded on the host path
-    return;
+    // a Snappy-framed index block: its contents are what k_ts_open decoded, when it decoded them all; otherwise the
+    // host path decodes it (and gives the reference's message) -- after the workspace grows, when that was the reason
+    const uint64_t o0 = iopen ? iopen[0] : 0;
+    if (!(o0 & 2) || iopen[2] || iopen[1] > 0x7FFFFFFFull) {
+      if (o0 & 4) {
+        s.gate = 1;
+        s.need_out = iopen[1];
+      }
+      s.status = TS_HOST;
+      return;
+    }
+    s.idx_dec = 1;
+    ic = idec;
+    clen = iopen[1];
   }
+  s.idx_clen = clen;
   if (itype > 1) {
     s.pcode = TSM_TYPE;
   } else if (clen < 4) {
     s.pcode = TSM_SMALL;
   } else {
-    const uint32_t nres = load_le32(file + s.idx_off + clen - 4);
+    const uint32_t nres = load_le32(ic + clen - 4);
     if ((uint64_t)nres > (clen - 4) / 4) {
       s.pcode = TSM_CONTENTS;
     } else if (nres == 0 || (clen - 4) / nres > 4096) {
@@ -2684,7 +2700,8 @@ __global__ void __launch_bounds__(256) k_ts_index(const uint8_t* __restrict__ fi
                                                   const lcrc_tscan_key fkey, uint64_t seg_cap,
                                                   lcrc_tscan_dev* __restrict__ st, uint64_t* __restrict__ local_c,
                                                   uint64_t* __restrict__ local_f, uint64_t* __restrict__ part,
-                                                  uint32_t* __restrict__ zero, uint64_t nzero) {
+                                                  uint32_t* __restrict__ zero, uint64_t nzero,
+                                                  const uint8_t* __restrict__ idec, const uint64_t* __restrict__ iopen) {
   __shared__ uint8_t key[256];
   __shared__ uint64_t hdr[3], sa[4], sb[4];
   // the batch's mismatch bitmap starts at zero (no memset launch)
@@ -2692,15 +2709,15 @@ __global__ void __launch_bounds__(256) k_ts_index(const uint8_t* __restrict__ fi
     zero[i] = 0;
   if (threadIdx.x == 0) {
     lcrc_tscan_dev s;
-    ts_open_state(file, file_len, fkey, seg_cap, key, blockIdx.x == 0, s);
+    ts_open_state(file, file_len, fkey, seg_cap, key, blockIdx.x == 0, idec, iopen, s);
     if (blockIdx.x == 0) *st = s;
     hdr[0] = s.nres;  // 0 unless the index block can be walked (a later metaindex verdict changes nothing here)
-    hdr[1] = s.idx_off;
-    hdr[2] = s.idx_size;
+    hdr[1] = s.idx_dec ? ~0ull : s.idx_off;
+    hdr[2] = s.idx_clen;
   }
   __syncthreads();
   const uint64_t nres = hdr[0];
-  const uint8_t* d = file + hdr[1];
+  const uint8_t* d = hdr[1] == ~0ull ? idec : file + hdr[1];
   const uint32_t len = (uint32_t)hdr[2];
   for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
     const uint64_t i = t0 + threadIdx.x;
@@ -2731,10 +2748,12 @@ __global__ void __launch_bounds__(256) k_ts_index(const uint8_t* __restrict__ fi
 __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
                                                  lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ local_c,
                                                  const uint64_t* __restrict__ part, lcrc_tblk_dev* __restrict__ out,
-                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap, uint64_t vcap) {
+                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap, uint64_t vcap,
+                                                 const uint8_t* __restrict__ idec, uint64_t* __restrict__ iopen) {
   __shared__ uint64_t sa[4], sb[4];
   const uint32_t status = st->status;  // as k_ts_index left it
   const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  if (lead) iopen[2] = 0;  // k_ts_open's failure mark, read by k_ts_index: clear for the next scan
   if (status != TS_OK) {
     if (lead) st->n_total = 0;
     return;
@@ -2794,8 +2813,8 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     st->n_total = ntot;
     st->n_verify = ntot + (split ? npieces : 0);
   }
-  const uint8_t* d = file + st->idx_off;
-  const uint32_t len = (uint32_t)st->idx_size;
+  const uint8_t* d = st->idx_dec ? idec : file + st->idx_off;
+  const uint32_t len = (uint32_t)st->idx_clen;
   for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
     uint64_t base, bf;
     wg_sum_parts(part, 0, t0 / 256, sa, sb, base, bf);
@@ -2907,7 +2926,8 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
         b.status = c != load_le32(file + b.offset + b.size + 1);
       }
       if (b.status == 0 && b.type > 1) b.status = 4;  // LCRC_TBLK_BAD_TYPE
-      if (b.status == 0 && b.type == 1) flen = (uint32_t)b.size;
+      if (b.status == 0 && b.type == 1 && !(k == 2 && st->idx_dec)) flen = (uint32_t)b.size;  // (k_ts_open decoded
+      // and checked a Snappy-framed index already)
     }
     lcrc_desc_dev f;
     f.offset = flen ? b.offset : 0;
@@ -3174,7 +3194,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     chunks = xc;
   }
   const bool over = total > ts_out_cap;
-  if (t == 0 && threadIdx.x == 0) {
+  if (t == 0 && threadIdx.x == 0 && live) {
     st->need_out = total;
     st->need_chunks = chunks;
     st->gate = over ? 1u : chunks == 0 ? 2u : 0u;
@@ -3224,6 +3244,121 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     if (over && st->status == TS_OK) st->status = TS_HOST;
     ts_final(st, blk, n_out, status_out);
   }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// k_ts_open (lcrc_table_scan_async_ex with LCRC_TSCAN_SNAPPY_INDEX): the table scan's first launch when the table was
+// written with compression -- its index block is then usually a Snappy frame (table.rs:430, write_block keeps the
+// frame when it saves 12.5%) -- decodes that frame on the device, as Table::open's read_block_from_file does on the
+// host (format.rs:194-206), so that the index walk reads the decoded contents instead of handing the table to the host.
+// One wave per workgroup, the frame's data chunks dealt round-robin over the workgroups. A chunk is decoded in LDS (its
+// whole output: a copy may reach back anywhere in it), its masked CRC-32C computed there (td_chunk_crc), and copied out
+// to the decoded-index workspace; a chunk whose compressed bytes exceed the staging is decoded lane-serially in the
+// workspace and checksummed there. iopen[0]: 1 framed | 2 decoded (framing good, total within the workspace) | 4 over
+// the workspace; iopen[1]: the decoded length; iopen[2]: set by a chunk that does not decode or check (k_ts_emit
+// clears it). The index block's own checksum comes with the batch, as for a raw index; every verdict on the footer
+// and the handle is ts_open_state's.
+// ---------------------------------------------------------------------------------------------------
+constexpr uint32_t TO_IN = 32768 + 16;  // compressed bytes staged (+ the dword alignment)
+constexpr uint32_t TO_OUT = 65536;      // a whole chunk's output, V = 0^pad || M a multiple of 1 KiB
+constexpr uint32_t TO_LDS = TD_TAB_WORDS * 4 + TO_IN + SN_SLACK + TO_OUT;
+
+__global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file, uint64_t file_len,
+                                               const uint32_t* __restrict__ tab_c, uint8_t* __restrict__ idec,
+                                               uint64_t idec_cap, uint64_t* __restrict__ iopen) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t to_lds[];
+  uint32_t* const T = (uint32_t*)to_lds;
+  uint8_t* const lin = to_lds + TD_TAB_WORDS * 4;
+  uint8_t* const lout = lin + TO_IN + SN_SLACK;
+  const uint32_t lane = __lane_id();
+  // the footer's index handle, checked as ts_open_state checks it (all lanes alike)
+  uint64_t io = 0, is = 0;
+  bool framed = false;
+  if (file_len >= 48) {
+    const uint8_t* f = file + file_len - 48;
+    const uint64_t magic = (uint64_t)load_le32(f + 40) | ((uint64_t)load_le32(f + 44) << 32);
+    uint64_t mo, ms;
+    uint32_t p = magic == 0xdb4775248b80fb57ull ? dev_varint<64>(f, 0, 48, &mo) : ~0u;
+    if (p != ~0u) p = dev_varint<64>(f, p, 48, &ms);
+    if (p != ~0u) p = dev_varint<64>(f, p, 48, &io);
+    if (p != ~0u) p = dev_varint<64>(f, p, 48, &is);
+    framed = p != ~0u && io <= file_len && is + 5 <= file_len - io && is + 1 <= 0x7FFFFFFFull && file[io + is] == 1;
+  }
+  const uint8_t* const p = file + io;
+  const uint32_t len = (uint32_t)is;
+  uint64_t total = 0, chunks = 0, padded;
+  uint32_t mi, mo;
+  const bool ok = framed && snappy_frame_size(p, len, total, chunks, mi, mo, padded);
+  const bool fits = total <= idec_cap;
+  if (blockIdx.x == 0 && lane == 0) {
+    iopen[1] = ok ? total : 0;
+    iopen[0] = (framed ? 1u : 0u) | (ok && fits ? 2u : 0u) | (ok && !fits ? 4u : 0u);
+  }
+  if (!ok || !fits || blockIdx.x >= chunks) return;  // (uniform)
+  for (uint32_t i = lane; i < TD_TAB_WORDS / 4; i += 64) ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i];
+  __syncthreads();
+  bool good = true;
+  uint64_t o = 0, k = 0;
+  for (uint32_t at = 0; at < len;) {  // the framing is good (snappy_frame_size): headers and lengths in bounds
+    const uint32_t type = ld_u8(p + at);
+    const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
+    const uint32_t body = at + 4;
+    at = body + cl;
+    if (type > 1) continue;  // stream identifier, skippable chunks
+    uint32_t ulen = cl - 4, q = body + 4;
+    if (type == 0) {  // preamble = uncompressed length
+      ulen = 0;
+      for (uint32_t i = 0, sh = 0; i < 5 && q < at; ++i, sh += 7) {
+        const uint32_t b = ld_u8(p + q++);
+        ulen |= (b & 127u) << sh;
+        if (!(b & 128)) break;
+      }
+    }
+    const uint64_t oc = o;
+    o += ulen;
+    if (k++ % gridDim.x != blockIdx.x) continue;
+    const uint32_t want = ld_u8(p + body) | (ld_u8(p + body + 1) << 8) | (ld_u8(p + body + 2) << 16) |
+                          ((uint32_t)ld_u8(p + body + 3) << 24);
+    uint32_t crc;
+    bool cok = true;
+    if (type == 1) {  // uncompressed: checksummed where it lies, copied out
+      crc = td_chunk_crc<false>(T, p + q, ulen, lane);
+      for (uint32_t x = lane; x < ulen; x += 64) idec[oc + x] = p[q + x];
+    } else if (at - q + 4 <= TO_IN) {
+      const uint32_t pad = ((ulen + 1023) & ~1023u) - ulen;
+      for (uint32_t x = 16 * lane; x < pad; x += 1024) *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
+      const uint8_t* zs = p + q;
+      const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
+      const uint32_t* za = (const uint32_t*)(zs - d);
+      const uint32_t ndw = (d + (at - q) + 3) >> 2;
+      for (uint32_t x = lane; x < ndw; x += 64) ((uint32_t*)lin)[x] = za[x];
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      cok = snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane);
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      crc = cok ? td_chunk_crc<true>(T, lout, ulen, lane) : 0u;
+      if (cok) {
+        const uint8_t* src = lout + pad;
+        uint32_t x0 = 0;
+        if (((oc | pad) & 15) == 0) {  // whole 16 B pieces, then the tail byte by byte
+          x0 = ulen & ~15u;
+          for (uint32_t x = 16 * lane; x < x0; x += 1024) *(u32x4*)(idec + oc + x) = *(const u32x4*)(src + x);
+        }
+        for (uint32_t x = x0 + lane; x < ulen; x += 64) idec[oc + x] = src[x];
+      }
+    } else {  // too large for the staging: lane-serial in the workspace, checksummed there
+      uint64_t oo = oc;
+      if (lane == 0) cok = sn_serial_decode(p + q, p + at, idec, oo, oc + ulen);
+      cok = bcast(cok ? 1u : 0u) != 0;
+      __threadfence_block();
+      crc = cok ? td_chunk_crc<false>(T, idec + oc, ulen, lane) : 0u;
+    }
+    good = good && cok && mask32c(crc) == want;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();  // the staging is reused by the next chunk
+  }
+  if (!good && lane == 0) iopen[2] = 1;  // (every writer stores the same 1)
 }
 
 }  // namespace lcrc_dev
@@ -3374,18 +3509,29 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
 // gcap: the most workgroups (the rest of the tiles grid-stride)
 hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
                                 lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
-                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, hipStream_t s) {
+                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
+                                const uint64_t* iopen, hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
   LCRC_LAUNCH(lcrc_dev::k_ts_index, dim3((unsigned)(g < gcap ? g : gcap)), dim3(256), 0, s, file, file_len, *key, cap,
-              st, local_c, local_f, part, zero, nzero);
+              st, local_c, local_f, part, zero, nzero, idec, iopen);
+  return hipGetLastError();
+}
+// a Snappy-framed index block decoded into idec (k_ts_open); 64 one-wave workgroups
+hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uint32_t* tab_c, uint8_t* idec,
+                               uint64_t idec_cap, uint64_t* iopen, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_open,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::TO_LDS);
+  if (attr != hipSuccess) return attr;
+  LCRC_LAUNCH(lcrc_dev::k_ts_open, dim3(64), dim3(64), lcrc_dev::TO_LDS, s, file, file_len, tab_c, idec, idec_cap, iopen);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
                                const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t vcap, uint64_t bound, uint32_t gcap, hipStream_t s) {
+                               uint64_t vcap, uint64_t bound, uint32_t gcap, const uint8_t* idec, uint64_t* iopen,
+                               hipStream_t s) {
   const uint64_t g = bound / 256 + 1;
   LCRC_LAUNCH(lcrc_dev::k_ts_emit, dim3((unsigned)(g < gcap ? g : gcap)), dim3(256), 0, s, file, file_len, st,
-              local_c, part, out, descs, cap, vcap);
+              local_c, part, out, descs, cap, vcap, idec, iopen);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,

@@ -15,6 +15,13 @@ from test_table_scan import FILTER, _as_tuples, _handcrafted, _kvs
 OK, CORRUPT, HOST, CAPACITY = 0, 1, 2, 3
 
 
+def _seq_kvs(n, vlen=24, seed=5):
+    """db_bench-style sequential keys: the index block compresses, so a table written with compression=1 gets a
+    Snappy-framed index block (table.rs:430, write_block)."""
+    rng = np.random.default_rng(seed)
+    return [(b"%016d" % i, rng.integers(0, 256, vlen, dtype=np.uint8).tobytes()) for i in range(n)]
+
+
 class _Scan:
     """Device buffers for one async scan: the file, the result array, the count and the status words."""
 
@@ -27,8 +34,9 @@ class _Scan:
         self.count = lcrc.DeviceBuffer(8)
         self.status = lcrc.DeviceBuffer(8)
 
-    def run(self, eng, filter_name=None):
-        eng.table_scan_async(self.file, self.n, self.blocks, self.cap, self.count, self.status, filter_name)
+    def run(self, eng, filter_name=None, snappy_index=False):
+        eng.table_scan_async(self.file, self.n, self.blocks, self.cap, self.count, self.status, filter_name,
+                             snappy_index=snappy_index)
         eng.sync()
         return self.read()
 
@@ -43,13 +51,13 @@ class _Scan:
             b.close()
 
 
-def _expect_async(lcrc, eng, orc, f, filt=None, cap=None, decoded=1 << 22, mode=0, masked=False):
+def _expect_async(lcrc, eng, orc, f, filt=None, cap=None, decoded=1 << 22, mode=0, masked=False, snappy_index=False):
     """Run the async scan and compare with the oracle; returns the status."""
     want, werr = orc.table_scan_expect(f, filt, mode, masked)
     eng.table_scan_reserve(len(f), cap if cap is not None else 4096, decoded)
     s = _Scan(lcrc, f, cap if cap is not None else 4096)
     try:
-        st, code, n, got = s.run(eng, filt)
+        st, code, n, got = s.run(eng, filt, snappy_index)
         if st == OK:
             assert werr is None
             assert sorted(_as_tuples(got)) == want
@@ -310,3 +318,85 @@ def test_async_multi_chunk_frames(lcrc, orc, engines):
     g[off + n // 2] ^= 0x21  # inside a middle chunk's bytes
     g[off + n + 1:off + n + 5] = orc.crc(bytes(g[off:off + n + 1]), 0).to_bytes(4, "little")
     assert _expect_async(lcrc, engines[lcrc.MODE_REF], orc, bytes(g)) == OK
+
+
+def _index_block(f, blocks):
+    return [b for b in blocks if b[2] == 3][0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,block_size", [(3000, 4096), (6000, 256), (40000, 128)])
+@pytest.mark.parametrize("filt", [None, FILTER])
+def test_async_snappy_index(lcrc, orc, engines, n, block_size, filt):
+    """A table written with compression has a Snappy-framed index block (table.rs:430): without
+    LCRC_TSCAN_SNAPPY_INDEX the device walk hands it to the host; with it the index is decoded on the device
+    (k_ts_open: one chunk of the frame per workgroup; the 40000-key case has several 64 KiB chunks) and the scan is
+    the oracle's. The synchronous wrapper (which always sets the flag) agrees."""
+    f, blocks = orc.table_build(_seq_kvs(n), block_size=block_size, compression=1, filter_name=filt,
+                                filter_block=b"s" * 90)
+    off, size, _ = _index_block(f, blocks)
+    assert f[off + size] == 1  # the index block is a Snappy frame
+    if n == 40000:
+        assert len(orc.snappy_frame_decode(f[off:off + size])) > 3 * 65536
+    eng = engines[lcrc.MODE_REF]
+    assert _expect_async(lcrc, eng, orc, f, filt, cap=len(blocks) + 4) == HOST
+    assert _expect_async(lcrc, eng, orc, f, filt, cap=len(blocks) + 4, snappy_index=True) == OK
+    got, err = _sync(lcrc, eng, f, filt)
+    assert err is None and _as_tuples(got) == orc.table_scan_expect(f, filt)[0]
+    # the flag on a table whose index is stored raw: the same scan as without it
+    g, gb = orc.table_build(_kvs(2000, 3), block_size=1024, compression=1)
+    assert g[sum(_index_block(g, gb)[:2])] == 0
+    assert _expect_async(lcrc, eng, orc, g, cap=len(gb) + 4, snappy_index=True) == OK
+
+
+@pytest.mark.gpu
+def test_async_snappy_index_corruption(lcrc, orc, engines):
+    """A Snappy-framed index whose chunk does not decode or check (the block trailer re-sealed, so only the frame is
+    wrong), and one whose block checksum fails: the device says LCRC_TSCAN_HOST or the oracle's verdict, and the
+    synchronous scan gives the oracle's message in every case."""
+    f, blocks = orc.table_build(_seq_kvs(5000), block_size=512, compression=1)
+    off, size, _ = _index_block(f, blocks)
+    eng = engines[lcrc.MODE_REF]
+
+    def reseal(g):
+        g[off + size + 1:off + size + 5] = orc.crc(bytes(g[off:off + size + 1]), 0).to_bytes(4, "little")
+        return bytes(g)
+
+    cases = {}
+    g = bytearray(f)
+    g[off + 10 + 8 + 40] ^= 0x01  # inside the first chunk's compressed body
+    cases["chunk body"] = reseal(g)
+    g = bytearray(f)
+    g[off + 10 + 4] ^= 0x80  # the first chunk's stored masked CRC-32C
+    cases["chunk crc"] = reseal(g)
+    g = bytearray(f)
+    g[off + 1] = 0x07  # the stream identifier's length
+    cases["framing"] = reseal(g)
+    g = bytearray(f)
+    g[off + size // 2] ^= 0x04
+    cases["block crc"] = bytes(g)  # not resealed
+    for name, case in cases.items():
+        st = _expect_async(lcrc, eng, orc, case, snappy_index=True)
+        assert st in (HOST, CORRUPT), name
+        got, err = _sync(lcrc, eng, case, None)
+        want, werr = orc.table_scan_expect(case, None)
+        assert err == werr and (got is None or _as_tuples(got) == want), name
+    # the clean table after the failures: the failure mark does not stick
+    assert _expect_async(lcrc, eng, orc, f, snappy_index=True) == OK
+
+
+@pytest.mark.gpu
+def test_async_snappy_index_workspace(lcrc, orc):
+    """The decoded index takes the scan's decode workspace (lcrc_table_scan_reserve's decoded_cap): over it the scan
+    is LCRC_TSCAN_HOST, the synchronous wrapper grows the workspace and the next async scan decodes on the device."""
+    f, blocks = orc.table_build(_seq_kvs(8000), block_size=256, compression=1)
+    off, size, _ = _index_block(f, blocks)
+    assert f[off + size] == 1 and len(orc.snappy_frame_decode(f[off:off + size])) > 4096
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    try:
+        assert _expect_async(lcrc, eng, orc, f, cap=len(blocks) + 4, decoded=16, snappy_index=True) == HOST
+        got, err = _sync(lcrc, eng, f, None)
+        assert err is None and _as_tuples(got) == orc.table_scan_expect(f, None)[0]
+        assert _expect_async(lcrc, eng, orc, f, cap=len(blocks) + 4, decoded=0, snappy_index=True) == OK
+    finally:
+        eng.close()
