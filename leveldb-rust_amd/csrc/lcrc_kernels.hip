@@ -1793,12 +1793,19 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
 constexpr uint32_t SN_SLACK = 128;
 constexpr uint32_t SN_MAX = 16384;
 // k_ts_decode (the whole-table scan's decode): 8 waves per 256-block tile, each with this LDS staging
-constexpr uint32_t TD_WAVES = 8;
+#ifndef LCRC_TD_WAVES  // (measurement builds vary the staging: tools/probe/build_one.sh)
+#define LCRC_TD_WAVES 8
+#define LCRC_TD_IN 6144
+#define LCRC_TD_OUT 7168
+#endif
+constexpr uint32_t TD_WAVES = LCRC_TD_WAVES;
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
-constexpr uint32_t TD_IN = 6144 + 16;   // LDS staging per wave: compressed bytes (+ 4 for the tail dword)
-constexpr uint32_t TD_OUT = 7168;       // decoded bytes (a multiple of 1 KiB: V fits as is)
+constexpr uint32_t TD_IN = LCRC_TD_IN + 16;  // LDS staging per wave: compressed bytes (+ 4 for the tail dword)
+constexpr uint32_t TD_OUT = LCRC_TD_OUT;     // decoded bytes (a multiple of 1 KiB: V fits as is)
+static_assert(TD_OUT % 1024 == 0, "the chunk CRC reads V in whole 1 KiB passes");
 constexpr uint32_t TD_WAVE_LDS = TD_IN + SN_SLACK + TD_OUT;
 constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
+static_assert(TD_LDS <= 163840, "k_ts_decode's LDS");
 
 // `slow`: the decoded bytes (16-aligned) of the compressed chunks too large for k_ts_decode's LDS staging (TD_IN
 // compressed, TD_OUT decoded), which it decodes lane-serially into the table scan's workspace
