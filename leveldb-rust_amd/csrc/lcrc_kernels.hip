@@ -1794,9 +1794,9 @@ constexpr uint32_t SN_SLACK = 128;
 constexpr uint32_t SN_MAX = 16384;
 // k_ts_decode (the whole-table scan's decode): 8 waves per 256-block tile, each with this LDS staging
 #ifndef LCRC_TD_WAVES  // (measurement builds vary the staging: tools/probe/build_one.sh)
-#define LCRC_TD_WAVES 8
-#define LCRC_TD_IN 6144
-#define LCRC_TD_OUT 7168
+#define LCRC_TD_WAVES 12  // (8 waves with 6 + 7 KiB staging: 2.46 vs 2.09 ms per compressed 64K-block scan with 12)
+#define LCRC_TD_IN 4096
+#define LCRC_TD_OUT 6144
 #endif
 constexpr uint32_t TD_WAVES = LCRC_TD_WAVES;
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
