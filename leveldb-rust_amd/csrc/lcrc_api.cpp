@@ -210,7 +210,7 @@ struct lcrc_ctx {
   DevBuf<uint64_t> ts_count;
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
   void* ts_host = nullptr;              // pinned: the state read back by the synchronous wrapper
-  uint64_t ts_decoded_cap = 0, ts_chunk_cap = 0;
+  uint64_t ts_decoded_cap = 0;
   uint64_t ts_out_cap = 0;  // the decode workspace: ts_decoded_cap + the 16-alignment of its (large) chunks
   // lcrc_ctx_options (lcrc_ctx_create_ex; tests and measurement only -- the library reads no environment variable)
   uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (tests reach the tile loops with a small one)
@@ -1324,30 +1324,24 @@ const char* lcrc_table_scan_message(uint32_t code) {
   return code < sizeof(kTscanMsg) / sizeof(kTscanMsg[0]) ? kTscanMsg[code] : "";
 }
 
-static uint64_t ts_chunk_cap(size_t max_blocks, uint64_t decoded_cap) {
-  return 2ull * max_blocks + decoded_cap / 1024 + 64;
-}
-
 // the batched verify's descriptors: the blocks and the pieces of a long filter / metaindex / index block
 static uint64_t ts_verify_cap(size_t max_blocks, uint64_t file_len) {
   return max_blocks + 1 + file_len / LCRC_TS_PIECE + 3;
 }
 
-static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap, uint64_t chunks) {
+// the device-only scan's workspace (every buffer its launches touch; nothing else: the host-assisted scan and
+// lcrc_snappy_frames size their own)
+static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap) {
   int rc = set_device(ctx);
   if (rc) return rc;
   const uint64_t nb = max_blocks + 1;
   const uint64_t nv = ts_verify_cap(max_blocks, max_file_len);
-  const uint64_t cc = std::max<uint64_t>(std::max(ts_chunk_cap(max_blocks, decoded_cap), chunks), ctx->ts_chunk_cap);
   decoded_cap = std::max<uint64_t>(decoded_cap, ctx->ts_decoded_cap);
   if ((rc = ctx->ts_state.ensure(1)) || (rc = ctx->idx_count.ensure(nb)) || (rc = ctx->idx_flag.ensure(nb)) ||
-      (rc = ctx->idx_pos.ensure(nb)) || (rc = ctx->idx_fpos.ensure(nb)) || (rc = ctx->sn_part.ensure(2 * (nb / 256 + 2))) ||
-      (rc = ctx->tbl_descs.ensure(nv)) || (rc = ctx->tbl_crcs.ensure(nv)) || (rc = ctx->tbl_mm.ensure(nv / 32 + 1)) ||
-      (rc = ctx->tbl_frames.ensure(nb)) || (rc = ctx->sn_size.ensure(nb)) || (rc = ctx->sn_nch.ensure(nb)) ||
-      (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) || (rc = ctx->sn_status.ensure(nb)) ||
-      (rc = ctx->sn_max.ensure(2)) || (rc = ctx->sn_cdesc.ensure(cc)) || (rc = ctx->sn_cexp.ensure(cc)) ||
-      (rc = ctx->sn_cframe.ensure(cc)) || (rc = ctx->sn_ccrc.ensure(cc)) || (rc = ctx->sn_cmm.ensure(cc / 32 + 1)) ||
-      (rc = ctx->sn_out.ensure(decoded_cap + 16 * (decoded_cap / 4096 + 1) + 16)) ||
+      (rc = ctx->sn_part.ensure(2 * (nb / 256 + 2))) || (rc = ctx->tbl_descs.ensure(nv)) ||
+      (rc = ctx->tbl_crcs.ensure(nv)) || (rc = ctx->tbl_mm.ensure(nv / 32 + 1)) || (rc = ctx->tbl_frames.ensure(nb)) ||
+      (rc = ctx->sn_nch.ensure(nb)) || (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) ||
+      (rc = ctx->sn_status.ensure(nb)) || (rc = ctx->sn_out.ensure(decoded_cap + 16 * (decoded_cap / 4096 + 1) + 16)) ||
       (rc = ctx->win.ensure(window_words(max_file_len))) || (rc = ctx->ts_idx.ensure(decoded_cap)))
     return rc;
   if (!ctx->ts_open.p) {
@@ -1356,7 +1350,6 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
   }
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   ctx->ts_decoded_cap = decoded_cap;
-  ctx->ts_chunk_cap = cc;
   // the workspace holds only the chunks k_ts_decode cannot decode in LDS (over 4 KiB compressed or 6 KiB decoded),
   // each 16-aligned: a caller reserving the exact decoded total still scans on the device
   ctx->ts_out_cap = decoded_cap + 16 * (decoded_cap / 4096 + 1);
@@ -1365,7 +1358,7 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
 
 int lcrc_table_scan_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap) {
   if (!ctx) return LCRC_EINVAL;
-  return ts_reserve(ctx, max_file_len, max_blocks, decoded_cap, 0);
+  return ts_reserve(ctx, max_file_len, max_blocks, decoded_cap);
 }
 
 int lcrc_table_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const char* filter_name,
@@ -1390,7 +1383,7 @@ int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     key.len = (uint32_t)(nl + 6);
   }
   // workspace for this size (reserved beforehand, this allocates nothing: graph-capturable)
-  int rc = ts_reserve(ctx, file_len, max_blocks, 0, 0);
+  int rc = ts_reserve(ctx, file_len, max_blocks, 0);
   if (rc) return rc;
   hipStream_t st = pick_stream(ctx, stream);
   lcrc_tscan_dev* S = ctx->ts_state.p;
@@ -1486,7 +1479,7 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
       if (hs->status == 3) {  // capacity: grow to what the table needs and scan again
         cap = std::max<uint64_t>(hs->n_data + 16, cap * 2);
       } else if (hs->status == 2 && hs->gate == 1) {  // decoded frames or index over the workspace: grow it, scan again
-        rc = ts_reserve(ctx, file_len, cap, hs->need_out + hs->need_out / 4 + 4096, hs->need_chunks + 64);
+        rc = ts_reserve(ctx, file_len, cap, hs->need_out + hs->need_out / 4 + 4096);
         if (rc == LCRC_ENOMEM) {
           ran = false;
           break;
