@@ -571,6 +571,13 @@ def workload_table(m, synth, engs, rank, device, args):
     got = scanners[0].table_scan_into(dev, len(f), out)
     if got != len(blocks) or (out["status"][:got] != 0).any():
         raise RuntimeError("table bench: the sealed table does not scan clean")
+    # the CPU baseline's sample: every block the scan found, read_block_from_file with verify_checksum on the host
+    # (the trailer CRC, and for a compressed table each frame decoded and its chunk CRCs checked); the device's
+    # trailer CRCs of the same blocks are its cross-check
+    scanned = out[:got].copy()
+    host_file = np.asarray(f if isinstance(f, np.ndarray) else np.frombuffer(f, np.uint8))
+    sample = ("table", host_file if args.compression else dev.download(np.uint8, len(f)), scanned["offset"],
+              scanned["size"])
     cap = len(blocks) + 8
     res = [(m.DeviceBuffer(cap * m.TBLK_DTYPE.itemsize, device), m.DeviceBuffer(8, device), m.DeviceBuffer(8, device))
            for _ in scanners]
@@ -626,7 +633,7 @@ def workload_table(m, synth, engs, rank, device, args):
            "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else
            "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async",
            "snappy_index": bool(args.compression and framed[kinds == m.TBLK_INDEX].any())}
-    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, None, None,
+    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, sample, lambda: scanned["crc"].copy(),
                     per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si),
                     kernel_events=not (args.table_sync or args.graph))
 
@@ -745,9 +752,23 @@ def cpu_baseline(orc, m, sample, mode, seconds, device_crcs):
     kind, data = sample[0], sample[1]
     threads, affinity, quota = usable_cpus()
     algo = orc.ALGO_SSE42_C if mode == "c" else orc.ALGO_PCLMUL_REF
-    raw = kind == "ranges_raw"  # WAL records carry the raw (unmasked) crc
+    raw = kind in ("ranges_raw", "table")  # WAL records and table trailers carry the raw (unmasked) crc
+    label = f"{'snap SSE4.2 crc32c' if mode == 'c' else 'crc32fast PCLMULQDQ'} restated in oracle/"
 
-    if kind == "uniform":
+    if kind == "table":
+        # read_block_from_file over every block (format.rs:146-213): crc32fast trailers (the reference's), Snappy
+        # frames decoded and every chunk's masked CRC-32C checked (oracle/crc_oracle.c orc_table_blocks_mt)
+        offs, sizes = sample[2], sample[3]
+
+        def fn(t):
+            crcs_, st_, secs_ = orc.table_blocks_mt(data, offs, sizes, t)
+            if st_.any():
+                raise RuntimeError("cpu baseline: the host walk finds a bad block in the table the device scanned clean")
+            return crcs_, secs_
+        nbytes = int(np.asarray(sizes, np.uint64).sum()) + len(offs)
+        what = f"one whole-table scan ({len(offs)} blocks, {nbytes / 2 ** 20:.0f} MiB stored)"
+        label = "read_block_from_file restated in oracle/ (crc32fast PCLMULQDQ trailers, Snappy frames decoded, chunk crc32c)"
+    elif kind == "uniform":
         nblk, blen = sample[2], sample[3]
         fn = lambda t: orc.crc_uniform_mt(data, nblk, blen, blen, t, algo)  # noqa: E731
         nbytes = nblk * blen
@@ -782,8 +803,7 @@ def cpu_baseline(orc, m, sample, mode, seconds, device_crcs):
     return {"value": round(gib / total, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
             "single_thread": round(one * nbytes / 2 ** 30 / one_s, 2), "cpu_model": model,
             "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
-            "sample": f"{passes} passes over {what} ({gib:.1f} GiB), "
-                      f"{'snap SSE4.2 crc32c' if mode == 'c' else 'crc32fast PCLMULQDQ'} restated in oracle/, "
+            "sample": f"{passes} passes over {what} ({gib:.1f} GiB), {label}, "
                       f"{threads} threads (every usable CPU: affinity {affinity}, cgroup quota {quota})",
             "cpu_seconds": round(total * threads, 1), "matches_device": match}
 

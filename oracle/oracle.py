@@ -58,6 +58,8 @@ def lib():
     L.orc_crc_ranges_mt.argtypes = [ctypes.c_int, vp, vp, vp, sz, ctypes.c_int, vp]
     L.orc_splitmix_fill.restype = None
     L.orc_splitmix_fill.argtypes = [ctypes.c_uint64, vp, sz]
+    L.orc_table_blocks_mt.restype = ctypes.c_double
+    L.orc_table_blocks_mt.argtypes = [ctypes.c_int, vp, vp, vp, sz, ctypes.c_int, vp, vp]
     _L = L
     return L
 
@@ -128,6 +130,20 @@ def crc_ranges_mt(data, offsets, lengths, threads, algo):
     out = np.empty(len(offs), np.uint32)
     secs = lib().orc_crc_ranges_mt(algo, _p(a), _p(offs), _p(lens), len(offs), threads, _p(out))
     return out, secs
+
+
+def table_blocks_mt(data, offsets, sizes, threads, algo=None):
+    """read_block_from_file with verify_checksum over a table's blocks (format.rs:146-213), C restatement, threaded:
+    (trailer CRCs, status per block -- 0 ok, 1 checksum mismatch, 3 bad Snappy content, 4 bad type --, seconds).
+    algo: the trailers' CRC (default crc32fast, the reference's)."""
+    a = _arr(data)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+    out = np.zeros(len(offs), np.uint32)
+    st = np.zeros(len(offs), np.uint8)
+    secs = lib().orc_table_blocks_mt(ALGO_PCLMUL_REF if algo is None else algo, _p(a), _p(offs), _p(sizes), len(offs),
+                                     threads, _p(out), _p(st))
+    return out, st, secs
 
 
 def mask_array(crcs):

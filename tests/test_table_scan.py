@@ -464,3 +464,31 @@ def test_table_scan_long_filter_policy_name(lcrc, orc, engines, compression):
     assert err is None and werr is None
     assert _as_tuples(got) == want
     assert (got["kind"] == 1).sum() == 1
+
+
+def test_oracle_table_blocks_c_matches_python_walk(orc):
+    """The C restatement the bench times as the table scan's CPU baseline (orc_table_blocks_mt: trailer CRC, type
+    dispatch, Snappy frame decode and chunk CRCs, format.rs:146-213) gives the Python walk's verdict for every block of
+    a compressed table, clean and with corrupted trailers, frames and types, on 1 and 4 threads."""
+    f, blocks = orc.table_build(_kvs(3000, 17), block_size=1024, compression=1, filter_name=FILTER,
+                                filter_block=b"c" * 100)
+    g = bytearray(f)
+    data = [b for b in blocks if b[2] == 0]
+    comp = [b for b in data if g[b[0] + b[1]] == 1]
+    off, n, _ = data[3]
+    g[off + n // 2] ^= 0x01  # trailer mismatch
+    for off, n, _ in comp[5:7]:  # a frame that does not decode or check, trailer re-sealed
+        g[off + n - 2] ^= 0x40
+        g[off + n + 1:off + n + 5] = orc.crc(bytes(g[off:off + n + 1]), 0).to_bytes(4, "little")
+    off, n, _ = comp[9]
+    g[off + n] = 9  # bad type, re-sealed
+    g[off + n + 1:off + n + 5] = orc.crc(bytes(g[off:off + n + 1]), 0).to_bytes(4, "little")
+    for case in (f, bytes(g)):
+        want, err = orc.table_scan_expect(case, FILTER)
+        assert err is None
+        offs = [w[0] for w in want]
+        sizes = [w[1] for w in want]
+        for threads in (1, 4):
+            crcs, st, _ = orc.table_blocks_mt(case, offs, sizes, threads)
+            assert [(int(c), int(s)) for c, s in zip(crcs, st)] == [(w[5], w[4]) for w in want]
+    assert {w[4] for w in orc.table_scan_expect(bytes(g), FILTER)[0]} >= {0, 1, 3, 4}
