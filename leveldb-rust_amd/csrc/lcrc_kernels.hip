@@ -1793,17 +1793,20 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
 constexpr uint32_t SN_SLACK = 128;
 constexpr uint32_t SN_MAX = 16384;
 // k_ts_decode (the whole-table scan's decode): 8 waves per 256-block tile, each with this LDS staging
-#ifndef LCRC_TD_WAVES  // (measurement builds vary the staging: tools/probe/build_one.sh)
-#define LCRC_TD_WAVES 12  // (8 waves with 6 + 7 KiB staging: 2.46 vs 2.09 ms per compressed 64K-block scan with 12)
-#define LCRC_TD_IN 4096
-#define LCRC_TD_OUT 6144
-#endif
-constexpr uint32_t TD_WAVES = LCRC_TD_WAVES;
+// Each wave of k_ts_decode decodes four frames at once, one per 16-lane row (row staging: the whole frame, TR_IN
+// bytes, and one decoded chunk, TR_OUT); a frame that does not fit goes through the whole wave (the wave decoder, its
+// staging TD_IN + TD_OUT made of the wave's four row areas); a chunk too large for that, lane-serially to the workspace.
+constexpr uint32_t TD_WAVES = 4;
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
-constexpr uint32_t TD_IN = LCRC_TD_IN + 16;  // LDS staging per wave: compressed bytes (+ 4 for the tail dword)
-constexpr uint32_t TD_OUT = LCRC_TD_OUT;     // decoded bytes (a multiple of 1 KiB: V fits as is)
+constexpr uint32_t TR_IN = 3072 + 16;    // a row's frame (+ the slack of its element-header reads)
+constexpr uint32_t TR_OUT = 4608;        // a row's decoded chunk (V: a multiple of 256 B)
+constexpr uint32_t TR_ROW_LDS = TR_IN + 16 + TR_OUT;
+constexpr uint32_t TD_WAVE_LDS = 4 * TR_ROW_LDS;
+constexpr uint32_t TD_IN = 12288 + 16;   // the whole wave's staging: compressed bytes (+ 4 for the tail dword)
+constexpr uint32_t TD_OUT = 16384;       // decoded bytes (a multiple of 1 KiB: V fits as is)
 static_assert(TD_OUT % 1024 == 0, "the chunk CRC reads V in whole 1 KiB passes");
-constexpr uint32_t TD_WAVE_LDS = TD_IN + SN_SLACK + TD_OUT;
+static_assert(TR_OUT % 256 == 0 && TR_ROW_LDS % 16 == 0, "row staging");
+static_assert(TD_IN + SN_SLACK + TD_OUT <= TD_WAVE_LDS, "the wave staging is the wave's row areas");
 constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
 static_assert(TD_LDS <= 163840, "k_ts_decode's LDS");
 
@@ -3162,6 +3165,162 @@ __device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint
   return ok;
 }
 
+// ---- four frames per wave: one per 16-lane row (lane g = lane & 15 of row lane >> 4) ----
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
+
+// One Snappy chunk per row: the elements in[q, qe) decoded into o[0, ulen) (both the row's LDS staging). Every row
+// walks its own chain -- one element per iteration, its header a broadcast read of the row's staging -- and executes
+// it 16 bytes per lane pass (all of an element's reads before its writes: a literal's bytes, or earlier output; a copy
+// shorter-offset than it is long repeats its last `a` bytes, j mod a). Validation as the wave decoder's. Rows with
+// active = false only ride along. Returns the row's verdict (output ends exactly at ulen).
+__device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, uint32_t qe, lds_u8* o, uint32_t ulen,
+                                                  bool active, uint32_t g) {
+  uint32_t w = 0;
+  bool ok = true;
+  while (true) {
+    const bool live = active && ok && q < qe;
+    if (!__builtin_amdgcn_ballot_w64(live)) break;
+    const uint32_t qq = live ? q : 0u;
+    const uint32_t ba = qq & ~3u;
+    const uint32_t d0 = *(lds_cu32*)(in + ba), d1 = *(lds_cu32*)(in + ba + 4);
+    const uint64_t x = (((uint64_t)d1 << 32) | d0) >> (8 * (qq & 3));
+    const uint32_t t = (uint32_t)x & 0xFFu, ext = (uint32_t)(x >> 8);
+    const uint32_t typ = t & 3, room = live ? qe - q : 0u;
+    uint32_t hdr, outlen, a;
+    bool good;
+    if (typ == 0) {
+      const uint32_t L = t >> 2;
+      const uint32_t nb = L >= 60 ? L - 59 : 0;
+      const uint32_t lm1 = nb ? (nb == 4 ? ext : ext & ((1u << (8 * nb)) - 1)) : L;
+      hdr = 1 + nb;
+      outlen = lm1 + 1;
+      a = qq + hdr;
+      good = room >= hdr && lm1 < room - hdr;  // the literal's bytes inside the input (no u32 wrap)
+    } else {
+      hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
+      outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
+      a = typ == 1 ? ((t >> 5) << 8) | (ext & 0xFFu) : typ == 2 ? (ext & 0xFFFFu) : ext;
+      good = room >= hdr;
+    }
+    const bool bad = live && (!good || w > ulen || outlen > ulen - w || (typ != 0 && (a == 0 || a > w)));
+    if (bad) ok = false;
+    const bool ex = live && !bad;
+    const uint32_t n = ex ? outlen : 0u;
+    const bool fin = typ == 0;
+    const uint32_t per = (!fin && a < outlen) ? a : 0u;
+    const uint32_t sa = fin ? a : w - a;
+    for (uint32_t b0 = 0; __builtin_amdgcn_ballot_w64(b0 < n); b0 += 64) {  // 64 bytes: four passes, reads first
+      uint32_t v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t j = b0 + 16 * i + g;
+        const uint32_t idx = j < n ? sa + (per ? small_mod(j, per) : j) : 0u;  // (per: a copy, n <= 64)
+        v[i] = fin ? in[idx] : o[idx];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t j = b0 + 16 * i + g;
+        if (j < n) o[w + j] = (uint8_t)v[i];
+      }
+    }
+    if (ex) {
+      q += fin ? hdr + outlen : hdr;
+      w += outlen;
+    }
+  }
+  return ok && w == ulen;
+}
+
+// The CRC-32C of V[pad, pad + len) per row, V = o[0, 256 np) with o[0, pad) zero (pad = 256 np - len): per 256 B
+// pass each lane walks 16 B (slice-by-4), the row tree joins them (Z16..Z128), the passes chain with Z256; the init
+// register is injected into the first min(4, len) bytes (td_chunk_crc's scheme on 16 lanes).
+__device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, uint32_t len, bool active,
+                                                  uint32_t g, uint32_t lane) {
+  const uint32_t np = active ? (len + 255) >> 8 : 0u, pad = (np << 8) - len, q4 = len < 4 ? len : 4u;
+  uint32_t acc = 0;
+  for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
+    const bool on = k < np;
+    const uint32_t x0 = 256 * k + 16 * g;
+    u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
+    w = td_inject(w, x0, pad, q4);
+    uint32_t cv = step4(T, 0u, w.x);
+    cv = step4(T, cv, w.y);
+    cv = step4(T, cv, w.z);
+    cv = step4(T, cv, w.w);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint32_t pn = row_down(cv, m);
+      if ((g & ((2u << m) - 1)) == 0) cv = zl(T, TAB_ZPIECE + m * 1024, cv) ^ pn;
+    }
+    const uint32_t pass = row_bcast0(cv, lane);
+    if (on) acc = k ? zl(T, TAB_ZWIN, acc) ^ pass : pass;
+  }
+  if (len < 4) acc ^= len ? 0xFFFFFFFFu >> (8 * len) : 0xFFFFFFFFu;
+  return acc ^ 0xFFFFFFFFu;
+}
+
+// One frame per row (p[0, len) in the file; `elig` rows only): staged whole into the row's input area, its chunks
+// walked there, each data chunk decoded (or, uncompressed, copied) into the row's output area and checksummed. Returns
+// 0 good, 1 bad, 2 deferred to the whole wave (a chunk larger than the row staging).
+__device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bool elig, const uint32_t* T, lds_u8* in,
+                                              lds_u8* o, uint32_t g, uint32_t lane) {
+  const uint32_t d = elig ? (uint32_t)((uintptr_t)p & 3) : 0u;
+  const uint32_t* za = (const uint32_t*)(p - d);
+  const uint32_t ndw = elig ? (d + len + 3) >> 2 : 0u;
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  for (uint32_t k = g; k < ndw; k += 16) ((lds_u32*)in)[k] = za[k];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  // the framing was validated by k_ts_finish: headers and lengths are in bounds, preambles are sane
+  uint32_t pos = d, res = 0;
+  const uint32_t end = d + (elig ? len : 0u);
+  while (true) {
+    bool have = false;
+    uint32_t type = 0, cl = 0;
+    while (elig && res == 0 && pos < end) {  // the next data chunk (stream identifier, skippable chunks passed)
+      type = in[pos];
+      cl = in[pos + 1] | ((uint32_t)in[pos + 2] << 8) | ((uint32_t)in[pos + 3] << 16);
+      if (type <= 1) {
+        have = true;
+        break;
+      }
+      pos += 4 + cl;
+    }
+    if (!__builtin_amdgcn_ballot_w64(have)) break;
+    const uint32_t body = pos + 4, next = body + cl;
+    uint32_t want = 0, ulen = 0, q = body + 4;
+    if (have) {
+      want = in[body] | ((uint32_t)in[body + 1] << 8) | ((uint32_t)in[body + 2] << 16) | ((uint32_t)in[body + 3] << 24);
+      if (type == 1) {
+        ulen = cl - 4;
+      } else {
+        for (uint32_t i = 0, sh = 0; i < 5 && q < next; ++i, sh += 7) {  // preamble = uncompressed length
+          const uint32_t b = in[q++];
+          ulen |= (b & 127u) << sh;
+          if (!(b & 128)) break;
+        }
+      }
+      if (ulen > TR_OUT) {
+        res = 2;  // too large for the row: the whole wave decodes this frame
+        have = false;
+      }
+    }
+    const uint32_t pad = have ? ((ulen + 255) & ~255u) - ulen : 0u;
+    for (uint32_t k = 16 * g; k < pad; k += 256) *(__attribute__((address_space(3))) u32x4*)(o + k) = u32x4{0, 0, 0, 0};
+    bool ok = true;
+    if (__builtin_amdgcn_ballot_w64(have && type == 1))  // uncompressed: copied to V + pad
+      for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += 16) o[pad + k] = in[q + k];
+    ok = row_snappy_decode(in, q, next, o + pad, ulen, have && type == 0, g) || !(have && type == 0);
+    const uint32_t crc = row_chunk_crc(T, o, ulen, have, g, lane);
+    if (have) {
+      if (!ok || mask32c(crc) != want) res = 1;
+      pos = next;
+    }
+  }
+  return res;
+}
+
 __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __restrict__ file,
                                                             const lcrc_desc_dev* __restrict__ frames,
                                                             const uint64_t* __restrict__ out_off, uint8_t* __restrict__ out,
@@ -3215,12 +3374,31 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   if (dec) {
     uint8_t* const lin = td_lds + TD_TAB_WORDS * 4 + wv * TD_WAVE_LDS;
     uint8_t* const lout = lin + TD_IN + SN_SLACK;
-    // this tile's frames (the last three blocks excluded), then the last workgroup's wave 0 the last three
+    // this tile's frames (the last three blocks excluded): four per wave at a time, one per row; a frame the row
+    // staging cannot hold (bad[] = 2) then through the whole wave; then the last workgroup's wave 0 the last three
     const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
-    for (uint64_t f = lo + wv; f < hi; f += TD_WAVES)
-      if (frames[f].length && !fstatus[f] &&
-          !td_frame(file + frames[f].offset, frames[f].length, T, lin, lout, out, out_off[f] + before, lane) && lane == 0)
-        bad[f - lo] = 1;
+    const uint32_t r = lane >> 4, g = lane & 15;
+    lds_u8* const rin = (lds_u8*)(lin + r * TR_ROW_LDS);
+    lds_u8* const rout = rin + TR_IN + 16;
+    for (uint64_t f0 = lo + 4 * wv; f0 < hi; f0 += 4 * TD_WAVES) {
+      const uint64_t f = f0 + r;
+      const bool valid = f < hi;
+      const uint32_t len = valid ? frames[f].length : 0u;
+      const bool live = len && !fstatus[f];
+      const bool elig = live && len + 3 <= TR_IN - 16;
+      const uint32_t v = row_frame(file + (valid ? frames[f].offset : 0), len, elig, T, rin, rout, g, lane);
+      if (live && g == 0) bad[f - lo] = elig ? (uint8_t)v : 2;
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();  // (the next round overwrites the row staging)
+    }
+    for (uint64_t f0 = lo + 4 * wv; f0 < hi; f0 += 4 * TD_WAVES)
+      for (uint64_t f = f0; f < f0 + 4 && f < hi; ++f)
+        if (bad[f - lo] == 2) {
+          const bool ok = td_frame(file + frames[f].offset, frames[f].length, T, lin, lout, out, out_off[f] + before, lane);
+          __builtin_amdgcn_s_waitcnt(0);
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) bad[f - lo] = ok ? 0 : 1;
+        }
     if (last && wv == 0)
       for (uint64_t f = tail; f < n; ++f) {
         const uint64_t tb = (f / 256 == t) ? before : 0;  // (a frame among the last three in an earlier tile: its
