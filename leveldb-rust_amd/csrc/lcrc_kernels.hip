@@ -2055,6 +2055,28 @@ __device__ __forceinline__ uint32_t small_mod(uint32_t x, uint32_t a) {
 }
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+// ndw dwords from global za (4-byte aligned) to LDS dst (16-byte aligned) by nl lanes (li: the lane's index among
+// them): whole 16 B units, eight per lane loaded before any is stored -- one memory latency per group, not one per
+// dword as a plain copy loop waits -- then the last 0..3 dwords (no read beyond the dword holding the last byte)
+__device__ __forceinline__ void stage_to_lds(const uint32_t* za, lds_u8* dst, uint32_t ndw, uint32_t li, uint32_t nl) {
+  typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
+  typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+  const uint32_t units = ndw >> 2;
+  for (uint32_t b = 0; b < units; b += 8 * nl) {
+    u32x4 t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t u = b + li + nl * i;
+      if (u < units) t[i] = *(const u32x4_ua*)(za + 4 * u);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t u = b + li + nl * i;
+      if (u < units) *(lds_u32x4_t*)(dst + 16 * u) = t[i];
+    }
+  }
+  if (li < (ndw & 3)) ((lds_u32_t*)dst)[4 * units + li] = za[4 * units + li];
+}
 __device__ bool snappy_wave_decode(const uint8_t* in_g, uint32_t q, uint32_t qe, uint8_t* o_g, uint32_t ulen,
                                    uint32_t lane) {
   // both staging buffers are LDS: say so, so that every access is a ds_ op (a generic pointer picked between them at
@@ -2293,7 +2315,7 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
           const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
           const uint32_t* za = (const uint32_t*)(zs - d);
           const uint32_t ndw = (d + (at - q) + 3) >> 2;
-          for (uint32_t k = lane; k < ndw; k += 64) ((uint32_t*)lin)[k] = za[k];
+          stage_to_lds(za, (lds_u8*)lin, ndw, lane, 64);
           __builtin_amdgcn_s_waitcnt(0);
           __builtin_amdgcn_wave_barrier();
           ok = snappy_wave_decode(lin, d, d + (at - q), lout, ulen, lane);
@@ -3144,7 +3166,7 @@ __device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint
         const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
         const uint32_t* za = (const uint32_t*)(zs - d);
         const uint32_t ndw = (d + (at - q) + 3) >> 2;
-        for (uint32_t k = lane; k < ndw; k += 64) ((uint32_t*)lin)[k] = za[k];
+        stage_to_lds(za, (lds_u8*)lin, ndw, lane, 64);
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
         ok = snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane);
@@ -3268,8 +3290,7 @@ __device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bo
   const uint32_t d = elig ? (uint32_t)((uintptr_t)p & 3) : 0u;
   const uint32_t* za = (const uint32_t*)(p - d);
   const uint32_t ndw = elig ? (d + len + 3) >> 2 : 0u;
-  typedef __attribute__((address_space(3))) uint32_t lds_u32;
-  for (uint32_t k = g; k < ndw; k += 16) ((lds_u32*)in)[k] = za[k];
+  stage_to_lds(za, in, ndw, g, 16);
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
   // the framing was validated by k_ts_finish: headers and lengths are in bounds, preambles are sane
@@ -3516,7 +3537,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
       const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
       const uint32_t* za = (const uint32_t*)(zs - d);
       const uint32_t ndw = (d + (at - q) + 3) >> 2;
-      for (uint32_t x = lane; x < ndw; x += 64) ((uint32_t*)lin)[x] = za[x];
+      stage_to_lds(za, (lds_u8*)lin, ndw, lane, 64);
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
       cok = snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane);
