@@ -3200,13 +3200,19 @@ __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, 
                                                   bool active, uint32_t g) {
   uint32_t w = 0;
   bool ok = true;
+  // an element's header (5 bytes from in[q]): two dword reads; the next element's is issued before this one's bytes
+  // are moved (its position is known once this header is decoded; the input is never written), so the chain pays one
+  // LDS latency per element instead of two
+  auto header = [&](uint32_t at) {
+    const uint32_t ba = at & ~3u;
+    const uint32_t d0 = *(lds_cu32*)(in + ba), d1 = *(lds_cu32*)(in + ba + 4);
+    return (((uint64_t)d1 << 32) | d0) >> (8 * (at & 3));
+  };
+  uint64_t x = header(active && q < qe ? q : 0u);
   while (true) {
     const bool live = active && ok && q < qe;
     if (!__builtin_amdgcn_ballot_w64(live)) break;
     const uint32_t qq = live ? q : 0u;
-    const uint32_t ba = qq & ~3u;
-    const uint32_t d0 = *(lds_cu32*)(in + ba), d1 = *(lds_cu32*)(in + ba + 4);
-    const uint64_t x = (((uint64_t)d1 << 32) | d0) >> (8 * (qq & 3));
     const uint32_t t = (uint32_t)x & 0xFFu, ext = (uint32_t)(x >> 8);
     const uint32_t typ = t & 3, room = live ? qe - q : 0u;
     uint32_t hdr, outlen, a;
@@ -3232,6 +3238,8 @@ __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, 
     const bool fin = typ == 0;
     const uint32_t per = (!fin && a < outlen) ? a : 0u;
     const uint32_t sa = fin ? a : w - a;
+    const uint32_t qn = ex ? q + (fin ? hdr + outlen : hdr) : q;
+    x = header(qn < qe ? qn : 0u);
     for (uint32_t b0 = 0; __builtin_amdgcn_ballot_w64(b0 < n); b0 += 64) {  // 64 bytes: four passes, reads first
       uint32_t v[4];
 #pragma unroll
@@ -3246,10 +3254,8 @@ __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, 
         if (j < n) o[w + j] = (uint8_t)v[i];
       }
     }
-    if (ex) {
-      q += fin ? hdr + outlen : hdr;
-      w += outlen;
-    }
+    q = qn;
+    w += n;
   }
   return ok && w == ulen;
 }
