@@ -400,3 +400,26 @@ def test_async_snappy_index_workspace(lcrc, orc):
         assert _expect_async(lcrc, eng, orc, f, cap=len(blocks) + 4, decoded=0, snappy_index=True) == OK
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_async_snappy_index_uncompressed_chunk(lcrc, orc, engines):
+    """A framed index whose only chunk is stored uncompressed (type 1: framing saved nothing on a tiny index): decoded
+    on the device with LCRC_TSCAN_SNAPPY_INDEX -- the chunk checksummed where it lies and copied out -- and the scan is
+    the oracle's; with the chunk's stored CRC broken the device hands the table to the host walk, whose message is
+    the oracle's."""
+    v = orc.varint
+    f = _handcrafted(orc, [(b"a", v(0) + v(100))], index_type=1)
+    want, werr = orc.table_scan_expect(f)
+    assert werr is None
+    eng = engines[lcrc.MODE_REF]
+    assert _expect_async(lcrc, eng, orc, f, snappy_index=True) == OK
+    ih = [w for w in want if w[2] == 3][0]
+    off, size = ih[0], ih[1]
+    assert f[off + size] == 1 and f[off + 10] == 1  # the frame's data chunk is type 1
+    g = bytearray(f)
+    g[off + 14] ^= 0x01  # the chunk's masked CRC-32C
+    g[off + size + 1:off + size + 5] = orc.crc(bytes(g[off:off + size + 1]), 0).to_bytes(4, "little")
+    assert _expect_async(lcrc, eng, orc, bytes(g), snappy_index=True) in (HOST, CORRUPT)
+    got, err = _sync(lcrc, eng, bytes(g), None)
+    assert err == orc.table_scan_expect(bytes(g))[1]
