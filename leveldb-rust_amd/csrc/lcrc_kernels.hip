@@ -3240,12 +3240,16 @@ __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, 
     const uint32_t sa = fin ? a : w - a;
     const uint32_t qn = ex ? q + (fin ? hdr + outlen : hdr) : q;
     x = header(qn < qe ? qn : 0u);
+    // (the pattern modulus only when some row copies a pattern: most iterations skip its VALU work)
+    const bool any_per = __builtin_amdgcn_ballot_w64(per != 0) != 0;
     for (uint32_t b0 = 0; __builtin_amdgcn_ballot_w64(b0 < n); b0 += 64) {  // 64 bytes: four passes, reads first
       uint32_t v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t j = b0 + 16 * i + g;
-        const uint32_t idx = j < n ? sa + (per ? small_mod(j, per) : j) : 0u;  // (per: a copy, n <= 64)
+        uint32_t jj = j;
+        if (any_per) jj = per ? small_mod(j, per) : j;  // (per: a copy, n <= 64)
+        const uint32_t idx = j < n ? sa + jj : 0u;
         v[i] = fin ? in[idx] : o[idx];
       }
 #pragma unroll
