@@ -3197,7 +3197,7 @@ typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 // shorter-offset than it is long repeats its last `a` bytes, j mod a). Validation as the wave decoder's. Rows with
 // active = false only ride along. Returns the row's verdict (output ends exactly at ulen).
 __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, uint32_t qe, lds_u8* o, uint32_t ulen,
-                                                  bool active, uint32_t g) {
+                                                  bool active, uint32_t g, lds_u8* dump) {
   uint32_t w = 0;
   bool ok = true;
   // an element's header (5 bytes from in[q]): two dword reads; the next element's is issued before this one's bytes
@@ -3250,12 +3250,15 @@ __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, 
         uint32_t jj = j;
         if (any_per) jj = per ? small_mod(j, per) : j;  // (per: a copy, n <= 64)
         const uint32_t idx = j < n ? sa + jj : 0u;
-        v[i] = fin ? in[idx] : o[idx];
+        v[i] = (fin ? in : (const lds_u8*)o)[idx];  // one read from whichever area holds the bytes
       }
+      // every lane stores (no exec-mask juggling): the lanes past the element into the slack byte after the row's
+      // input, which only ever feeds header reads past the input's end (never used)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t j = b0 + 16 * i + g;
-        if (j < n) o[w + j] = (uint8_t)v[i];
+        lds_u8* const dst = j < n ? o + w + j : dump;
+        *dst = (uint8_t)v[i];
       }
     }
     q = qn;
@@ -3342,7 +3345,8 @@ __device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bo
     bool ok = true;
     if (__builtin_amdgcn_ballot_w64(have && type == 1))  // uncompressed: copied to V + pad
       for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += 16) o[pad + k] = in[q + k];
-    ok = row_snappy_decode(in, q, next, o + pad, ulen, have && type == 0, g) || !(have && type == 0);
+    ok = row_snappy_decode(in, q, next, o + pad, ulen, have && type == 0, g, (lds_u8*)in + TR_IN + 15) ||
+         !(have && type == 0);
     const uint32_t crc = row_chunk_crc(T, o, ulen, have, g, lane);
     if (have) {
       if (!ok || mask32c(crc) != want) res = 1;
