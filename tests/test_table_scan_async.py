@@ -423,3 +423,47 @@ def test_async_snappy_index_uncompressed_chunk(lcrc, orc, engines):
     assert _expect_async(lcrc, eng, orc, bytes(g), snappy_index=True) in (HOST, CORRUPT)
     got, err = _sync(lcrc, eng, bytes(g), None)
     assert err == orc.table_scan_expect(bytes(g))[1]
+
+
+@pytest.mark.gpu
+def test_async_snappy_index_graph_replay(lcrc, orc):
+    """The seven-launch scan of a table with a Snappy-framed index (LCRC_TSCAN_SNAPPY_INDEX) captured in one HIP graph
+    after lcrc_table_scan_reserve and replayed: the oracle's blocks each time, and after the file's index frame is
+    corrupted in place (same buffers, trailer re-sealed) the replay hands the table to the host walk, and a replay of
+    the restored file is clean again (k_ts_open's failure mark does not stick across replays)."""
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    f, blocks = orc.table_build(_seq_kvs(6000), block_size=512, compression=1)
+    off, size, _ = _index_block(f, blocks)
+    assert f[off + size] == 1
+    want, _ = orc.table_scan_expect(f)
+    cap = len(blocks) + 8
+    eng.table_scan_reserve(len(f), cap, 1 << 22)
+    s = _Scan(lcrc, f, cap)
+    g = None
+    try:
+        g = eng.graph_capture(lambda: eng.table_scan_async(s.file, s.n, s.blocks, s.cap, s.count, s.status,
+                                                           snappy_index=True))
+        for _ in range(2):
+            s.blocks.zero()
+            s.count.zero()
+            eng.graph_launch(g)
+            eng.sync()
+            st, _, n, got = s.read()
+            assert st == OK and sorted(_as_tuples(got)) == want
+        bad = bytearray(f)
+        bad[off + 10 + 8 + 30] ^= 0x01  # inside the first chunk's compressed body
+        bad[off + size + 1:off + size + 5] = orc.crc(bytes(bad[off:off + size + 1]), 0).to_bytes(4, "little")
+        s.file.upload(np.frombuffer(bytes(bad), np.uint8))
+        eng.graph_launch(g)
+        eng.sync()
+        assert s.read()[0] == HOST
+        s.file.upload(np.frombuffer(f, np.uint8))
+        eng.graph_launch(g)
+        eng.sync()
+        st, _, n, got = s.read()
+        assert st == OK and sorted(_as_tuples(got)) == want
+    finally:
+        if g is not None:
+            eng.graph_destroy(g)
+        s.close()
+        eng.close()
