@@ -1350,7 +1350,7 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
   }
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   ctx->ts_decoded_cap = decoded_cap;
-  // the workspace holds only the chunks k_ts_decode cannot decode in LDS (over 4 KiB compressed or 6 KiB decoded),
+  // the workspace holds only the chunks k_ts_decode cannot decode in LDS (over 12 KiB compressed or 16 KiB decoded),
   // each 16-aligned: a caller reserving the exact decoded total still scans on the device
   ctx->ts_out_cap = decoded_cap + 16 * (decoded_cap / 4096 + 1);
   return LCRC_OK;

@@ -1792,7 +1792,7 @@ __device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32
 // bytes, each at most SN_MAX (k_snappy_decode_wave sizes them from the batch's largest chunk)
 constexpr uint32_t SN_SLACK = 128;
 constexpr uint32_t SN_MAX = 16384;
-// k_ts_decode (the whole-table scan's decode): 8 waves per 256-block tile, each with this LDS staging
+// k_ts_decode (the whole-table scan's decode): TD_WAVES waves per 256-block tile, each with this LDS staging
 // Each wave of k_ts_decode decodes four frames at once, one per 16-lane row (row staging: the whole frame, TR_IN
 // bytes, and one decoded chunk, TR_OUT); a frame that does not fit goes through the whole wave (the wave decoder, its
 // staging TD_IN + TD_OUT made of the wave's four row areas); a chunk too large for that, lane-serially to the workspace.
@@ -3069,7 +3069,9 @@ __global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, u
 //
 // One workgroup of TD_WAVES waves per 256-block tile of k_ts_finish (its in-tile scans of the frames' padded decoded
 // sizes give each frame's global-memory workspace for the lane-serial path; the workgroup adds the tiles before its
-// own once). The last three blocks (filter, metaindex, index: whatever ts_final may move) are the last tile's.
+// own once). A wave decodes four frames at a time, one per 16-lane row (row_frame); a frame the row staging cannot
+// hold goes through the whole wave (td_frame). The last three blocks (filter, metaindex, index: whatever ts_final may
+// move) are the last tile's.
 //
 // Chunk CRC (td_chunk_crc): the chunk M is read as V = 0^pad || M, |V| = 1024 np (leading zeros walked from register
 // 0 stay 0, so walk(0, V) = walk(0, M)); per 1 KiB pass each lane walks 16 B (slice-by-4), the 16-lane rows join with
