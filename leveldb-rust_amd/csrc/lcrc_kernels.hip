@@ -3468,6 +3468,119 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   }
 }
 
+#ifndef LCRC_TO_TWO_PHASE  // k_ts_open's index chunks through the two-phase decoder (0: the wave decoder)
+#define LCRC_TO_TWO_PHASE 1
+#endif
+// Two-phase decode of one chunk (k_ts_open's index chunks: tens of short elements per window, each key a copy of the
+// last): phase 1 walks the element chain as the wave decoder does (64 candidate starts per window, the chain by
+// v_readlane, the same validation) but only RECORDS the elements -- ea[k] = out position | (length - 1) << 16, eb[k] =
+// literal input position | 1 << 31 or copy offset -- and marks each start in a bitmap over the output. Phase 2 writes
+// the output 64 bytes at a time, one byte per lane: the lane's element is the previous block's last element plus the
+// starts at or below it in this block (a popcount of the bitmap word), its source a literal's input byte or an
+// earlier output byte; a source inside the same 64 bytes (not yet written) is chased by pointer jumping
+// (ds_bpermute, at most six rounds: every source lies before its byte). No batch selection and no element-by-element
+// round trips. Returns 1 decoded, 0 malformed, 2 more elements than ecap (the caller decodes with the wave decoder).
+__device__ uint32_t snappy_two_phase(const uint8_t* in_g, uint32_t q, uint32_t qe, uint8_t* o_g, uint32_t ulen,
+                                     uint32_t* ea_g, uint32_t* eb_g, uint32_t ecap, uint32_t* bm_g, uint32_t lane) {
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  const lds_u8* const in = (const lds_u8*)in_g;
+  lds_u8* const o = (lds_u8*)o_g;
+  lds_u32* const ea = (lds_u32*)ea_g;
+  lds_u32* const eb = (lds_u32*)eb_g;
+  lds_u32* const bm = (lds_u32*)bm_g;
+  const uint32_t nbw = ((ulen + 63) >> 6) * 2;  // bitmap words, whole 64-bit blocks
+  for (uint32_t k = lane; k < nbw; k += 64) bm[k] = 0;
+  uint32_t w0 = 0, ne = 0;
+  for (uint32_t base = q; base < qe;) {
+    const uint32_t i = base + lane;  // candidate start (reads stay inside the staging's slack)
+    const uint32_t t = in[i], b1 = in[i + 1], b2 = in[i + 2], b3 = in[i + 3], b4 = in[i + 4];
+    const uint32_t typ = t & 3;
+    const uint32_t room = qe > i ? qe - i : 0;
+    uint32_t hdr, outlen, a;
+    bool good;
+    if (typ == 0) {
+      const uint32_t L = t >> 2;
+      const uint32_t nb = L >= 60 ? L - 59 : 0;
+      const uint32_t ext = b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+      const uint32_t lm1 = nb ? (nb == 4 ? ext : ext & ((1u << (8 * nb)) - 1)) : L;
+      hdr = 1 + nb;
+      outlen = lm1 + 1;
+      a = i + hdr;
+      good = room >= hdr && lm1 < room - hdr;
+    } else {
+      hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
+      outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
+      a = typ == 1 ? ((t >> 5) << 8) | b1 : typ == 2 ? b1 | (b2 << 8) : b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+      good = room >= hdr;
+    }
+    const uint32_t size = typ == 0 ? hdr + outlen : hdr;
+    const uint32_t nxt = good ? lane + size : 0x7FFFFFFFu;
+    const uint32_t lim = qe - base < 64 ? qe - base : 64;
+    uint64_t mask = 0;
+    uint32_t cur = 0;
+    while (cur < lim) {
+      mask |= 1ull << cur;
+      cur = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)cur);
+    }
+    const bool sel = (mask >> lane) & 1;
+    const uint32_t v = sel ? outlen : 0u;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    const uint32_t w = w0 + incl - v;
+    const bool bad = sel && (!good || w > ulen || outlen > ulen - w || (typ != 0 && (a == 0 || a > w)));
+    if (__builtin_amdgcn_ballot_w64(bad)) return 0;
+    const uint32_t cnt = (uint32_t)__builtin_popcountll(mask);
+    if (ne + cnt > ecap) return 2;
+    if (sel) {
+      const uint32_t k = ne + (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1));
+      ea[k] = w | ((outlen - 1) << 16);  // (w < ulen <= 65536, outlen <= 65536)
+      eb[k] = typ == 0 ? (a | 0x80000000u) : a;
+      __hip_atomic_fetch_or(&bm[w >> 5], 1u << (w & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    ne += cnt;
+    w0 += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    base += cur;
+  }
+  if (w0 != ulen) return 0;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  int32_t eprev = -1;  // the element covering the byte before this block
+  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  for (uint32_t x0 = 0; x0 < ulen; x0 += 64) {
+    const uint64_t m = ((uint64_t)bm[(x0 >> 5) + 1] << 32) | bm[x0 >> 5];
+    const uint32_t x = x0 + lane;
+    const bool valid = x < ulen;
+    const int32_t e = eprev + (int32_t)__builtin_popcountll(m & le);
+    const uint32_t A = valid ? ea[e] : 0u, B = valid ? eb[e] : 0x80000000u;
+    const uint32_t ew = A & 0xFFFFu, elen = (A >> 16) + 1;
+    const uint32_t off = x - ew;
+    uint32_t src, fin, ptr = 64;
+    if (B >> 31) {
+      src = (B & 0x7FFFFFFFu) + off;
+      fin = 1;
+    } else {
+      const uint32_t per = B < elen ? B : 0u;  // (a copy is at most 64 bytes long: off < 64)
+      src = per ? ew - B + small_mod(off, per) : x - B;
+      fin = 0;
+      if (valid && src >= x0) ptr = src - x0;  // written in this block: chase it
+    }
+    while (__builtin_amdgcn_ballot_w64(ptr < 64)) {
+      const int p4 = (int)(ptr < 64 ? ptr : lane) * 4;
+      const uint32_t ns = (uint32_t)__builtin_amdgcn_ds_bpermute(p4, (int)src);
+      const uint32_t nf = (uint32_t)__builtin_amdgcn_ds_bpermute(p4, (int)fin);
+      const uint32_t np = (uint32_t)__builtin_amdgcn_ds_bpermute(p4, (int)ptr);
+      if (ptr < 64) {
+        src = ns;
+        fin = nf;
+        ptr = np;
+      }
+    }
+    const uint32_t byte = valid ? (fin ? in[src] : o[src]) : 0u;
+    if (valid) o[x] = (uint8_t)byte;
+    eprev += (int32_t)__builtin_popcountll(m);
+  }
+  return 1;
+}
+
 // ---------------------------------------------------------------------------------------------------
 // k_ts_open (lcrc_table_scan_async_ex with LCRC_TSCAN_SNAPPY_INDEX): the table scan's first launch when the table was
 // written with compression -- its index block is then usually a Snappy frame (table.rs:430, write_block keeps the
@@ -3483,15 +3596,23 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
 // ---------------------------------------------------------------------------------------------------
 constexpr uint32_t TO_IN = 32768 + 16;  // compressed bytes staged (+ the dword alignment)
 constexpr uint32_t TO_OUT = 65536;      // a whole chunk's output, V = 0^pad || M a multiple of 1 KiB
-constexpr uint32_t TO_LDS = TD_TAB_WORDS * 4 + TO_IN + SN_SLACK + TO_OUT;
+constexpr uint32_t TO_BM = 8192 + 16;   // the two-phase decode's element-start bitmap (+ one word past the end)
+constexpr uint32_t TO_ECAP = 7000;      // its element records (ea, eb); the area then holds the CRC tables
+constexpr uint32_t TO_E = 8 * TO_ECAP;
+static_assert(TO_E >= TD_TAB_WORDS * 4 && TO_E % 16 == 0, "the element area holds the CRC tables afterwards");
+constexpr uint32_t TO_LDS = TO_IN + SN_SLACK + TO_OUT + TO_BM + TO_E;
+static_assert(TO_LDS <= 163840 && (TO_IN + SN_SLACK) % 16 == 0, "k_ts_open's LDS");
 
 __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file, uint64_t file_len,
                                                const uint32_t* __restrict__ tab_c, uint8_t* __restrict__ idec,
                                                uint64_t idec_cap, uint64_t* __restrict__ iopen) {
   extern __shared__ __attribute__((aligned(16))) uint8_t to_lds[];
-  uint32_t* const T = (uint32_t*)to_lds;
-  uint8_t* const lin = to_lds + TD_TAB_WORDS * 4;
+  uint8_t* const lin = to_lds;
   uint8_t* const lout = lin + TO_IN + SN_SLACK;
+  uint32_t* const bm = (uint32_t*)(lout + TO_OUT);
+  uint32_t* const T = (uint32_t*)(lout + TO_OUT + TO_BM);  // the CRC tables, or the two-phase element records
+  uint32_t* const ea = T;
+  uint32_t* const eb = T + TO_ECAP;
   const uint32_t lane = __lane_id();
   // the footer's index handle, checked as ts_open_state checks it (all lanes alike)
   uint64_t io = 0, is = 0;
@@ -3517,8 +3638,13 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
     iopen[0] = (framed ? 1u : 0u) | (ok && fits ? 2u : 0u) | (ok && !fits ? 4u : 0u);
   }
   if (!ok || !fits || blockIdx.x >= chunks) return;  // (uniform)
-  for (uint32_t i = lane; i < TD_TAB_WORDS / 4; i += 64) ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i];
-  __syncthreads();
+  bool tables = false;  // T holds the CRC tables (the two-phase decode borrows the area)
+  auto load_tables = [&]() {
+    if (!tables) stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, lane, 64);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    tables = true;
+  };
   bool good = true;
   uint64_t o = 0, k = 0;
   for (uint32_t at = 0; at < len;) {  // the framing is good (snappy_frame_size): headers and lengths in bounds
@@ -3544,6 +3670,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
     uint32_t crc;
     bool cok = true;
     if (type == 1) {  // uncompressed: checksummed where it lies, copied out
+      load_tables();
       crc = td_chunk_crc<false>(T, p + q, ulen, lane);
       for (uint32_t x = lane; x < ulen; x += 64) idec[oc + x] = p[q + x];
     } else if (at - q + 4 <= TO_IN) {
@@ -3556,9 +3683,16 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
       stage_to_lds(za, (lds_u8*)lin, ndw, lane, 64);
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
+#if LCRC_TO_TWO_PHASE
+      tables = false;
+      const uint32_t r = snappy_two_phase(lin, d, d + (at - q), lout + pad, ulen, ea, eb, TO_ECAP, bm, lane);
+      cok = r == 2 ? snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane) : r == 1;
+#else
       cok = snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane);
+#endif
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
+      load_tables();
       crc = cok ? td_chunk_crc<true>(T, lout, ulen, lane) : 0u;
       if (cok) {
         const uint8_t* src = lout + pad;
@@ -3574,6 +3708,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
       if (lane == 0) cok = sn_serial_decode(p + q, p + at, idec, oo, oc + ulen);
       cok = bcast(cok ? 1u : 0u) != 0;
       __threadfence_block();
+      load_tables();
       crc = cok ? td_chunk_crc<false>(T, idec + oc, ulen, lane) : 0u;
     }
     good = good && cok && mask32c(crc) == want;
