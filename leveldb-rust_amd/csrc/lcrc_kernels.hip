@@ -1798,14 +1798,14 @@ constexpr uint32_t SN_MAX = 16384;
 // staging TD_IN + TD_OUT made of the wave's four row areas); a chunk too large for that, lane-serially to the workspace.
 constexpr uint32_t TD_WAVES = 4;
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
-constexpr uint32_t TR_IN = 3072 + 16;    // a row's frame (+ the slack of its element-header reads)
-constexpr uint32_t TR_OUT = 4608;        // a row's decoded chunk (V: a multiple of 256 B)
+constexpr uint32_t TR_IN = 3008 + 16;    // a row's frame (+ the slack of its element-header reads)
+constexpr uint32_t TR_OUT = 5120;        // a row's decoded chunk (V: a multiple of 1 KiB)
 constexpr uint32_t TR_ROW_LDS = TR_IN + 16 + TR_OUT;
 constexpr uint32_t TD_WAVE_LDS = 4 * TR_ROW_LDS;
 constexpr uint32_t TD_IN = 12288 + 16;   // the whole wave's staging: compressed bytes (+ 4 for the tail dword)
 constexpr uint32_t TD_OUT = 16384;       // decoded bytes (a multiple of 1 KiB: V fits as is)
 static_assert(TD_OUT % 1024 == 0, "the chunk CRC reads V in whole 1 KiB passes");
-static_assert(TR_OUT % 256 == 0 && TR_ROW_LDS % 16 == 0, "row staging");
+static_assert(TR_OUT % 1024 == 0 && TR_ROW_LDS % 16 == 0, "row staging");
 static_assert(TD_IN + SN_SLACK + TD_OUT <= TD_WAVE_LDS, "the wave staging is the wave's row areas");
 constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
 static_assert(TD_LDS <= 163840, "k_ts_decode's LDS");
@@ -3269,29 +3269,46 @@ __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, 
   return ok && w == ulen;
 }
 
-// The CRC-32C of V[pad, pad + len) per row, V = o[0, 256 np) with o[0, pad) zero (pad = 256 np - len): per 256 B
-// pass each lane walks 16 B (slice-by-4), the row tree joins them (Z16..Z128), the passes chain with Z256; the init
-// register is injected into the first min(4, len) bytes (td_chunk_crc's scheme on 16 lanes).
+// The CRC-32C of V[pad, pad + len) per row, V = o[0, 1024 np) with o[0, pad) zero (pad = 1024 np - len): per 1 KiB
+// pass each lane walks 64 B (slice-by-4, the init register injected into the first min(4, len) bytes of M), the row
+// tree joins the lanes with Z64, Z128, Z256, Z512, and the passes chain with Z1024 -- a quarter of the passes (and of
+// their tree and broadcast) of 16 B per lane.
 __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, uint32_t len, bool active,
                                                   uint32_t g, uint32_t lane) {
-  const uint32_t np = active ? (len + 255) >> 8 : 0u, pad = (np << 8) - len, q4 = len < 4 ? len : 4u;
+  const uint32_t np = active ? (len + 1023) >> 10 : 0u, pad = (np << 10) - len, q4 = len < 4 ? len : 4u;
   uint32_t acc = 0;
   for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
     const bool on = k < np;
-    const uint32_t x0 = 256 * k + 16 * g;
-    u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
-    w = td_inject(w, x0, pad, q4);
-    uint32_t cv = step4(T, 0u, w.x);
-    cv = step4(T, cv, w.y);
-    cv = step4(T, cv, w.z);
-    cv = step4(T, cv, w.w);
+    uint32_t cv = 0;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const uint32_t pn = row_down(cv, m);
-      if ((g & ((2u << m) - 1)) == 0) cv = zl(T, TAB_ZPIECE + m * 1024, cv) ^ pn;
+    for (int sp = 0; sp < 4; ++sp) {
+      const uint32_t x0 = 1024 * k + 64 * g + 16 * sp;
+      u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
+      w = td_inject(w, x0, pad, q4);
+      cv = step4(T, cv, w.x);
+      cv = step4(T, cv, w.y);
+      cv = step4(T, cv, w.z);
+      cv = step4(T, cv, w.w);
+    }
+    // row tree over 64 B pieces: level m joins lane g with g + 2^m, shifting the left part by 64 * 2^m bytes
+    {
+      const uint32_t pn = row_down(cv, 0);
+      if ((g & 1) == 0) cv = zl(T, TAB_ZPIECE + 2 * 1024, cv) ^ pn;
+    }
+    {
+      const uint32_t pn = row_down(cv, 1);
+      if ((g & 3) == 0) cv = zl(T, TAB_ZPIECE + 3 * 1024, cv) ^ pn;
+    }
+    {
+      const uint32_t pn = row_down(cv, 2);
+      if ((g & 7) == 0) cv = zl(T, TAB_ZWIN, cv) ^ pn;
+    }
+    {
+      const uint32_t pn = row_down(cv, 3);
+      if ((g & 15) == 0) cv = zl(T, TAB_ZWIN + 1024, cv) ^ pn;
     }
     const uint32_t pass = row_bcast0(cv, lane);
-    if (on) acc = k ? zl(T, TAB_ZWIN, acc) ^ pass : pass;
+    if (on) acc = k ? zl(T, TAB_ZWIN + 2048, acc) ^ pass : pass;
   }
   if (len < 4) acc ^= len ? 0xFFFFFFFFu >> (8 * len) : 0xFFFFFFFFu;
   return acc ^ 0xFFFFFFFFu;
@@ -3342,7 +3359,7 @@ __device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bo
         have = false;
       }
     }
-    const uint32_t pad = have ? ((ulen + 255) & ~255u) - ulen : 0u;
+    const uint32_t pad = have ? ((ulen + 1023) & ~1023u) - ulen : 0u;
     for (uint32_t k = 16 * g; k < pad; k += 256) *(__attribute__((address_space(3))) u32x4*)(o + k) = u32x4{0, 0, 0, 0};
     bool ok = true;
     if (__builtin_amdgcn_ballot_w64(have && type == 1))  // uncompressed: copied to V + pad
