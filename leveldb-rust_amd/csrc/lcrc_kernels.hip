@@ -3560,6 +3560,12 @@ __device__ uint32_t snappy_two_phase(const uint8_t* in_g, uint32_t q, uint32_t q
   if (w0 != ulen) return 0;
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
+#ifdef LCRC_PROBE_CLOCK
+  {
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && blockIdx.x < 1024) lcrc_dbg_stamp[(3072 + blockIdx.x) * 8 + 4] = t_;  // (k_windows: below 3072)
+  }
+#endif
   int32_t eprev = -1;  // the element covering the byte before this block
   const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   for (uint32_t x0 = 0; x0 < ulen; x0 += 64) {
@@ -3611,6 +3617,18 @@ __device__ uint32_t snappy_two_phase(const uint8_t* in_g, uint32_t q, uint32_t q
 // clears it). The index block's own checksum comes with the batch, as for a raw index; every verdict on the footer
 // and the handle is ts_open_state's.
 // ---------------------------------------------------------------------------------------------------
+#ifdef LCRC_PROBE_CLOCK  // diagnostic build: k_ts_open's per-workgroup phase stamps (s_memrealtime, 100 MHz)
+#define TO_STAMP(i)                                                                              \
+  do {                                                                                           \
+    __builtin_amdgcn_s_waitcnt(0);                                                               \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                              \
+    if (__lane_id() == 0 && blockIdx.x < 1024) lcrc_dbg_stamp[(3072 + blockIdx.x) * 8 + (i)] = t_; \
+  } while (0)
+#else
+#define TO_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 constexpr uint32_t TO_IN = 32768 + 16;  // compressed bytes staged (+ the dword alignment)
 constexpr uint32_t TO_OUT = 65536;      // a whole chunk's output, V = 0^pad || M a multiple of 1 KiB
 constexpr uint32_t TO_BM = 8192 + 16;   // the two-phase decode's element-start bitmap (+ one word past the end)
@@ -3631,6 +3649,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
   uint32_t* const ea = T;
   uint32_t* const eb = T + TO_ECAP;
   const uint32_t lane = __lane_id();
+  TO_STAMP(0);
   // the footer's index handle, checked as ts_open_state checks it (all lanes alike)
   uint64_t io = 0, is = 0;
   bool framed = false;
@@ -3654,6 +3673,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
     iopen[1] = ok ? total : 0;
     iopen[0] = (framed ? 1u : 0u) | (ok && fits ? 2u : 0u) | (ok && !fits ? 4u : 0u);
   }
+  TO_STAMP(1);
   if (!ok || !fits || blockIdx.x >= chunks) return;  // (uniform)
   bool tables = false;  // T holds the CRC tables (the two-phase decode borrows the area)
   auto load_tables = [&]() {
@@ -3691,6 +3711,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
       crc = td_chunk_crc<false>(T, p + q, ulen, lane);
       for (uint32_t x = lane; x < ulen; x += 64) idec[oc + x] = p[q + x];
     } else if (at - q + 4 <= TO_IN) {
+      TO_STAMP(2);
       const uint32_t pad = ((ulen + 1023) & ~1023u) - ulen;
       for (uint32_t x = 16 * lane; x < pad; x += 1024) *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
       const uint8_t* zs = p + q;
@@ -3700,6 +3721,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
       stage_to_lds(za, (lds_u8*)lin, ndw, lane, 64);
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
+      TO_STAMP(3);
 #if LCRC_TO_TWO_PHASE
       tables = false;
       const uint32_t r = snappy_two_phase(lin, d, d + (at - q), lout + pad, ulen, ea, eb, TO_ECAP, bm, lane);
@@ -3709,8 +3731,10 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
 #endif
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
+      TO_STAMP(5);
       load_tables();
       crc = cok ? td_chunk_crc<true>(T, lout, ulen, lane) : 0u;
+      TO_STAMP(6);
       if (cok) {
         const uint8_t* src = lout + pad;
         uint32_t x0 = 0;
@@ -3733,6 +3757,7 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
     __builtin_amdgcn_wave_barrier();  // the staging is reused by the next chunk
   }
   if (!good && lane == 0) iopen[2] = 1;  // (every writer stores the same 1)
+  TO_STAMP(7);
 }
 
 }  // namespace lcrc_dev
