@@ -93,7 +93,16 @@ def parse(argv=None):
                    help="fixed config starting and ending in (pinned) host memory: H2D + kernel + D2H per step "
                         "(the PCIe-inclusive end-to-end rate reported in DESIGN.md, never the headline value)")
     p.add_argument("--chunk-mib", type=int, default=32, help="host-resident pipeline chunk size")
-    return p.parse_args(argv)
+    p.add_argument("--engine-opt", action="append", default=[], metavar="NAME=V",
+                   help="measurement only: an lcrc_ctx_create_ex option for every context the bench creates "
+                        "(general=ranges|blocks, batch_grid_b, wal_grid_b, ts_grid, ts_blocks_div, ...); repeatable")
+    p.add_argument("--assume-bus-id", default=None, help=argparse.SUPPRESS)  # test-only: --engine host's "device"
+    a = p.parse_args(argv)
+    a.engine_opts = {}
+    for kv in a.engine_opt:
+        k, _, v = kv.partition("=")
+        a.engine_opts[k] = v if k == "general" else int(v)
+    return a
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -121,6 +130,29 @@ def spawn_ranks(n, argv):
     for p in procs:
         rc = max(rc, p.wait())
     return rc
+
+
+def bus_id_code(s):
+    """A PCI bus ID "dddd:bb:dd.f" as one integer (exact in the float64 the gloo gather carries); -1 for none."""
+    if not s:
+        return -1
+    dom, bus, df = s.split(":")
+    dev, fn = df.split(".")
+    return (int(dom, 16) << 16) | (int(bus, 16) << 8) | (int(dev, 16) << 3) | int(fn, 16)
+
+
+def bus_id_text(c):
+    c = int(c)
+    return None if c < 0 else f"{c >> 16:04x}:{(c >> 8) & 255:02x}:{(c >> 3) & 31:02x}.{c & 7:x}"
+
+
+def check_distinct_devices(codes, shared_ok):
+    """An N-rank line is the sum of N GPUs only if the ranks drive N distinct GPUs: refuse (raise) when two ranks
+    resolved to one PCI bus ID, unless the test-only LCRC_RANK_DEVICE_MOD=1 put them there on purpose."""
+    ids = [c for c in codes if c >= 0]
+    if len(set(ids)) != len(ids) and not shared_ok:
+        raise SystemExit(f"bench.py: ranks share a GPU (PCI bus IDs {[bus_id_text(c) for c in codes]}); "
+                         "each rank must drive its own device (LCRC_RANK_DEVICE_MOD=1 is for tests only)")
 
 
 class Dist:
@@ -567,7 +599,7 @@ def workload_table(m, synth, engs, rank, device, args):
     nscan = len(engs)
     for e in engs:
         e.close()
-    scanners = [m.Engine(device, m.MODE_REF) for _ in range(nscan)]
+    scanners = [m.Engine(device, m.MODE_REF, **args.engine_opts) for _ in range(nscan)]
     got = scanners[0].table_scan_into(dev, len(f), out)
     if got != len(blocks) or (out["status"][:got] != 0).any():
         raise RuntimeError("table bench: the sealed table does not scan clean")
@@ -596,8 +628,7 @@ def workload_table(m, synth, engs, rank, device, args):
     scanners[0].sync()
     st = res[0][2].download(np.uint32, 2)
     n = int(res[0][1].download(np.uint64, 1)[0])
-    if not args.table_sync and (st[0] != 0 or n != got or
-                                res[0][0].download(m.TBLK_DTYPE, n).tobytes() != out[:got].tobytes()):
+    if st[0] != 0 or n != got or res[0][0].download(m.TBLK_DTYPE, n).tobytes() != out[:got].tobytes():
         raise RuntimeError(f"table bench: the device-only scan disagrees with the synchronous scan (status {st.tolist()}, "
                            f"{n} vs {got} blocks)")
 
@@ -822,6 +853,10 @@ def main(argv=None):
         # test-only: rank r on device r % device_count, so that N device-bound ranks can share a 1-GPU box
         # (tests/test_multi_rank_gpu.py); the driver's N-GPU runs never set it (rank r = device LOCAL_RANK)
         device = dist.local_rank % max(1, m.device_count())
+    # every rank's PCI bus ID, checked before any work: N ranks on fewer GPUs would report a sum that no N GPUs made
+    bus_codes = [int(r[0]) for r in dist.gather([bus_id_code(m.pci_bus_id(device) if args.engine == "device"
+                                                             else args.assume_bus_id)])]
+    check_distinct_devices(bus_codes, os.environ.get("LCRC_RANK_DEVICE_MOD") == "1")
     synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
     mode = m.MODE_C if args.mode == "c" else m.MODE_REF
     flags = m.FLAG_MASK if mode == m.MODE_C else 0
@@ -833,7 +868,7 @@ def main(argv=None):
         engs = []
         w = workload_fixed_host(m, synth, rank, args)
     else:
-        engs = [m.Engine(device, mode, flags) for _ in range(max(1, nstreams))]
+        engs = [m.Engine(device, mode, flags, **args.engine_opts) for _ in range(max(1, nstreams))]
         if args.host_resident:
             w = workload_host(m, synth, engs, rank, device, args)
         else:
@@ -862,7 +897,7 @@ def main(argv=None):
     rows = dist.gather([rank, device, elapsed, fp, launch_us])
     per_gpu = []
     for r in rows:
-        row = {"rank": int(r[0]), "device": int(r[1]),
+        row = {"rank": int(r[0]), "device": int(r[1]), "pci_bus_id": bus_id_text(bus_codes[int(r[0])]),
                "gib_s": round(w.nbytes * args.steps / r[2] / 2 ** 30, 2),
                "pct_hbm": round(100.0 * w.nbytes * args.steps / r[2] / (PEAK_GBS * 1e9), 2),
                "crc_xor": f"{int(r[3]):08x}"}

@@ -130,6 +130,9 @@ typedef struct lcrc_wal_rec {
  * streams race on that workspace. For concurrent streams use one context per stream (bench.py does: one
  * context per engine). Different contexts never share workspace. */
 int lcrc_device_count(int* n);
+/* The PCI bus ID of a device ("dddd:bb:dd.f", NUL-terminated in out[0, len)): a multi-process caller can check that
+ * its ranks drive distinct GPUs (bench.py records it per rank and refuses two ranks on one GPU). */
+int lcrc_device_pci_bus_id(int device, char* out, int len);
 int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags);
 /* Kernel-selection and grid overrides for tests and measurement (production callers use lcrc_ctx_create, which is
  * lcrc_ctx_create_ex with every option at its default). Zero-initialise, set size = sizeof(lcrc_ctx_options); a

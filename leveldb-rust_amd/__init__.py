@@ -104,7 +104,7 @@ _lib = None
 ABI_SYMBOLS = [
     "lcrc32_value", "lcrc32_extend", "lcrc32c_value", "lcrc32c_extend", "lcrc32c_mask", "lcrc32c_unmask",
     "lcrc_extend", "lcrc_combine", "lcrc_hasher_init", "lcrc_hasher_update", "lcrc_hasher_finalize",
-    "lcrc_device_count", "lcrc_ctx_create", "lcrc_ctx_create_ex", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream", "lcrc_ctx_join",
+    "lcrc_device_count", "lcrc_device_pci_bus_id", "lcrc_ctx_create", "lcrc_ctx_create_ex", "lcrc_ctx_destroy", "lcrc_ctx_reserve", "lcrc_ctx_stream", "lcrc_ctx_join",
     "lcrc_ctx_sync", "lcrc_batch", "lcrc_batch_covered", "lcrc_batch_uniform", "lcrc_batch_uniform_queue", "lcrc_batch_queue", "lcrc_batch_multi", "lcrc_batch_host_uniform", "lcrc_wal_scan", "lcrc_wal_scan_async", "lcrc_wal_scan_queue",
     "lcrc_table_scan", "lcrc_table_scan_async", "lcrc_table_scan_async_ex", "lcrc_table_scan_reserve", "lcrc_table_scan_message",
     "lcrc_batch_seal", "lcrc_snappy_frames",
@@ -146,6 +146,7 @@ def lib():
     sig("lcrc_hasher_update", None, ctypes.POINTER(_Hasher), vp, sz)
     sig("lcrc_hasher_finalize", u32, ctypes.POINTER(_Hasher))
     sig("lcrc_device_count", i32, ctypes.POINTER(ctypes.c_int))
+    sig("lcrc_device_pci_bus_id", i32, i32, ctypes.c_char_p, i32)
     sig("lcrc_ctx_create", i32, ctypes.POINTER(vp), i32, i32, u32)
     sig("lcrc_ctx_create_ex", i32, ctypes.POINTER(vp), i32, i32, u32, ctypes.POINTER(_CtxOptions))
     sig("lcrc_ctx_destroy", i32, vp)
@@ -311,6 +312,13 @@ def device_count():
     n = ctypes.c_int(0)
     lib().lcrc_device_count(ctypes.byref(n))
     return n.value
+
+
+def pci_bus_id(device):
+    """The device's PCI bus ID ("dddd:bb:dd.f", lcrc_device_pci_bus_id)."""
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().lcrc_device_pci_bus_id(int(device), buf, 64), "lcrc_device_pci_bus_id")
+    return buf.value.decode()
 
 
 class DeviceBuffer:

@@ -314,6 +314,16 @@ int lcrc_device_count(int* n) {
   return c > 0 ? LCRC_OK : LCRC_ENODEV;
 }
 
+int lcrc_device_pci_bus_id(int device, char* out, int len) {
+  if (!out || len < 13) return LCRC_EINVAL;
+  const hipError_t e = hipDeviceGetPCIBusId(out, len, device);
+  if (e != hipSuccess) {
+    out[0] = 0;
+    return fail_hip(e, "hipDeviceGetPCIBusId");
+  }
+  return LCRC_OK;
+}
+
 int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
   return lcrc_ctx_create_ex(out, device, mode, flags, nullptr);
 }
@@ -1463,7 +1473,9 @@ int lcrc_table_scan(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, const
     uint64_t cap = std::max<uint64_t>(std::max<uint64_t>(max_blocks, ctx->ts_blocks.cap), 1024);
     lcrc_tscan_dev* hs = (lcrc_tscan_dev*)ctx->ts_host;
     bool ran = true;
-    for (int attempt = 0; attempt < 3; ++attempt) {
+    // up to three independent reasons to grow (the decoded index over the workspace -- reported first, as
+    // ts_open_state stops there --, the result capacity, the decoded frames over the workspace), then the scan itself
+    for (int attempt = 0; attempt < 4; ++attempt) {
       rc = ctx->ts_blocks.ensure(cap);
       if (!rc) rc = ctx->ts_count.ensure(1);
       if (!rc)

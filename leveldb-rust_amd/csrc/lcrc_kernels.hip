@@ -1771,19 +1771,30 @@ __global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
 // ---------------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return *p; }
 
-// Snappy raw-format length preamble (varint32) of a compressed chunk's data; false when malformed
-__device__ __forceinline__ bool snappy_ulen(const uint8_t* p, uint32_t n, uint32_t& ulen, uint32_t& used) {
+// The Snappy raw-format length preamble of a compressed chunk's data, as the snap crate (Cargo.toml:15, "1") reads it
+// for FrameDecoder (format.rs:196): bytes::read_varu64 -- up to 10 bytes, the value taken mod 2^64 (a byte's bits
+// shifted past bit 63 are dropped, an 11th byte is an error) -- and the frame decoder then rejects a decoded length
+// over MAX_BLOCK_SIZE (65,536). byte(i) reads preamble byte i (i < n). True with ulen (<= 65,536) and used (the
+// preamble's bytes) when the chunk's length is acceptable; a 5-byte preamble of 2^32 is NOT a zero length.
+template <class ByteAt>
+__device__ __forceinline__ bool snappy_preamble(ByteAt byte, uint32_t n, uint32_t& ulen, uint32_t& used) {
+  uint64_t v = 0;
   ulen = 0;
-  for (uint32_t i = 0; i < 5 && i < n; ++i) {
-    const uint32_t b = ld_u8(p + i);
-    ulen |= (b & 127u) << (7 * i);
+  used = 0;
+  for (uint32_t i = 0; i < 10 && i < n; ++i) {
+    const uint32_t b = byte(i);
+    v |= (uint64_t)(b & 127u) << (7 * i);
     if (!(b & 128)) {
       used = i + 1;
-      return true;
+      ulen = v <= 65536 ? (uint32_t)v : 0u;
+      return v <= 65536;
     }
   }
   return false;
 }
+// snap's FrameDecoder reads a chunk body into a buffer of MAX_COMPRESS_BLOCK_SIZE = 76,490 bytes (the worst-case
+// compressed size of a 64 KiB block): any chunk longer than that, of any type, is an error
+constexpr uint32_t SN_MAX_CHUNK = 76490;
 
 // the framing walk of one frame p[0, len): decoded size, data-chunk count, largest compressed data (after the
 // crc) and decoded chunk; false when the framing is malformed
@@ -1831,7 +1842,7 @@ __device__ __forceinline__ bool snappy_frame_size(const uint8_t* __restrict__ p,
     const uint32_t type = ld_u8(p + at);
     const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
     at += 4;
-    if (len - at < cl) {
+    if (len - at < cl || cl > SN_MAX_CHUNK) {
       ok = false;
       break;
     }
@@ -1844,7 +1855,7 @@ __device__ __forceinline__ bool snappy_frame_size(const uint8_t* __restrict__ p,
     } else if (type <= 1) {
       uint32_t ulen = cl >= 4 ? cl - 4 : 0, used = 0;
       if (cl < 4) ok = false;
-      else if (type == 0) ok = snappy_ulen(p + at + 4, cl - 4, ulen, used);
+      else if (type == 0) ok = snappy_preamble([&](uint32_t i) { return ld_u8(p + at + 4 + i); }, cl - 4, ulen, used);
       if (ulen > 65536) ok = false;
       if (type == 0 && cl - 4 > max_in) max_in = cl - 4;
       if (ulen > max_out) max_out = ulen;
@@ -2099,7 +2110,8 @@ __device__ bool snappy_wave_decode(const uint8_t* in_g, uint32_t q, uint32_t qe,
       hdr = 1 + nb;
       outlen = lm1 + 1;
       a = i + hdr;
-      good = room >= hdr && lm1 < room - hdr;  // literal bytes inside the input (no u32 wrap)
+      good = room >= hdr && lm1 < room - hdr && (nb == 0 || room >= 5);  // bytes inside the input (no u32 wrap);
+      // an extended length needs 4 bytes after the tag whatever nb is (snap's read_literal reads one 4-byte word)
     } else {
       hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
       outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
@@ -2228,7 +2240,7 @@ __device__ bool sn_serial_decode(const uint8_t* qp, const uint8_t* qe, uint8_t* 
       ln = tag >> 2;
       if (ln >= 60) {
         const uint32_t nb = ln - 59;
-        if ((uint64_t)(qe - qp) < nb) { ok = false; break; }
+        if ((uint64_t)(qe - qp) < 4) { ok = false; break; }  // snap: 4 bytes after the tag whatever nb is
         ln = 0;
         for (uint32_t k = 0; k < nb; ++k) ln |= (uint32_t)qp[k] << (8 * k);
         qp += nb;
@@ -2303,12 +2315,9 @@ __global__ void __launch_bounds__(64) k_snappy_decode_wave(const uint8_t* __rest
         for (uint32_t k = lane; k < cl - 4; k += 64) out[o + k] = src[k];
         o += cl - 4;
       } else {
-        uint32_t ulen = 0, q = body + 4;  // preamble = uncompressed length
-        for (uint32_t i = 0, sh = 0; i < 5 && q < at; ++i, sh += 7) {
-          const uint32_t b = rd.byte(q++);
-          ulen |= (b & 127u) << sh;
-          if (!(b & 128)) break;
-        }
+        uint32_t ulen = 0, q = body + 4, used = 0;  // preamble = uncompressed length (valid: pass 1)
+        snappy_preamble([&](uint32_t i) { return rd.byte(q + i); }, at - q, ulen, used);
+        q += used;
         if (ulen <= out_cap && at - q + 4 <= in_lim) {
           // stage the elements: aligned dwords from the one holding the first byte
           const uint8_t* zs = rd.a + q;
@@ -3154,12 +3163,9 @@ __device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint
     if (type == 1) {  // uncompressed: checksummed where it lies
       crc = td_chunk_crc<false>(T, rd.a + body + 4, cl - 4, lane);
     } else {
-      uint32_t ulen = 0, q = body + 4;  // preamble = uncompressed length
-      for (uint32_t i = 0, sh = 0; i < 5 && q < at; ++i, sh += 7) {
-        const uint32_t b = rd.byte(q++);
-        ulen |= (b & 127u) << sh;
-        if (!(b & 128)) break;
-      }
+      uint32_t ulen = 0, q = body + 4, used = 0;  // preamble = uncompressed length (valid: k_ts_finish)
+      snappy_preamble([&](uint32_t i) { return rd.byte(q + i); }, at - q, ulen, used);
+      q += used;
       if (ulen <= TD_OUT && at - q + 4 <= TD_IN) {
         // decoded at V + pad of the output staging, V[0, pad) zeroed: the CRC reads whole aligned 16 B pieces
         const uint32_t pad = ((ulen + 1023) & ~1023u) - ulen;
@@ -3226,7 +3232,7 @@ __device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, 
       hdr = 1 + nb;
       outlen = lm1 + 1;
       a = qq + hdr;
-      good = room >= hdr && lm1 < room - hdr;  // the literal's bytes inside the input (no u32 wrap)
+      good = room >= hdr && lm1 < room - hdr && (nb == 0 || room >= 5);  // (as snappy_wave_decode)
     } else {
       hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
       outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
@@ -3347,12 +3353,10 @@ __device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bo
       want = in[body] | ((uint32_t)in[body + 1] << 8) | ((uint32_t)in[body + 2] << 16) | ((uint32_t)in[body + 3] << 24);
       if (type == 1) {
         ulen = cl - 4;
-      } else {
-        for (uint32_t i = 0, sh = 0; i < 5 && q < next; ++i, sh += 7) {  // preamble = uncompressed length
-          const uint32_t b = in[q++];
-          ulen |= (b & 127u) << sh;
-          if (!(b & 128)) break;
-        }
+      } else {  // preamble = uncompressed length (valid: k_ts_finish)
+        uint32_t used = 0;
+        snappy_preamble([&](uint32_t i) { return (uint32_t)in[q + i]; }, next - q, ulen, used);
+        q += used;
       }
       if (ulen > TR_OUT) {
         res = 2;  // too large for the row: the whole wave decodes this frame
@@ -3414,7 +3418,10 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     chunks = xc;
   }
   const bool over = total > ts_out_cap;
-  if (t == 0 && threadIdx.x == 0 && live) {
+  // recorded by workgroup 0 and by the last tile's workgroup (the same values): the last one runs ts_final and is the
+  // only one that changes st->status, so its `live` is always the scan's own; workgroup 0 may read a status the last
+  // one has already set to TS_HOST (frames over the workspace) and skip the record
+  if (threadIdx.x == 0 && live && (t == 0 || last)) {
     st->need_out = total;
     st->need_chunks = chunks;
     st->gate = over ? 1u : chunks == 0 ? 2u : 0u;
@@ -3523,7 +3530,7 @@ __device__ uint32_t snappy_two_phase(const uint8_t* in_g, uint32_t q, uint32_t q
       hdr = 1 + nb;
       outlen = lm1 + 1;
       a = i + hdr;
-      good = room >= hdr && lm1 < room - hdr;
+      good = room >= hdr && lm1 < room - hdr && (nb == 0 || room >= 5);  // (as snappy_wave_decode)
     } else {
       hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
       outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
@@ -3691,13 +3698,10 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
     at = body + cl;
     if (type > 1) continue;  // stream identifier, skippable chunks
     uint32_t ulen = cl - 4, q = body + 4;
-    if (type == 0) {  // preamble = uncompressed length
-      ulen = 0;
-      for (uint32_t i = 0, sh = 0; i < 5 && q < at; ++i, sh += 7) {
-        const uint32_t b = ld_u8(p + q++);
-        ulen |= (b & 127u) << sh;
-        if (!(b & 128)) break;
-      }
+    if (type == 0) {  // preamble = uncompressed length (valid: snappy_frame_size)
+      uint32_t used = 0;
+      snappy_preamble([&](uint32_t i) { return ld_u8(p + q + i); }, at - q, ulen, used);
+      q += used;
     }
     const uint64_t oc = o;
     o += ulen;

@@ -76,10 +76,25 @@ const char* decode_footer(const uint8_t* f, Handle& metaindex, Handle& index) {
 }
 
 // ---- Snappy ---------------------------------------------------------------------------------------
+// The length preamble as snap's bytes::read_varu64 reads it (up to 10 bytes, mod 2^64), accepted only up to the
+// frame decoder's MAX_BLOCK_SIZE (65,536): a 5-byte preamble of 2^32 is an error, not a zero length.
+static bool snappy_preamble(const uint8_t*& p, const uint8_t* end, uint32_t& out) {
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < 10 && p < end; ++i) {
+    const uint64_t b = *p++;
+    v |= (b & 127u) << (7 * i);
+    if (!(b & 128u)) {
+      out = (uint32_t)v;
+      return v <= 65536;
+    }
+  }
+  return false;
+}
+
 bool snappy_raw_decompress(const uint8_t* p, size_t n, std::vector<uint8_t>& out) {
   const uint8_t* end = p + n;
   uint32_t ulen;
-  if (!get_varint32(p, end, ulen)) return false;
+  if (!snappy_preamble(p, end, ulen)) return false;
   const size_t base = out.size();
   out.reserve(base + ulen);
   while (p < end) {
@@ -90,7 +105,7 @@ bool snappy_raw_decompress(const uint8_t* p, size_t n, std::vector<uint8_t>& out
         len = tag >> 2;
         if (len >= 60) {
           const uint32_t nb = (uint32_t)len - 59;  // 1..4 little-endian length bytes
-          if ((size_t)(end - p) < nb) return false;
+          if ((size_t)(end - p) < 4) return false;  // snap reads the length as one 4-byte word, whatever nb is
           len = 0;
           for (uint32_t i = 0; i < nb; ++i) len |= (uint64_t)p[i] << (8 * i);
           p += nb;
@@ -135,7 +150,7 @@ bool snappy_frame_decode(const uint8_t* p, size_t n, std::vector<uint8_t>& out) 
     const uint32_t type = p[0];
     const uint32_t len = (uint32_t)p[1] | ((uint32_t)p[2] << 8) | ((uint32_t)p[3] << 16);
     p += 4;
-    if ((uint64_t)(end - p) < len) return false;
+    if ((uint64_t)(end - p) < len || len > 76490) return false;  // snap: MAX_COMPRESS_BLOCK_SIZE, any chunk type
     const uint8_t* body = p;
     p += len;
     if (type == 0xff) {  // stream identifier (may repeat)

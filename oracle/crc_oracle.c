@@ -297,7 +297,7 @@ static int snappy_raw(const uint8_t* p, size_t n, uint8_t* out, size_t ulen) {
       len = t >> 2;
       if (len >= 60) {
         const size_t nb = len - 59;
-        if (n - q < nb) return 1;
+        if (n - q < 4) return 1; /* snap's read_literal: 4 input bytes after the tag whatever nb is */
         len = 0;
         for (size_t k = 0; k < nb; ++k) len |= (size_t)p[q + k] << (8 * k);
         q += nb;
@@ -344,7 +344,7 @@ static int frame_check(const uint8_t* p, size_t n, uint8_t* scratch) {
     const uint32_t type = p[at];
     const size_t cl = p[at + 1] | ((size_t)p[at + 2] << 8) | ((size_t)p[at + 3] << 16);
     at += 4;
-    if (n - at < cl) return 1;
+    if (n - at < cl || cl > 76490) return 1; /* snap: MAX_COMPRESS_BLOCK_SIZE, any chunk type */
     const uint8_t* b = p + at;
     at += cl;
     if (type == 0xff) {
@@ -361,11 +361,13 @@ static int frame_check(const uint8_t* p, size_t n, uint8_t* scratch) {
         data = b + 4;
         ulen = cl - 4;
       } else {
-        size_t q = 4, v = 0;
+        /* the preamble as snap's bytes::read_varu64: up to 10 bytes, the value mod 2^64 */
+        size_t q = 4;
+        uint64_t v = 0;
         int sh = 0, done = 0;
-        while (q < cl && sh <= 28) {
+        while (q < cl && sh <= 63) {
           const uint32_t c = b[q++];
-          v |= (size_t)(c & 127) << sh;
+          v |= (uint64_t)(c & 127) << sh;
           sh += 7;
           if (!(c & 128)) {
             done = 1;

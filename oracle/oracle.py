@@ -486,15 +486,33 @@ def _get_varint(buf, p, limit, bits):
     return None, p
 
 
+SNAPPY_MAX_BLOCK = 65536         # snap's frame.rs MAX_BLOCK_SIZE: a chunk's decoded bytes
+SNAPPY_MAX_COMPRESS_BLOCK = 76490  # snap's MAX_COMPRESS_BLOCK_SIZE: FrameDecoder's body buffer, any chunk type
+
+
+def _snap_varu64(z):
+    """snap's bytes::read_varu64 (snap "1", Cargo.toml:15): (value mod 2**64, bytes used), or (None, 0) when no byte
+    below 0x80 comes within 10 bytes (an 11th byte's shift of 70 fails checked_shl)."""
+    v = 0
+    for i in range(min(len(z), 10)):
+        v |= (z[i] & 127) << (7 * i)
+        if z[i] < 128:
+            return v & ((1 << 64) - 1), i + 1
+    return None, 0
+
+
 def snappy_frame_decode(data):
-    """Pure-Python Snappy framing decode with chunk CRC check; None when corrupt."""
+    """Snappy framing decode with chunk CRC check as snap's read::FrameDecoder does it (format.rs:196); None when corrupt.
+    Restated from the snap crate's published behaviour (the crate is absent here): the first chunk must be the stream
+    identifier; a chunk longer than MAX_COMPRESS_BLOCK_SIZE (any type) is an error; a data chunk has a 4-byte masked
+    CRC-32C; its decoded bytes are at most MAX_BLOCK_SIZE; 0x02..0x7f are unskippable, 0x80..0xfe skipped."""
     data, p, out, seen = bytes(data), 0, bytearray(), False
     while p < len(data):
         if len(data) - p < 4:
             return None
         typ, n = data[p], data[p + 1] | (data[p + 2] << 8) | (data[p + 3] << 16)
         p += 4
-        if len(data) - p < n:
+        if len(data) - p < n or n > SNAPPY_MAX_COMPRESS_BLOCK:
             return None
         body, p = data[p:p + n], p + n
         if typ == 0xFF:
@@ -518,8 +536,8 @@ def snappy_frame_decode(data):
 
 
 def _snappy_raw(z):
-    ulen, p = _get_varint(z, 0, len(z), 32)
-    if ulen is None:
+    ulen, p = _snap_varu64(z)
+    if ulen is None or ulen > SNAPPY_MAX_BLOCK:  # snap: Header::read, then the frame decoder's dn > MAX_BLOCK_SIZE
         return None
     out = bytearray()
     while p < len(z):
@@ -530,7 +548,10 @@ def _snappy_raw(z):
             n = tag >> 2
             if n >= 60:
                 nb = n - 59
-                if len(z) - p < nb:
+                # snap's read_literal reads the length as one 4-byte word: it needs 4 input bytes after the tag
+                # whatever nb is ("the literal must have length >= 61"), so a short extended literal at the end of the
+                # input is an error even when its own bytes fit
+                if len(z) - p < 4:
                     return None
                 n = int.from_bytes(z[p:p + nb], "little")
                 p += nb

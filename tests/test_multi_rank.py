@@ -81,3 +81,30 @@ def test_queue_grouping():
     assert [len(p) for p in bench.balanced_jobs(list(range(32)))] == [32]
     assert [len(p) for p in bench.balanced_jobs(list(range(65)))] == [22, 22, 21]
     assert bench.launches_of(50) == 2 and bench.launches_of(32) == 1
+
+
+def test_bench_refuses_ranks_on_one_gpu():
+    """Two ranks whose devices resolve to one PCI bus ID: bench.py refuses to print a 2-GPU line,
+    unless the test-only LCRC_RANK_DEVICE_MOD=1 put them there on purpose; each rank's bus ID is in per_gpu."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--engine", "host", "--blocks", str(NBLK),
+           "--steps", "2", "--warmup", "1", "--assume-bus-id", "0000:75:00.0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=_env(), cwd=ROOT)
+    assert r.returncode != 0 and "ranks share a GPU" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(_env(), LCRC_RANK_DEVICE_MOD="1"),
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = _line(r.stdout)
+    assert [g["pci_bus_id"] for g in res["per_gpu"]] == ["0000:75:00.0"] * 2
+
+
+def test_bus_id_codes():
+    sys.path.insert(0, ROOT)
+    import bench
+    for s in ("0000:75:00.0", "0001:e5:1f.7", "ffff:00:00.1"):
+        assert bench.bus_id_text(float(bench.bus_id_code(s))) == s
+    bench.check_distinct_devices([bench.bus_id_code("0000:05:00.0"), bench.bus_id_code("0000:15:00.0"), -1, -1],
+                                 False)
+    with pytest.raises(SystemExit):
+        bench.check_distinct_devices([bench.bus_id_code("0000:05:00.0")] * 2, False)
+    bench.check_distinct_devices([bench.bus_id_code("0000:05:00.0")] * 2, True)

@@ -33,6 +33,9 @@ def test_bench_two_device_ranks(orc, synth, NBLK):
     assert res["n_gpus"] == world and res["scaling"] == "weak"
     assert [g["rank"] for g in res["per_gpu"]] == list(range(world))
     assert [g["device"] for g in res["per_gpu"]] == [0] * world  # rank r on device r % 1
+    # each rank's PCI bus ID: the same GPU for both (allowed only under LCRC_RANK_DEVICE_MOD=1)
+    bus = [g["pci_bus_id"] for g in res["per_gpu"]]
+    assert bus[0] and len(bus[0]) == 12 and bus == [bus[0]] * world
     assert res["roofline"] is not None and res["roofline"]["frac"] > 0
     for g in res["per_gpu"]:
         # each rank checksummed its own batch on the device: its fingerprint is the oracle's (masked CRC-32C)
