@@ -354,7 +354,8 @@ class Workload:
         self.per_step_sync = per_step_sync
         self.engines = engines  # the engines the steps run on, when not the bench's own
         self.kernel_events = kernel_events  # the launches can carry the roofline's events (queued fast path)
-        self.single = None  # single(i): one launch of the dominant kernel, for the alone-on-the-GPU figure
+        self.single = None  # single(i): one launch of the dominant kernel (or one whole scan), alone on the GPU
+        self.bound = "hbm"  # the measured limiter of the dominant kernel (roofline.bound)
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -654,6 +655,10 @@ def workload_table(m, synth, engs, rank, device, args):
                 scanners[k].table_scan_async(devs[i % 2], len(f), res[k][0], cap, res[k][1], res[k][2], snappy_index=si)
 
     run.keep = (pinned, scanners, res, devs)  # (a graph holds raw pointers: the files must outlive it)
+    single = None
+    if not (args.table_sync or args.graph):  # one whole scan alone on the GPU (its first launch's start to its last end)
+        def single(i):
+            scanners[0].table_scan_async(devs[i % 2], len(f), res[0][0], cap, res[0][1], res[0][2], snappy_index=si)
     cfg = {"workload": ("whole-table verify scan: ~64K Snappy-compressed data blocks (4 KiB raw, db_bench values) + "
                         "index: block crc32fast trailers, frames decoded, every chunk's masked CRC-32C"
                         if args.compression else
@@ -664,9 +669,14 @@ def workload_table(m, synth, engs, rank, device, args):
            "form": "lcrc_table_scan (results to pinned host)" if args.table_sync else
            "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async",
            "snappy_index": bool(args.compression and framed[kinds == m.TBLK_INDEX].any())}
-    return Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, sample, lambda: scanned["crc"].copy(),
-                    per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si),
-                    kernel_events=not (args.table_sync or args.graph))
+    w = Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, sample, lambda: scanned["crc"].copy(),
+                 per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si),
+                 kernel_events=not (args.table_sync or args.graph))
+    w.single = single
+    # the compressed scan's decoders are bound by instruction issue (SQ counters: VALU + SALU per element, DESIGN.md
+    # section 4), not by HBM: its fraction of 8 TB/s is reported, but the bound is not bandwidth
+    w.bound = "issue" if args.compression else "hbm"
+    return w
 
 
 def workload_seal(m, synth, engs, rank, device, args):
@@ -726,7 +736,9 @@ def workload_snappy(m, synth, engs, rank, device, args):
 
     cfg = {"workload": "Snappy frames: 64K x (1 compressed chunk -> 4 KiB), decode + masked CRC-32C per chunk",
            "frames": nfr, "frame_bytes": len(frame)}
-    return Workload(run, cap, cfg, None, None, None, per_step_sync=True)
+    w = Workload(run, cap, cfg, None, None, None, per_step_sync=True)
+    w.bound = "issue"  # the wave decoder: a chain of dependent elements
+    return w
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -883,7 +895,7 @@ def main(argv=None):
     timers = w.engines if w.engines else engs
     # one batch handed over alone (fixed config): timed before the warmup, so that the timed region's launches are
     # the last ones of the dominant kernel in a profiled run (tools/summarize_profile.py)
-    single = single_launches(w, engs[0]) if (w.single is not None and engs) else None
+    single = single_launches(w, (w.engines or engs)[0]) if (w.single is not None and (w.engines or engs)) else None
     # this rank's fingerprint (gathered over gloo with the rates below), taken before the timed region so that
     # the timed launches are the last ones of the dominant kernel in a profiled run (tools/summarize_profile.py)
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
@@ -932,7 +944,7 @@ def main(argv=None):
         bytes_per_launch = w.nbytes * cov_steps / cov_launches
         achieved = bytes_per_launch / launch_s / 1e9
         result["roofline"] = {
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
+            "bound": w.bound, "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(prof_config, args.mode),
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
@@ -949,8 +961,10 @@ def main(argv=None):
                 "launch_us_median": round(med, 2), "launch_us_min": round(one[0], 2),
                 "launch_us_max": round(one[-1], 2), "launches": len(one),
                 "frac_best": round(bytes_per_launch / (one[0] * 1e-6) / 1e9 / PEAK_GBS, 4),
-                "timing": "one lcrc_batch_uniform launch alone on the GPU (the previous one's end waited for), its "
-                          "own start and end events; median over the launches (before the warmup)"}
+                "timing": ("one lcrc_batch_uniform launch" if w.cfg.get("kernels_per_step", 1) == 1 else
+                           f"one whole scan ({w.cfg.get('kernels_per_step')} dependent launches)") +
+                          " alone on the GPU (the previous one's end waited for), its own start and end events (the "
+                          "first launch's start to the last one's end); median over the launches (before the warmup)"}
     else:
         result["roofline"] = None
     # the CPU baseline (north_star: "next to the reference's own CPU CRC32C timed on the same box's host cores in the

@@ -4,6 +4,7 @@
 // present every batched call returns LCRC_ENODEV.
 #include <hip/hip_runtime_api.h>
 
+#include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -68,6 +69,12 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t m, hipStream_t st);
+hipError_t lcrc_launch_wal_onepass(int grid_a, int grid_b, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
+                                   uint32_t* counts, uint2* slots, uint8_t* stops, uint64_t* local, uint64_t* part,
+                                   uint32_t* rl_cnt, uint4* rl, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
+                                   uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, uint64_t* n_kb,
+                                   uint32_t* win, const uint32_t* gtab, uint32_t init, uint32_t xorout, uint32_t poly,
+                                   uint32_t* crcs, hipStream_t st);
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
                                    uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
                                    hipStream_t st);
@@ -167,6 +174,8 @@ struct lcrc_ctx {
   DevBuf<uint64_t> wal_offsets;
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs;
+  DevBuf<uint32_t> wal_rlcnt;  // (wal_onepass) per 16 KiB region: records the window pass finishes
+  DevBuf<uint4> wal_rl;        // (wal_onepass) their lists, WAL_RMAX slots per region
   // lcrc_batch_multi: this context's shard (the byte span its descriptors cover, the rebased descriptors,
   // CRCs and mismatch words)
   DevBuf<uint8_t> ms_data;
@@ -215,6 +224,7 @@ struct lcrc_ctx {
   // lcrc_ctx_options (lcrc_ctx_create_ex; tests and measurement only -- the library reads no environment variable)
   uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (tests reach the tile loops with a small one)
   int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan
+  bool wal_onepass = false;  // lcrc_ctx_options.wal_onepass
   uint32_t batch_grid_b = 0;  // lcrc_batch's k_blocks grid (0: 2 per CU)
   uint32_t wal_grid_b = 0;    // the WAL scan's k_blocks grid (0: every resident workgroup)
 };
@@ -330,7 +340,9 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
 
 int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, const lcrc_ctx_options* opt) {
   if (!out || (mode != LCRC_MODE_REF && mode != LCRC_MODE_C)) return LCRC_EINVAL;
-  if (opt && (opt->size < sizeof(lcrc_ctx_options) || opt->general < 0 || opt->general > 2)) return LCRC_EINVAL;
+  // (a caller built against the round-4 header passes the struct without wal_onepass: accepted, option off)
+  if (opt && (opt->size < offsetof(lcrc_ctx_options, wal_onepass) || opt->general < 0 || opt->general > 2))
+    return LCRC_EINVAL;
   *out = nullptr;
   int ndev = 0;
   int rc = lcrc_device_count(&ndev);
@@ -393,6 +405,7 @@ int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, con
     ctx->wal_grid_b = opt->wal_grid_b;
     if (opt->ts_grid) ctx->ts_grid = opt->ts_grid;
     if (opt->ts_blocks_div) ctx->ts_blocks_div = (int)opt->ts_blocks_div;
+    if (opt->size >= offsetof(lcrc_ctx_options, wal_onepass) + sizeof(uint32_t)) ctx->wal_onepass = opt->wal_onepass != 0;
   }
   *out = ctx;
   return LCRC_OK;
@@ -421,6 +434,8 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->wal_offsets.release();
   ctx->wal_descs.release();
   ctx->wal_crcs.release();
+  ctx->wal_rlcnt.release();
+  ctx->wal_rl.release();
   ctx->ms_data.release();
   ctx->ms_desc.release();
   ctx->ms_out.release();
@@ -964,6 +979,19 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   uint64_t* n_total = ctx->wal_offsets.p;
   uint64_t* local = ctx->wal_offsets.p + 1;
   uint64_t* part = ctx->wal_offsets.p + 1 + nblocks;
+  if (max_recs && ctx->wal_onepass) {
+    // the one-pass form: the window pass finishes the records that lie in one 16 KiB region, k_blocks the others
+    // (wal_offsets' last word: their count)
+    const uint64_t nreg = 2 * nblocks;
+    if ((rc = ctx->wal_rlcnt.ensure(nreg + 1)) || (rc = ctx->wal_rl.ensure(nreg * 8 + 1))) return rc;
+    uint64_t* n_kb = ctx->wal_offsets.p + 1 + nblocks + (nblocks + 63) / 64;
+    HIPCHK(lcrc_launch_wal_onepass(ctx->grid_a, ctx->wal_grid_b ? ctx->wal_grid_b : ctx->grid_b / LCRC_WAL_GRID_DIV,
+                                   file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local,
+                                   part, ctx->wal_rlcnt.p, ctx->wal_rl.p, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p,
+                                   max_recs, n_total, n_recs, n_kb, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout,
+                                   ctx->poly, ctx->wal_crcs.p, st));
+    return LCRC_OK;
+  }
   // One stream: the header walk (k_wal_parse, one lane per 32 KiB block following the 7-byte headers,
   // then k_wal_emit), the window pass over the whole file, then one k_blocks over all records (the log format stores
   // the raw crc: no mask) that also stores each record's crc and verdict.

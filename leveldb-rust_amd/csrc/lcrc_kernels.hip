@@ -793,6 +793,170 @@ __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, co
 }
 
 // ---------------------------------------------------------------------------------------------------
+// k_windows_wal: the one-pass WAL scan's window pass (lcrc_ctx_options.wal_onepass; log.rs:204-279). It is
+// k_windows<false> -- every 256 B window's raw value to `out`, for the records k_blocks still finishes -- that also
+// finishes the records k_wal_emit1 listed for each region (the ones whose covered bytes lie in the region, up to
+// WAL_RMAX), so that those never go through a second pass over the file:
+//  * a record's partial head and tail windows are re-read right after the refill loads of the same region are
+//    issued (the same lines: L2 hits, no second HBM read) and used one iteration later, after that region's walk:
+//    vector loads retire in issue order, so loads issued at the finish would wait behind the next region's
+//    sixteen refills;
+//  * the re-read window is walked masked -- bytes outside the record's [lo, hi) zeroed, the init register injected
+//    into its first bytes (walk(R, M) = walk(0, M ^ LE(R)) for |M| >= 4) -- by four lanes, 64 B each, joined with
+//    Z64 / Z128 from the replicated S1 set; a window masked at hi is walk(0, M || 0^(256 - hi)) = Z_{256-hi}(...);
+//  * the full windows between head and tail are folded from this wave's own window values (its LDS row) with
+//    Z256, and the trailing zero padding is undone by one GF(2) multiply with x^(-8 pad) (an LDS copy of TAB_INV).
+// The stored CRC comes in the list; the record's crc and verdict go to recs[o], as k_blocks stores them.
+// ---------------------------------------------------------------------------------------------------
+// a * b mod P, reflected (bit 31 = x^0): zlib's multmodp recurrence without branches
+__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; --i) {
+    p ^= b & (0u - ((a >> i) & 1u));
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+constexpr uint32_t WW_WAVES = A_THREADS / 64;
+constexpr uint32_t WAL_RMAX = 8;  // records per region finished by k_windows_wal (two boundary windows each: 16)
+
+// bytes [64 q, 64 q + 64) of the boundary window of lane (w4, q): w4 = slot 2k (record k's head window) or 2k + 1
+// (its tail window, when the record ends in another window); its mask [lo, hi) and whether it holds the start
+struct WalBnd {
+  u32x4 d[4];
+  uint32_t lo, hi;
+  bool on, head;
+};
+
+__device__ __forceinline__ void wal_bnd_load(WalBnd& B, const uint4& sl, uint32_t cnt, __amdgpu_buffer_rsrc_t rs,
+                                             uint32_t lane) {
+  const uint32_t w4 = lane >> 2, q = lane & 3, k = w4 >> 1, tail = w4 & 1;
+  const uint32_t se = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * k), (int)sl.y);
+  const uint32_t s = se & 0xFFFFu, e = se >> 16;
+  const uint32_t ws = s >> 8, we = (e - 1) >> 8;
+  B.on = k < cnt && (!tail || we != ws);
+  B.head = !tail;
+  B.lo = tail ? 0u : s & 255u;
+  B.hi = (tail || ws == we) ? ((e - 1) & 255u) + 1u : 256u;
+  const uint32_t off = 256u * (tail ? we : ws) + 64u * q;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) B.d[i] = B.on ? LCRC_REFILL(rs, off + 16 * i) : u32x4{0, 0, 0, 0};
+}
+
+// walk(0, window bytes [lo, hi) ^ injected init, zero elsewhere) of each boundary window, in lane 4 w4 of its group
+__device__ __forceinline__ uint32_t wal_bnd_walk(const void* L, const Rot& R, const WalBnd& B, uint32_t init,
+                                                 uint32_t lane) {
+  const uint32_t q = lane & 3;
+  const int lo = (int)B.lo - (int)(64 * q), hi = (int)B.hi - (int)(64 * q);  // chunk-relative
+  const uint32_t qn = B.hi - B.lo < 4 ? B.hi - B.lo : 4u;
+  const uint32_t rq = !B.head ? 0u : qn == 4 ? init : init & ((1u << (8 * qn)) - 1u);
+  uint32_t w[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const int kl = min(max(lo - 4 * d, 0), 4), kh = min(max(hi - 4 * d, 0), 4);
+    const uint32_t keep = (uint32_t)((1ull << (8 * kh)) - (1ull << (8 * kl)));
+    const int D = lo - 4 * d;  // where the record's first byte lies relative to this dword
+    const uint32_t inj = (D > -4 && D < 4) ? (uint32_t)((((uint64_t)rq) << 32) >> (32 - 8 * D)) : 0u;
+    w[d] = (B.d[d >> 2][d & 3] & keep) ^ inj;
+  }
+  uint32_t x = w[0];
+#pragma unroll
+  for (int d = 1; d < 16; ++d) x = step4x(L, R, x, w[d]);
+  x = step4x(L, R, x, 0u);
+  // chunks 0..3 of the window: Z64(c0) ^ c1, Z64(c2) ^ c3, then Z128 = Z64 o Z64
+  const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, false);  // row_shl:1
+  if ((q & 1) == 0) x = zrot<SET_S1>(L, R, x) ^ n1;
+  const uint32_t n2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x102, 0xF, 0xF, false);  // row_shl:2
+  if (q == 0) x = zrot<SET_S1>(L, R, zrot<SET_S1>(L, R, x)) ^ n2;
+  return x;
+}
+
+__global__ void __launch_bounds__(A_THREADS) k_windows_wal(const uint8_t* __restrict__ base, uint64_t span,
+                                                          uint64_t nreg, const uint32_t* __restrict__ gtab,
+                                                          uint32_t* __restrict__ out,
+                                                          const uint32_t* __restrict__ rl_cnt,
+                                                          const uint4* __restrict__ rl,
+                                                          lcrc_wal_rec_dev* __restrict__ recs, uint64_t max_recs,
+                                                          uint32_t init, uint32_t xorout, uint32_t poly) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
+  __shared__ uint32_t WV[WW_WAVES * 64];  // each wave's window values of its current region
+  __shared__ uint32_t INV[256];           // x^(-8 k) mod P, k < 256
+  __shared__ uint32_t wg_ticket;
+  WinOne src{base, span, nreg, out, 0, nullptr, nullptr};
+  const uint32_t lane = __lane_id();
+  const uint32_t tid = threadIdx.x;
+  const Share share = make_share(nreg);
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t voff_a = lane_voff<KW_LAY>(lane, 0), voff_b = lane_voff<KW_LAY>(lane, 1);
+  uint64_t t = share.region(wv);
+  // the first region's list, before its data (vector loads retire in issue order)
+  uint4 sl = make_uint4(0, 0, 0, 0);
+  if (t != NO_REGION && lane < WAL_RMAX) sl = rl[t * WAL_RMAX + lane];
+  uint32_t cnt = t != NO_REGION ? rl_cnt[t] : 0u;
+  u32x4 va[8], vb[8];
+  uint32_t ht;
+  const __amdgpu_buffer_rsrc_t rs0 = src.first(t, ht);
+  __builtin_amdgcn_sched_barrier(0);
+  load_half<KW_LAY>(va, rs0, voff_a);
+  __builtin_amdgcn_sched_barrier(0);
+  load_half<KW_LAY>(vb, rs0, voff_b);
+  __builtin_amdgcn_sched_barrier(0);
+  build_tables<true>(L, gtab, wv, lane, nullptr);
+  for (uint32_t i = tid; i < 256; i += A_THREADS) INV[i] = gtab[TAB_INV + i];
+  WalBnd B;
+  wal_bnd_load(B, sl, cnt, rs0, lane);  // the first region's boundary windows (the lines just requested)
+  if (tid == 0) wg_ticket = A_THREADS / 64;
+  lds_barrier();
+  const Rot R = make_rot(lane);
+  uint64_t tn = take_region(&wg_ticket, share, lane);
+  while (t != NO_REGION) {
+    const __amdgpu_buffer_rsrc_t rsn = src.rsrc(tn, 0);
+    // the next region's list, before its refills
+    uint4 sln = make_uint4(0, 0, 0, 0);
+    if (tn != NO_REGION && lane < WAL_RMAX) sln = rl[tn * WAL_RMAX + lane];
+    const uint32_t cntn = tn != NO_REGION ? rl_cnt[tn] : 0u;
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t x = walk_half<true, KW_LAY, false>(L, R, va, 0u, rsn, voff_a);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t tnn = take_region(&wg_ticket, share, lane);
+    const uint32_t p = walk_half<true, KW_LAY>(L, R, vb, x, rsn, voff_b);
+    const uint32_t wl = window_of_lane<KW_LAY>(lane);
+    out[t * 64 + wl] = p;
+    WV[wv * 64 + wl] = p;
+    // region t's listed records
+    const uint32_t m = wal_bnd_walk(L, R, B, init, lane);
+    const uint32_t mh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(32 * lane), (int)m);       // lane 8 k: head
+    const uint32_t mt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(32 * lane + 16), (int)m);  // lane 8 k + 4: tail
+    if (__builtin_amdgcn_ballot_w64(lane < cnt)) {
+      const uint32_t s = sl.y & 0xFFFFu, e = sl.y >> 16;
+      const uint32_t ws = s >> 8, we = (e - 1) >> 8;
+      const uint32_t nfull = we > ws ? we - ws - 1 : 0u;
+      uint32_t acc = mh;
+      for (uint32_t i = 0; __builtin_amdgcn_ballot_w64(lane < cnt && i < nfull); ++i)
+        if (i < nfull) acc = zlook(L, A_ZT, acc) ^ WV[wv * 64 + ws + 1 + i];
+      if (we != ws) acc = zlook(L, A_ZT, acc) ^ mt;
+      const uint32_t pad = 255u - ((e - 1) & 255u);
+      if (__builtin_amdgcn_ballot_w64(lane < cnt && pad != 0)) acc = pad ? gf_mul(INV[pad], acc, poly) : acc;
+      const uint32_t len = e - s;
+      if (len < 4) acc ^= init >> (8 * len);
+      const uint32_t crc = acc ^ xorout;
+      if (lane < cnt && sl.x < max_recs) {
+        recs[sl.x].crc = crc;
+        recs[sl.x].status = crc != sl.z ? 1 : 0;
+      }
+    }
+    // the next region's boundary windows: the lines its refills just requested
+    sl = sln;
+    cnt = cntn;
+    wal_bnd_load(B, sl, cnt, rsn, lane);
+    t = tn;
+    tn = tnn;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // k_blocks: one 16-lane row per range. LDS (40 KiB): T0..T3 [4 KiB], Z16..Z128 [16 KiB],
 // Z256..Z2048 [16 KiB], Z4096 [4 KiB], unreplicated (the hot loop is in k_windows).
 // The kernel is latency-bound (a few dependent memory round trips per range), so every load a range
@@ -954,7 +1118,9 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
   unsigned long long b_ph[4] = {0, 0, 0, 0};  // first iteration: loads landed, head walked, folded, tail walked
   uint32_t b_nit = 0;
 #endif
+  const uint64_t n_cap = n;  // the descriptor (and WAL record) capacity
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan)
+  if ((uint64_t)blockIdx.x * (B_THREADS / 16) >= n) return;  // no range for this workgroup: not even the table load
   const uint32_t lane = __lane_id();
   const uint32_t g = lane & 15, row = lane >> 4;
   const uint64_t wave = (uint64_t)blockIdx.x * (B_THREADS / 64) + (threadIdx.x >> 6);
@@ -1129,7 +1295,7 @@ __global__ void __launch_bounds__(B_THREADS) __attribute__((amdgpu_waves_per_eu(
         bad = bad || !exp_ok || expv != crc;
       }
       if (mismatch) mismatch_bit(mismatch, i, n, bad, flags);
-      if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
+      if (recs && ridx < n_cap) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
         recs[ridx].crc = crc;
         recs[ridx].status = bad ? 1 : 0;
       }
@@ -1173,16 +1339,6 @@ constexpr uint32_t R_SLOTS = 32;    // ranges shared by the rows of a workgroup 
 constexpr uint32_t R_KMAX = 4096;   // chunks of a shared range (x^(8 * 4096 * k) table); longer: private
 constexpr uint32_t R_OVF = 16;      // bytes past one full chunk walked at the end instead of a second chunk
 
-// a * b mod P, reflected (bit 31 = x^0): zlib's multmodp recurrence without branches
-__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
-  uint32_t p = 0;
-#pragma unroll
-  for (int i = 31; i >= 0; --i) {
-    p ^= b & (0u - ((a >> i) & 1u));
-    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
-  }
-  return p;
-}
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
@@ -1213,6 +1369,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
   const uint32_t tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t* __restrict__ xch = inv + 4097;  // x^(8 * 4096 * k) mod P, k < R_KMAX
+  const uint64_t n_cap = n;  // the descriptor (and WAL record) capacity
   if (n_dev) n = *n_dev < n ? *n_dev : n;  // count produced on the device (WAL scan, async table scan)
   if (blockIdx.x >= n) return;  // a grid sized by a bound: no range is dealt to this workgroup
   // A row's first range is its own ticket (the row index), and rows claim no shared chunk before they have
@@ -1509,7 +1666,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
         out[rng] = crc;
         const bool bad = oob || (has_exp && (!exp_ok || expv != crc));
         if (mismatch) mismatch_bit(mismatch, rng, n, bad, flags);
-        if (recs) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
+        if (recs && rng < n_cap) {  // WAL scan: the verdict of read_physical_record's checksum compare (log.rs:260-273)
           recs[rng].crc = crc;
           recs[rng].status = bad ? 1 : 0;
         }
@@ -1556,17 +1713,31 @@ __device__ __forceinline__ uint32_t wal_single(uint64_t b, uint32_t at, uint32_t
   return (s >> 8) == ((s + length) >> 8) ? 1u : 0u;  // last covered byte s + length
 }
 
+// The one-pass WAL scan (lcrc_ctx_options.wal_onepass): a record whose covered bytes lie in one 16 KiB region of the
+// file (one half of its 32 KiB log block) is finished by the window pass itself (k_windows_wal), up to WAL_RMAX per
+// region in file order; the others -- records across the middle of their log block, and a region's records past
+// WAL_RMAX -- go to k_blocks. wal_route decides it identically in the parse (counts) and the emit (slots).
+__device__ __forceinline__ bool wal_route(uint32_t at, uint32_t length, uint32_t& n0, uint32_t& n1, uint32_t& half) {
+  const uint32_t s = at + 6, e = at + 7 + length;  // covered bytes [s, e), block-relative
+  half = s >= 16384 ? 1u : 0u;
+  if (e <= 16384 && n0 < WAL_RMAX) return ++n0, true;
+  if (s >= 16384 && n1 < WAL_RMAX) return ++n1, true;
+  return false;
+}
+
+template <bool ONEPASS>
 __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file, uint64_t file_len,
                                                uint64_t nblocks, uint32_t* __restrict__ counts,
                                                uint2* __restrict__ slots, uint8_t* __restrict__ stops,
                                                uint64_t* __restrict__ local, uint64_t* __restrict__ part,
-                                               uint32_t bx) {
+                                               uint32_t bx, uint32_t* __restrict__ rl_cnt = nullptr) {
   const uint64_t b = (uint64_t)bx * 64 + threadIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint8_t* blk = file + b * 32768ull;
   const uint64_t rem = b < nblocks ? file_len - b * 32768ull : 0;
   const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
   uint32_t consumed = 0, nrec = 0, nsingle = 0, stop = LCRC_WAL_STOP_TRAILER_DEV;
+  uint32_t n0 = 0, n1 = 0;  // (ONEPASS) records finished by the window pass in each half of the block
   while (cap - consumed >= 7) {
     uint32_t length, type;
     // bytes 4..7 at the header inside the block: ONE dword load per hop (the length and type bytes), instead of
@@ -1588,11 +1759,24 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
       stop = LCRC_WAL_STOP_ZERO_DEV;
       break;
     }
-    const uint32_t one = wal_single(b, consumed, length);
-    if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | (one << 8));
+    uint32_t one, tag;
+    if constexpr (ONEPASS) {  // the high count: records for k_blocks; slot bits: 8 window pass, 9 half
+      uint32_t half;
+      const bool wp = wal_route(consumed, length, n0, n1, half);
+      one = wp ? 0u : 1u;
+      tag = (wp ? 1u << 8 : 0u) | (half << 9);
+    } else {  // the high count: one-window records
+      one = wal_single(b, consumed, length);
+      tag = one << 8;
+    }
+    if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | tag);
     ++nrec;
     nsingle += one;
     consumed += 7 + length;
+  }
+  if (ONEPASS && b < nblocks) {
+    rl_cnt[2 * b] = n0;
+    rl_cnt[2 * b + 1] = n1;
   }
   // wave exclusive scan by shuffles of (records | one-window records << 32)
   const uint64_t mine = (uint64_t)nrec | ((uint64_t)nsingle << 32);
@@ -1610,11 +1794,13 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
   if (lane == 63) part[bx] = inc;
 }
 
+template <bool ONEPASS>
 __global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
                                                   uint64_t nblocks, uint32_t* __restrict__ counts,
                                                   uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                                  uint64_t* __restrict__ local, uint64_t* __restrict__ part) {
-  wal_parse_body(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x);
+                                                  uint64_t* __restrict__ local, uint64_t* __restrict__ part,
+                                                  uint32_t* __restrict__ rl_cnt) {
+  wal_parse_body<ONEPASS>(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x, rl_cnt);
 }
 
 // several logs in one launch (lcrc_wal_scan_queue): log blockIdx.y, its parse workgroups blockIdx.x
@@ -1640,7 +1826,7 @@ struct WalJobsArg {
 __global__ void __launch_bounds__(64) k_wal_parse_q(const WalJobsArg jobs) {
   const WalJobDev& J = jobs.j[blockIdx.y];
   if ((uint64_t)blockIdx.x * WAL_PARTB >= J.nblocks) return;  // past this log's blocks (workgroup-uniform)
-  wal_parse_body(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
+  wal_parse_body<false>(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
 }
 
 // record o (file order) and its verify descriptor at position pos of k_blocks' order. The descriptor's
@@ -1675,6 +1861,16 @@ __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcr
 // by each emit workgroup) + local[b]. Descriptors: the one-window records first, then the others, each in file
 // order (both only when every record fits max_recs; else in file order). Workgroup 0 also writes the total
 // record count to n_total (device) and n_out (device or pinned host memory).
+// (ONEPASS) a record the window pass finishes: its slot in its region's list -- {record index, covered bytes
+// [s, e) relative to the region as s | e << 16, the stored CRC (header bytes 0..3)}
+__device__ __forceinline__ void wal_region_slot(const uint8_t* __restrict__ blk, uint4* __restrict__ rl, uint64_t b,
+                                                uint32_t half, uint32_t rank, uint64_t o, uint32_t at,
+                                                uint32_t length) {
+  const uint32_t s = at + 6 - 16384 * half, e = at + 7 + length - 16384 * half;
+  rl[(2 * b + half) * WAL_RMAX + rank] = make_uint4((uint32_t)o, s | (e << 16), load_le32(blk + at), 0u);
+}
+
+template <bool ONEPASS>
 __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, uint64_t nblocks,
                                               const uint32_t* __restrict__ counts,
                                               const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
@@ -1683,7 +1879,8 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
                                               lcrc_wal_rec_dev* __restrict__ recs,
                                               lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
                                               uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
-                                              uint32_t bx) {
+                                              uint32_t bx, uint4* __restrict__ rl = nullptr,
+                                              uint64_t* __restrict__ n_kb = nullptr) {
   const uint64_t g = (uint64_t)bx * blockDim.x + threadIdx.x;
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
@@ -1707,8 +1904,53 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
   if (bx == 0 && threadIdx.x == 0) {
     *n_total = tot_r;
     if (n_out) *n_out = tot_r;
+    if (ONEPASS) *n_kb = tot_s < max_recs ? tot_s : max_recs;  // the records k_blocks finishes
   }
   if (b >= nblocks || max_recs == 0) return;  // wave-uniform
+  if constexpr (ONEPASS) {
+    // file order as below; the window pass's records to their region's list, the others' descriptors packed in
+    // file order for k_blocks (the high counts are theirs)
+    const uint32_t cnt = counts[b];
+    const uint64_t loc = local[b];
+    const uint64_t first = (uint32_t)before + (uint32_t)loc;
+    const uint64_t first_kb = (before >> 32) + (loc >> 32);
+    uint2 sl = make_uint2(0, 0);
+    if (i < cnt) sl = slots[g];
+    const bool wp = (sl.y >> 8) & 1u;
+    const uint32_t hf = (sl.y >> 9) & 1u;
+    const uint64_t lt = (1ull << i) - 1;
+    const uint64_t kbm = __builtin_amdgcn_ballot_w64(i < cnt && !wp);
+    const uint64_t h0m = __builtin_amdgcn_ballot_w64(i < cnt && wp && hf == 0);
+    const uint64_t h1m = __builtin_amdgcn_ballot_w64(i < cnt && wp && hf == 1);
+    if (i >= cnt) return;
+    const uint8_t* blk = file + b * 32768ull;
+    uint32_t at = sl.x & 0xFFFFu, length = sl.x >> 16;
+    const uint64_t o = first + i;
+    if (wp) {
+      wal_region_slot(blk, rl, b, hf, __builtin_popcountll((hf ? h1m : h0m) & lt), o, at, length);
+      wal_put(recs, descs, o, ~0ull, max_recs, b * 32768ull + at, length, sl.y & 0xFFu, i + 1 == cnt, stops[b]);
+    } else {
+      wal_put(recs, descs, o, o < max_recs ? first_kb + __builtin_popcountll(kbm & lt) : ~0ull, max_recs,
+              b * 32768ull + at, length, sl.y & 0xFFu, i + 1 == cnt, stops[b]);
+    }
+    if (i == WAL_SLOTS - 1 && cnt > WAL_SLOTS) {  // the rest of a block with more records than slots, in order
+      uint32_t n0 = __builtin_popcountll(h0m), n1 = __builtin_popcountll(h1m);
+      uint64_t nk = __builtin_popcountll(kbm);
+      for (uint32_t j = WAL_SLOTS; j < cnt; ++j) {
+        at += 7 + length;
+        uint32_t type, half;
+        wal_header(blk, at, length, type);
+        const uint32_t r0 = n0, r1 = n1;
+        const bool wpj = wal_route(at, length, n0, n1, half);
+        const uint64_t oj = first + j;
+        if (wpj) wal_region_slot(blk, rl, b, half, half ? r1 : r0, oj, at, length);
+        wal_put(recs, descs, oj, wpj || oj >= max_recs ? ~0ull : first_kb + nk, max_recs, b * 32768ull + at, length,
+                type, j + 1 == cnt, stops[b]);
+        nk += wpj ? 0 : 1;
+      }
+    }
+    return;
+  }
   const bool split = tot_r <= max_recs;
   const uint32_t cnt = counts[b];
   const uint64_t loc = local[b];
@@ -1750,15 +1992,30 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
                                                   lcrc_wal_rec_dev* __restrict__ recs,
                                                   lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
                                                   uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out) {
-  wal_emit_body(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out, blockIdx.x);
+  wal_emit_body<false>(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out,
+                       blockIdx.x);
+}
+
+// the one-pass scan's emit: region lists for the window pass, packed k_blocks descriptors, their count in n_kb
+__global__ void __launch_bounds__(256) k_wal_emit1(const uint8_t* __restrict__ file, uint64_t nblocks,
+                                                   const uint32_t* __restrict__ counts,
+                                                   const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
+                                                   const uint64_t* __restrict__ local,
+                                                   const uint64_t* __restrict__ part,
+                                                   lcrc_wal_rec_dev* __restrict__ recs,
+                                                   lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
+                                                   uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
+                                                   uint4* __restrict__ rl, uint64_t* __restrict__ n_kb) {
+  wal_emit_body<true>(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out,
+                      blockIdx.x, rl, n_kb);
 }
 
 __global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
   const WalJobDev& J = jobs.j[blockIdx.y];
   // past this log's (block, slot) threads: workgroup 0 always runs (it writes the total)
   if (blockIdx.x && (uint64_t)blockIdx.x * 256 >= J.nblocks * WAL_SLOTS) return;
-  wal_emit_body(J.file, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, J.recs, J.descs, J.max_recs, J.n_total,
-                J.n_out, blockIdx.x);
+  wal_emit_body<false>(J.file, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, J.recs, J.descs, J.max_recs,
+                       J.n_total, J.n_out, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -4016,13 +4273,41 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  uint64_t* n_out, hipStream_t st) {
   const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
   if (nparts)
-    LCRC_LAUNCH(lcrc_dev::k_wal_parse, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
-                       slots, stops, local, part);
+    LCRC_LAUNCH(lcrc_dev::k_wal_parse<false>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks,
+                counts, slots, stops, local, part, nullptr);
   const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
   const uint64_t g = (nt + 255) / 256;
   LCRC_LAUNCH(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
                      stops, local, part, recs, descs, max_recs, n_total, n_out);
   return hipGetLastError();
+}
+
+// the one-pass WAL scan (lcrc_ctx_options.wal_onepass): header walk, emit (region lists + k_blocks descriptors), the
+// window pass that finishes the listed records, k_blocks over the rest (their count on the device, n_kb)
+hipError_t lcrc_launch_wal_onepass(int grid_a, int grid_b, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
+                                   uint32_t* counts, uint2* slots, uint8_t* stops, uint64_t* local, uint64_t* part,
+                                   uint32_t* rl_cnt, uint4* rl, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
+                                   uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, uint64_t* n_kb,
+                                   uint32_t* win, const uint32_t* gtab, uint32_t init, uint32_t xorout, uint32_t poly,
+                                   uint32_t* crcs, hipStream_t st) {
+  const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
+  if (nparts)
+    LCRC_LAUNCH(lcrc_dev::k_wal_parse<true>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
+                slots, stops, local, part, rl_cnt);
+  const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
+  const uint64_t g = (nt + 255) / 256;
+  LCRC_LAUNCH(lcrc_dev::k_wal_emit1, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
+              stops, local, part, recs, descs, max_recs, n_total, n_out, rl, n_kb);
+  if (max_recs == 0) return hipGetLastError();
+  const uint64_t nreg = (file_len + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
+  if (nreg) {
+    const uint64_t need = (nreg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
+    const int ga = (int)(need < (uint64_t)grid_a ? need : (uint64_t)grid_a);
+    LCRC_LAUNCH(lcrc_dev::k_windows_wal, dim3(ga), dim3(lcrc_dev::A_THREADS), 0, st, file, file_len, nreg, gtab, win,
+                rl_cnt, rl, recs, max_recs, init, xorout, poly);
+  }
+  return lcrc_launch_blocks(false, grid_b, file, file_len, descs, max_recs, 0, 0, nullptr, win, gtab, init, xorout, 0,
+                            crcs, nullptr, n_kb, recs, st);
 }
 
 // several logs' header walks and record emits, two launches (lcrc_wal_scan_queue); m <= MAX_WJOBS

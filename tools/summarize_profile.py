@@ -35,6 +35,16 @@ def counters(d, name):
     return per
 
 
+def stream_kernel(kernels):
+    """(name, stats) of the step's byte-streaming kernel: the k_windows* launch (every algorithmic byte passes through
+    it once); a config without one (the compressed table's decoders, the Snappy frames) falls back to the kernel with
+    the most time."""
+    win = [kv for kv in kernels.items() if kv[0].split("::")[-1].startswith("k_windows")]
+    if win:
+        return max(win, key=lambda kv: kv[1]["total_ns"])
+    return max(kernels.items(), key=lambda kv: kv[1]["total_ns"])
+
+
 def main(outdir, rnd, config, mode, committed=None, unprofiled=None):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -64,17 +74,23 @@ def main(outdir, rnd, config, mode, committed=None, unprofiled=None):
     if summary["kernels"] and os.path.exists(bj):
         with open(bj) as f:
             line = json.load(f)
-        dom = max(summary["kernels"].items(), key=lambda kv: kv[1]["total_ns"])
+        dom = stream_kernel(summary["kernels"])
         bpl = (line.get("roofline") or {}).get("bytes_per_launch")
         if bpl:
+            # `kernel` / `frac`: the byte-streaming kernel of the step (k_windows*: every algorithmic byte goes through
+            # it once), never merely the kernel with the most time (round 4 charged a WAL step's bytes to k_wal_parse)
             summary["kernel"] = dom[0]
+            summary["dominant_by_time"] = max(summary["kernels"].items(), key=lambda kv: kv[1]["total_ns"])[0]
             summary["avg_us"] = round(dom[1]["avg_ns"] / 1e3, 3)
             summary["bytes_per_launch"] = bpl
             summary["frac"] = round(bpl / dom[1]["avg_ns"] / 8000.0, 4)
-            # every kernel of the pipeline per dominant-kernel call (general path: k_windows + k_blocks, WAL:
-            # parse + emit + windows + blocks), for configs whose step is more than one kernel
+            summary["bound"] = (line.get("roofline") or {}).get("bound")
+            # every kernel of the pipeline per streaming-kernel call (general path: k_windows + k_blocks, WAL:
+            # parse + emit + windows + blocks), for configs whose step is more than one kernel, and the fraction of
+            # 8 TB/s the whole pipeline's kernel time implies
             summary["pipeline_us_per_call"] = round(
                 sum(k["total_ns"] for k in summary["kernels"].values()) / dom[1]["calls"] / 1e3, 3)
+            summary["frac_pipeline"] = round(bpl / (summary["pipeline_us_per_call"] * 1e3) / 8000.0, 4)
             summary["bench_line"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
                                      "frac": line["roofline"]["frac"], "launch_us": line["roofline"]["launch_us"],
                                      "launches": line["roofline"].get("launches"),
@@ -144,8 +160,8 @@ def main(outdir, rnd, config, mode, committed=None, unprofiled=None):
                                "agreement_profiled_run = frac_from_trace / the profiled run's own line frac")
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    # the dominant kernel's traffic for bench.py
-    dom = max(summary["kernels"].items(), key=lambda kv: kv[1]["total_ns"])[0] if summary["kernels"] else None
+    # the streaming kernel's traffic for bench.py, and the whole step's (every kernel's bytes per step)
+    dom = stream_kernel(summary["kernels"])[0] if summary["kernels"] else None
     hot = None
     for k in traffic:
         if dom and dom.split("<")[0] in k:
@@ -154,10 +170,15 @@ def main(outdir, rnd, config, mode, committed=None, unprofiled=None):
         hot = max(traffic, key=lambda k: traffic[k]["hbm_read_bytes_per_launch"])
     if hot:
         t = traffic[hot]
+        calls = {k: v["calls"] for k, v in summary["kernels"].items()}
+        per_step = calls.get(dom) or 1
+        step_rd = sum(v["hbm_read_bytes_per_launch"] * calls.get(k, 1) / per_step for k, v in traffic.items())
+        step_wr = sum(v["hbm_write_bytes_per_launch"] * calls.get(k, 1) / per_step for k, v in traffic.items())
         with open(os.path.join(prof, f"traffic_{config}_{mode}.json"), "w") as f:
             json.dump({"kernel": hot, "hbm_bytes_per_launch": t["hbm_read_bytes_per_launch"] + t["hbm_write_bytes_per_launch"],
                        "hbm_read_bytes_per_launch": t["hbm_read_bytes_per_launch"],
                        "hbm_write_bytes_per_launch": t["hbm_write_bytes_per_launch"],
+                       "step_hbm_read_bytes": step_rd, "step_hbm_write_bytes": step_wr,
                        "source": f"profiles/{tag}_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
                                  "FETCH_SIZE KiB x1024 x2 per the gfx950 correction)"}, f, indent=1)
     if summary.get("bench_line", {}).get("streams", 1) > 1 and "kernel" in summary:
