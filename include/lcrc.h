@@ -146,6 +146,7 @@ typedef struct lcrc_ctx_options {
   uint32_t ts_blocks_div; /* divisor of the table scan's range-pass grid (0: 1) */
   uint32_t wal_onepass;   /* 1: the WAL scan finishes the records that lie in one 16 KiB region inside its window pass
                              (k_windows_wal), k_blocks only the others (0: window pass + range pass over all) */
+  uint32_t ts_open_v1;    /* 1: the compressed index decoded by the one-wave k_ts_open (round 4) instead of k_ts_open2 */
 } lcrc_ctx_options;
 int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, const lcrc_ctx_options* opt);
 int lcrc_ctx_destroy(lcrc_ctx* ctx);

@@ -43,7 +43,8 @@ hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lc
                                 uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
                                 const uint64_t* iopen, hipStream_t s);
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uint32_t* tab_c, uint8_t* idec,
-                               uint64_t idec_cap, uint64_t* iopen, hipStream_t s);
+                               uint64_t idec_cap, uint64_t* iopen, uint32_t* scratch, hipStream_t s);
+uint64_t lcrc_ts_open_scratch_words();
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
                                const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t vcap, uint64_t bound, uint32_t gcap, const uint8_t* idec, uint64_t* iopen,
@@ -215,6 +216,8 @@ struct lcrc_ctx {
   DevBuf<lcrc_tscan_dev> ts_state;
   DevBuf<uint8_t> ts_idx;    // table scan: a Snappy-framed index block decoded on the device (k_ts_open)
   DevBuf<uint64_t> ts_open;  // k_ts_open's verdict words (zeroed when allocated)
+  DevBuf<uint32_t> ts_open_scr;  // k_ts_open2's per-workgroup source arrays (pointer jumping)
+  bool ts_open_v1 = false;       // lcrc_ctx_options.ts_open_v1: the one-wave k_ts_open instead
   DevBuf<lcrc_tblk_dev> ts_blocks;
   DevBuf<uint64_t> ts_count;
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
@@ -406,6 +409,7 @@ int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, con
     if (opt->ts_grid) ctx->ts_grid = opt->ts_grid;
     if (opt->ts_blocks_div) ctx->ts_blocks_div = (int)opt->ts_blocks_div;
     if (opt->size >= offsetof(lcrc_ctx_options, wal_onepass) + sizeof(uint32_t)) ctx->wal_onepass = opt->wal_onepass != 0;
+    if (opt->size >= offsetof(lcrc_ctx_options, ts_open_v1) + sizeof(uint32_t)) ctx->ts_open_v1 = opt->ts_open_v1 != 0;
   }
   *out = ctx;
   return LCRC_OK;
@@ -468,6 +472,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->ts_state.release();
   ctx->ts_idx.release();
   ctx->ts_open.release();
+  ctx->ts_open_scr.release();
   ctx->ts_blocks.release();
   ctx->ts_count.release();
   if (ctx->ts_host) (void)hipHostFree(ctx->ts_host);
@@ -1380,7 +1385,8 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
       (rc = ctx->tbl_crcs.ensure(nv)) || (rc = ctx->tbl_mm.ensure(nv / 32 + 1)) || (rc = ctx->tbl_frames.ensure(nb)) ||
       (rc = ctx->sn_nch.ensure(nb)) || (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) ||
       (rc = ctx->sn_status.ensure(nb)) || (rc = ctx->sn_out.ensure(decoded_cap + 16 * (decoded_cap / 4096 + 1) + 16)) ||
-      (rc = ctx->win.ensure(window_words(max_file_len))) || (rc = ctx->ts_idx.ensure(decoded_cap)))
+      (rc = ctx->win.ensure(window_words(max_file_len))) || (rc = ctx->ts_idx.ensure(decoded_cap)) ||
+      (!ctx->ts_open_v1 && (rc = ctx->ts_open_scr.ensure(lcrc_ts_open_scratch_words()))))
     return rc;
   if (!ctx->ts_open.p) {
     if ((rc = ctx->ts_open.ensure(4))) return rc;
@@ -1433,7 +1439,8 @@ int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
   // the index block's restart segments: entry counts, scanned per tile
   const bool sidx = flags & LCRC_TSCAN_SNAPPY_INDEX;
   if (sidx)
-    HIPCHK(lcrc_launch_ts_open(file, file_len, tab_c, ctx->ts_idx.p, ctx->ts_idx.cap, ctx->ts_open.p, st));
+    HIPCHK(lcrc_launch_ts_open(file, file_len, tab_c, ctx->ts_idx.p, ctx->ts_idx.cap, ctx->ts_open.p,
+                               ctx->ts_open_v1 ? nullptr : ctx->ts_open_scr.p, st));
   const uint64_t vcap = ts_verify_cap(cap, file_len);
   HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
                               ctx->ts_grid, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p, sidx ? ctx->ts_open.p : nullptr,

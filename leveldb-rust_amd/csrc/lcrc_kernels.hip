@@ -4021,6 +4021,473 @@ __global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file
   TO_STAMP(7);
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// k_ts_open2: k_ts_open with a 16-wave workgroup per index chunk (one wave per 64 KiB chunk left 29 CUs
+// decoding the bench table's index for 0.73 ms). The chunk's two-phase decode is made data-parallel end to end:
+//  A. every parse window (64 candidate element starts) gets, for each candidate, the element that would start there
+//     and -- by pointer jumping inside the window, five ds_bpermute rounds (elements are >= 2 bytes) -- the first
+//     start at or past the window's end reached from it (its exit; a malformed element on the way: none);
+//  B. one thread follows the real chain from window to window through those exits (one LDS read per window);
+//  C. each window's chain from its entry (the wave decoder's v_readlane walk): its element count and output bytes;
+//  D. exclusive scans of both over the windows;
+//  E. each window's element records and start bits at their global positions, with the wave decoder's validation;
+//  F. every output byte's source -- a literal's input byte, or an earlier output byte -- in a global scratch array,
+//     resolved by pointer jumping over the whole chunk (a copy of a copy of a copy: an index block's keys) until
+//     every source is a literal byte, then the bytes gathered;
+// then the chunk's masked CRC-32C with its 1 KiB passes spread over the waves and joined by one thread (Z1024), and
+// the copy-out. A chunk with more elements than the record area holds goes through the wave decoder (one wave).
+// ---------------------------------------------------------------------------------------------------
+constexpr uint32_t T2_THREADS = 1024, T2_WAVES = 16, T2_GRID = 32;
+constexpr uint32_t T2_ECAP = 6400;                 // element records (ea, eb)
+constexpr uint32_t T2_NWIN = (TO_IN + 63) / 64;     // parse windows of a staged chunk
+constexpr uint32_t T2_O_IN = 0, T2_O_OUT = TO_IN + SN_SLACK, T2_O_BM = T2_O_OUT + TO_OUT, T2_O_E = T2_O_BM + TO_BM;
+constexpr uint32_t T2_O_WCNT = T2_O_E + 8 * T2_ECAP, T2_O_WOUT = T2_O_WCNT + ((4 * T2_NWIN + 15) & ~15u);
+constexpr uint32_t T2_O_WENT = T2_O_WOUT + ((4 * T2_NWIN + 15) & ~15u);
+constexpr uint32_t T2_O_PASS = T2_O_WENT + ((2 * T2_NWIN + 15) & ~15u), T2_O_CTL = T2_O_PASS + 256;
+constexpr uint32_t T2_LDS = T2_O_CTL + 64;
+static_assert(T2_NWIN * 64 * 2 <= TO_OUT + TO_BM, "the exit table: the output area and the head of the bitmap");
+static_assert(8 * T2_ECAP >= TD_TAB_WORDS * 4, "the record area holds the CRC tables afterwards");
+static_assert(4 * T2_NWIN >= 2 * 1024, "the window counts' area holds the per-block start counts");
+static_assert(T2_LDS <= 163840 && T2_O_OUT % 16 == 0 && T2_O_E % 16 == 0 && T2_O_PASS % 16 == 0, "k_ts_open2's LDS");
+enum { T2_FAIL = 0, T2_NE = 1, T2_NOUT = 2, T2_CRC = 3, T2_DONE = 4, T2_TYPE = 5, T2_Q = 6, T2_AT = 7, T2_ULEN = 8,
+       T2_WANT = 9, T2_OCLO = 10, T2_OCHI = 11, T2_OK = 12, T2_LEN = 13 };
+constexpr uint32_t T2_FIN = 0x80000000u;  // scratch: the source is a literal input byte (else an output position)
+
+// the element that would start at in[i] (i < qe + 64: the staging's slack), as the wave decoder decodes it
+struct SnCand {
+  uint32_t typ, hdr, outlen, a, size;
+  bool good;
+};
+__device__ __forceinline__ SnCand sn_cand(const lds_u8* in, uint32_t i, uint32_t qe) {
+  SnCand c;
+  const uint32_t t = in[i], b1 = in[i + 1], b2 = in[i + 2], b3 = in[i + 3], b4 = in[i + 4];
+  c.typ = t & 3;
+  const uint32_t room = qe > i ? qe - i : 0;
+  if (c.typ == 0) {
+    const uint32_t L = t >> 2;
+    const uint32_t nb = L >= 60 ? L - 59 : 0;
+    const uint32_t ext = b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+    const uint32_t lm1 = nb ? (nb == 4 ? ext : ext & ((1u << (8 * nb)) - 1)) : L;
+    c.hdr = 1 + nb;
+    c.outlen = lm1 + 1;
+    c.a = i + c.hdr;
+    c.good = room >= c.hdr && lm1 < room - c.hdr && (nb == 0 || room >= 5);  // (as snappy_wave_decode)
+  } else {
+    c.hdr = c.typ == 1 ? 2 : c.typ == 2 ? 3 : 5;
+    c.outlen = c.typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
+    c.a = c.typ == 1 ? ((t >> 5) << 8) | b1 : c.typ == 2 ? b1 | (b2 << 8) : b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+    c.good = room >= c.hdr;
+  }
+  c.size = c.typ == 0 ? c.hdr + c.outlen : c.hdr;
+  return c;
+}
+
+// the chain of real element starts of a window from its entry (lanes >= lim: past the input's end)
+__device__ __forceinline__ uint64_t sn_chain(uint32_t nxt, uint32_t en, uint32_t lim) {
+  uint64_t mask = 0;
+  uint32_t cur = en;
+  while (cur < lim) {
+    mask |= 1ull << cur;
+    cur = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)cur);
+  }
+  return mask;
+}
+
+// the value of 1 KiB pass k of the chunk CRC (td_chunk_crc's loop body): lane 0 of the wave gets it
+template <bool FROM_LDS>
+__device__ __forceinline__ uint32_t td_pass(const uint32_t* T, const uint8_t* src, uint32_t k, uint32_t pad, uint32_t q,
+                                            uint32_t lane) {
+  const uint32_t g = lane & 15;
+  const uint32_t x0 = 1024 * k + 16 * lane;
+  u32x4 w;
+  if constexpr (FROM_LDS) {
+    w = *(const u32x4*)(src + x0);
+  } else {
+    if (x0 >= pad) {
+      w = *(const u32x4_ua*)(src + (x0 - pad));
+    } else {
+      w = u32x4{0, 0, 0, 0};
+      if (x0 + 16 > pad)
+        for (uint32_t b = pad - x0; b < 16; ++b) w[b >> 2] |= (uint32_t)src[x0 + b - pad] << (8 * (b & 3));
+    }
+  }
+  w = td_inject(w, x0, pad, q);
+  uint32_t cv = step4(T, 0u, w.x);
+  cv = step4(T, cv, w.y);
+  cv = step4(T, cv, w.z);
+  cv = step4(T, cv, w.w);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t pn = row_down(cv, m);
+    if ((g & ((2u << m) - 1)) == 0) cv = zl(T, TAB_ZPIECE + m * 1024, cv) ^ pn;
+  }
+  const uint32_t r0 = __builtin_amdgcn_readlane(cv, 0), r1 = __builtin_amdgcn_readlane(cv, 16);
+  const uint32_t r2 = __builtin_amdgcn_readlane(cv, 32), r3 = __builtin_amdgcn_readlane(cv, 48);
+  const uint32_t a = zl(T, TAB_ZWIN, r0) ^ r1, b = zl(T, TAB_ZWIN, r2) ^ r3;
+  return zl(T, TAB_ZWIN + 1024, a) ^ b;
+}
+
+// the raw CRC-32C of a chunk (ulen bytes: V = 0^pad || M in LDS, or M in global memory), every wave its passes,
+// thread 0 joining them (Z1024); needs the tables in T and every thread of the workgroup
+template <bool FROM_LDS>
+__device__ __forceinline__ uint32_t t2_chunk_crc(const uint32_t* T, const uint8_t* src, uint32_t ulen, uint32_t* passv,
+                                                 uint32_t* ctl, uint32_t tid) {
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  const uint32_t np = (ulen + 1023) >> 10, pad = (np << 10) - ulen, q = ulen < 4 ? ulen : 4u;
+  for (uint32_t k = wv; k < np; k += T2_WAVES) {
+    const uint32_t v = td_pass<FROM_LDS>(T, src, k, pad, q, lane);
+    if (lane == 0) passv[k] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = np ? passv[0] : 0u;
+    for (uint32_t k = 1; k < np; ++k) acc = zl(T, TAB_ZWIN + 2048, acc) ^ passv[k];
+    if (ulen < 4) acc ^= ulen ? 0xFFFFFFFFu >> (8 * ulen) : 0xFFFFFFFFu;
+    ctl[T2_CRC] = acc ^ 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  return ctl[T2_CRC];
+}
+
+// the chunk's elements in[q0, qe) decoded into o[0, ulen) by the whole workgroup (A-F above). 1 decoded, 0 malformed,
+// 2 more elements than T2_ECAP. S: this workgroup's scratch (ulen words).
+__device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, lds_u8* o, uint32_t ulen, uint8_t* L,
+                                  uint32_t* __restrict__ S, uint32_t tid) {
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  typedef __attribute__((address_space(3))) uint16_t lds_u16;
+  lds_u16* const xt = (lds_u16*)(L + T2_O_OUT);
+  lds_u32* const bm = (lds_u32*)(L + T2_O_BM);
+  lds_u32* const ea = (lds_u32*)(L + T2_O_E);
+  lds_u32* const eb = ea + T2_ECAP;
+  lds_u32* const wcnt = (lds_u32*)(L + T2_O_WCNT);
+  lds_u32* const wout = (lds_u32*)(L + T2_O_WOUT);
+  lds_u16* const went = (lds_u16*)(L + T2_O_WENT);
+  lds_u32* const ctl = (lds_u32*)(L + T2_O_CTL);
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  const uint32_t nw = (qe - q0 + 63) >> 6;
+  // A: exits
+  for (uint32_t w = wv; w < nw; w += T2_WAVES) {
+    const uint32_t base = q0 + 64 * w, lim = qe - base < 64 ? qe - base : 64u;
+    const SnCand c = sn_cand(in, base + lane, qe);
+    uint32_t p = lane >= lim ? lane : c.good ? lane + c.size : 0x7FFFu;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const uint32_t pj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((p < lim ? p : lane) * 4), (int)p);
+      if (p < lim) p = pj;
+    }
+    xt[w * 64 + lane] = p == 0x7FFFu ? (uint16_t)0xFFFF : (uint16_t)(base + p);
+  }
+  if (tid == 0) ctl[T2_FAIL] = 0;
+  __syncthreads();
+  // B: entries
+  if (tid == 0) {
+    uint32_t pos = q0, bad = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+      const uint32_t base = q0 + 64 * w;
+      uint32_t en = 0xFFFFu;
+      if (!bad && pos < qe && pos < base + 64) {
+        en = pos - base;
+        const uint32_t x = xt[w * 64 + en];
+        if (x == 0xFFFFu) bad = 1;
+        else pos = x;
+      }
+      went[w] = (uint16_t)en;
+    }
+    ctl[T2_FAIL] = bad || pos != qe;
+  }
+  __syncthreads();
+  if (ctl[T2_FAIL]) return 0;
+  // C: counts and output bytes per window
+  for (uint32_t w = wv; w < nw; w += T2_WAVES) {
+    const uint32_t en = went[w];
+    uint32_t cnt = 0, out = 0;
+    if (en != 0xFFFFu) {
+      const uint32_t base = q0 + 64 * w, lim = qe - base < 64 ? qe - base : 64u;
+      const SnCand c = sn_cand(in, base + lane, qe);
+      const uint32_t nxt = c.good ? lane + c.size : 0x7FFFFFFFu;
+      const uint64_t mask = sn_chain(nxt, en, lim);
+      const bool sel = (mask >> lane) & 1;
+      cnt = (uint32_t)__builtin_popcountll(mask);
+      out = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(sel ? c.outlen : 0u, lane), 63);
+    }
+    if (lane == 0) {
+      wcnt[w] = cnt;
+      wout[w] = out;
+    }
+  }
+  __syncthreads();
+  // D: exclusive scans over the windows (wave 0: nine windows per lane)
+  if (wv == 0) {
+    uint32_t lane9 = lane * 9;
+    __asm__ volatile("" : "+v"(lane9));  // (computed here: hoisted out of the chunk loop, its nine addresses spill)
+    uint32_t sc = 0, so = 0;
+    for (uint32_t j = 0; j < 9; ++j) {
+      const uint32_t w = lane9 + j;
+      if (w < nw) {
+        sc += wcnt[w];
+        so += wout[w];
+      }
+    }
+    const uint32_t ic = wave_incl_scan(sc, lane), io = wave_incl_scan(so, lane);
+    uint32_t ec = ic - sc, eo = io - so;
+    for (uint32_t j = 0; j < 9; ++j) {
+      const uint32_t w = lane9 + j;
+      if (w < nw) {
+        const uint32_t c = wcnt[w], u = wout[w];
+        wcnt[w] = ec;
+        wout[w] = eo;
+        ec += c;
+        eo += u;
+      }
+    }
+    if (lane == 63) {
+      ctl[T2_NE] = ic;
+      ctl[T2_NOUT] = io;
+    }
+  }
+  __syncthreads();
+  if (ctl[T2_NOUT] != ulen) return 0;
+  if (ctl[T2_NE] > T2_ECAP) return 2;
+  // the start bitmap (its head held the end of the exit table), whole 64-bit blocks
+  const uint32_t nblk = (ulen + 63) >> 6;
+  for (uint32_t k = tid; k < 2 * nblk; k += T2_THREADS) bm[k] = 0;
+  __syncthreads();
+  // E: records and start bits
+  for (uint32_t w = wv; w < nw; w += T2_WAVES) {
+    const uint32_t en = went[w];
+    if (en == 0xFFFFu) continue;
+    const uint32_t base = q0 + 64 * w, lim = qe - base < 64 ? qe - base : 64u;
+    const SnCand c = sn_cand(in, base + lane, qe);
+    const uint32_t nxt = c.good ? lane + c.size : 0x7FFFFFFFu;
+    const uint64_t mask = sn_chain(nxt, en, lim);
+    const bool sel = (mask >> lane) & 1;
+    const uint32_t v = sel ? c.outlen : 0u;
+    const uint32_t wpos = wout[w] + wave_incl_scan(v, lane) - v;
+    const bool bad = sel && (wpos > ulen || c.outlen > ulen - wpos || (c.typ != 0 && (c.a == 0 || c.a > wpos)));
+    if (__builtin_amdgcn_ballot_w64(bad)) {
+      if (lane == 0) ctl[T2_FAIL] = 1;
+      continue;
+    }
+    if (sel) {
+      const uint32_t k = wcnt[w] + (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1));
+      ea[k] = wpos | ((c.outlen - 1) << 16);  // (wpos < ulen <= 65536, outlen <= 65536)
+      eb[k] = c.typ == 0 ? (c.a | T2_FIN) : c.a;
+      __hip_atomic_fetch_or((uint32_t*)&bm[wpos >> 5], 1u << (wpos & 31), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  if (ctl[T2_FAIL]) return 0;
+  // F1: element starts before each 64-byte block (one thread per block; the counts' area reused)
+  lds_u16* const bpre = (lds_u16*)wcnt;
+  {
+    const uint32_t b = tid;
+    const uint32_t c = b < nblk ? (uint32_t)(__builtin_popcount(bm[2 * b]) + __builtin_popcount(bm[2 * b + 1])) : 0u;
+    const uint32_t inc = wave_incl_scan(c, lane);
+    if (lane == 63) wout[wv] = inc;  // the waves' totals (wout is free)
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t k = 0; k < wv; ++k) before += wout[k];
+    __syncthreads();
+    if (b < nblk) bpre[b] = (uint16_t)(before + inc - c);
+  }
+  __syncthreads();
+  // F2: sources
+  uint64_t todo = 0;
+#pragma unroll 1  // (unrolled, the 64 per-thread addresses are hoisted out of the chunk loop and spill)
+  for (uint32_t i = 0; i < 64; ++i) {
+    const uint32_t x = tid + T2_THREADS * i;
+    if (x >= ulen) break;
+    const uint32_t b = x >> 6, l = x & 63;
+    const uint64_t m = ((uint64_t)bm[2 * b + 1] << 32) | bm[2 * b];
+    const uint32_t e = bpre[b] + (uint32_t)__builtin_popcountll(m & ((2ull << l) - 1)) - 1;
+    const uint32_t A = ea[e], B = eb[e];
+    const uint32_t ew = A & 0xFFFFu, elen = (A >> 16) + 1, off = x - ew;
+    uint32_t src;
+    if (B & T2_FIN) {
+      src = T2_FIN | ((B & ~T2_FIN) + off);
+    } else {
+      const uint32_t per = B < elen ? B : 0u;  // (a copy is at most 64 bytes long: off < 64)
+      src = per ? ew - B + small_mod(off, per) : x - B;
+      todo |= 1ull << i;
+    }
+    S[x] = src;
+  }
+  __syncthreads();
+  // F3: pointer jumping (S[x] <- S[S[x]]) until every source is a literal's input byte
+  while (__syncthreads_or(todo != 0)) {
+#pragma unroll 1
+    for (uint32_t i0 = 0; i0 < 64; i0 += 8) {
+      if (!((todo >> i0) & 0xFF)) continue;
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = ((todo >> (i0 + j)) & 1) ? S[tid + T2_THREADS * (i0 + j)] : 0u;
+      uint32_t u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = ((todo >> (i0 + j)) & 1) ? S[v[j]] : 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((todo >> (i0 + j)) & 1) {
+          S[tid + T2_THREADS * (i0 + j)] = u[j];
+          if (u[j] & T2_FIN) todo &= ~(1ull << (i0 + j));
+        }
+    }
+  }
+  // F4: the bytes, at o[0, ulen)
+#pragma unroll 1
+  for (uint32_t i = 0; i < 64; ++i) {
+    const uint32_t x = tid + T2_THREADS * i;
+    if (x >= ulen) break;
+    o[x] = in[S[x] & ~T2_FIN];
+  }
+  __syncthreads();
+  return 1;
+}
+
+__global__ void __launch_bounds__(T2_THREADS) k_ts_open2(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                        const uint32_t* __restrict__ tab_c, uint8_t* __restrict__ idec,
+                                                        uint64_t idec_cap, uint64_t* __restrict__ iopen,
+                                                        uint32_t* __restrict__ scratch) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t t2_lds[];
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  uint8_t* const lin = t2_lds + T2_O_IN;
+  uint8_t* const lout = t2_lds + T2_O_OUT;
+  uint32_t* const T = (uint32_t*)(t2_lds + T2_O_E);
+  uint32_t* const passv = (uint32_t*)(t2_lds + T2_O_PASS);
+  lds_u32* const ctl = (lds_u32*)(t2_lds + T2_O_CTL);
+  uint32_t* const S = scratch + (uint64_t)blockIdx.x * 65536;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  // the footer's index handle and the framing walk, by wave 0 (as k_ts_open)
+  if (tid < 64) {
+    uint64_t io = 0, is = 0;
+    bool framed = false;
+    if (file_len >= 48) {
+      const uint8_t* f = file + file_len - 48;
+      const uint64_t magic = (uint64_t)load_le32(f + 40) | ((uint64_t)load_le32(f + 44) << 32);
+      uint64_t mo, ms;
+      uint32_t p = magic == 0xdb4775248b80fb57ull ? dev_varint<64>(f, 0, 48, &mo) : ~0u;
+      if (p != ~0u) p = dev_varint<64>(f, p, 48, &ms);
+      if (p != ~0u) p = dev_varint<64>(f, p, 48, &io);
+      if (p != ~0u) p = dev_varint<64>(f, p, 48, &is);
+      framed = p != ~0u && io <= file_len && is + 5 <= file_len - io && is + 1 <= 0x7FFFFFFFull && file[io + is] == 1;
+    }
+    uint64_t total = 0, chunks = 0, padded;
+    uint32_t mi, mo;
+    const bool ok = framed && snappy_frame_size(file + io, (uint32_t)is, total, chunks, mi, mo, padded);
+    const bool fits = total <= idec_cap;
+    if (blockIdx.x == 0 && lane == 0) {
+      iopen[1] = ok ? total : 0;
+      iopen[0] = (framed ? 1u : 0u) | (ok && fits ? 2u : 0u) | (ok && !fits ? 4u : 0u);
+    }
+    if (lane == 0) {
+      ctl[T2_OK] = ok && fits && blockIdx.x < chunks;
+      ctl[T2_OCLO] = (uint32_t)io;
+      ctl[T2_OCHI] = (uint32_t)(io >> 32);
+      ctl[T2_LEN] = (uint32_t)is;
+    }
+  }
+  __syncthreads();
+  if (!ctl[T2_OK]) return;  // (uniform)
+  const uint8_t* const p = file + ((uint64_t)ctl[T2_OCHI] << 32 | ctl[T2_OCLO]);
+  const uint32_t len = ctl[T2_LEN];
+  uint32_t at = 0, k = 0;  // (thread 0) the framing walk's position and data-chunk count
+  uint64_t o = 0;
+  bool good = true;  // (thread 0)
+  while (true) {
+    __syncthreads();
+    if (tid == 0) {
+      ctl[T2_DONE] = 1;
+      while (at < len) {  // the next data chunk of this workgroup (the framing is good: snappy_frame_size)
+        const uint32_t type = ld_u8(p + at);
+        const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
+        const uint32_t body = at + 4;
+        at = body + cl;
+        if (type > 1) continue;
+        uint32_t ulen = cl - 4, q = body + 4;
+        if (type == 0) {
+          uint32_t used = 0;
+          snappy_preamble([&](uint32_t i) { return ld_u8(p + q + i); }, at - q, ulen, used);
+          q += used;
+        }
+        const uint64_t oc = o;
+        o += ulen;
+        if (k++ % gridDim.x != blockIdx.x) continue;
+        ctl[T2_DONE] = 0;
+        ctl[T2_TYPE] = type;
+        ctl[T2_Q] = q;
+        ctl[T2_AT] = at;
+        ctl[T2_ULEN] = ulen;
+        ctl[T2_WANT] = ld_u8(p + body) | (ld_u8(p + body + 1) << 8) | (ld_u8(p + body + 2) << 16) |
+                       ((uint32_t)ld_u8(p + body + 3) << 24);
+        ctl[T2_OCLO] = (uint32_t)oc;
+        ctl[T2_OCHI] = (uint32_t)(oc >> 32);
+        break;
+      }
+    }
+    __syncthreads();
+    if (ctl[T2_DONE]) break;
+    const uint32_t type = ctl[T2_TYPE], q = ctl[T2_Q], ae = ctl[T2_AT], ulen = ctl[T2_ULEN], want = ctl[T2_WANT];
+    const uint64_t oc = (uint64_t)ctl[T2_OCHI] << 32 | ctl[T2_OCLO];
+    const uint32_t pad = ((ulen + 1023) & ~1023u) - ulen;
+    uint32_t crc = 0;
+    bool cok = true;
+    if (type == 1) {  // uncompressed: checksummed where it lies, copied out
+      stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, tid, T2_THREADS);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      crc = t2_chunk_crc<false>(T, p + q, ulen, passv, (uint32_t*)ctl, tid);
+      for (uint32_t x = tid; x < ulen; x += T2_THREADS) idec[oc + x] = p[q + x];
+    } else if (ae - q + 4 > TO_IN) {  // too large for the staging: lane-serial in the workspace, checksummed there
+      if (tid == 0) {
+        uint64_t oo = oc;
+        ctl[T2_FAIL] = !sn_serial_decode(p + q, p + ae, idec, oo, oc + ulen);
+      }
+      __threadfence_block();
+      __syncthreads();
+      cok = !ctl[T2_FAIL];
+      stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, tid, T2_THREADS);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      if (cok) crc = t2_chunk_crc<false>(T, idec + oc, ulen, passv, (uint32_t*)ctl, tid);
+    } else {
+      const uint8_t* zs = p + q;
+      const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
+      const uint32_t ndw = (d + (ae - q) + 3) >> 2;
+      stage_to_lds((const uint32_t*)(zs - d), (lds_u8*)lin, ndw, tid, T2_THREADS);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      uint32_t r = sn_par_decode((const lds_u8*)lin, d, d + (ae - q), (lds_u8*)(lout + pad), ulen, t2_lds, S, tid);
+      if (r == 2) {  // more elements than the records hold: the wave decoder, on wave 0
+        if (tid < 64) {
+          const bool w_ok = snappy_wave_decode(lin, d, d + (ae - q), lout + pad, ulen, lane);
+          if (lane == 0) ctl[T2_FAIL] = !w_ok;
+        }
+        __syncthreads();
+        r = ctl[T2_FAIL] ? 0u : 1u;
+      }
+      cok = r == 1;
+      if (cok) {
+        for (uint32_t x = 16 * tid; x < pad; x += 16 * T2_THREADS) *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
+        stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, tid, T2_THREADS);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        crc = t2_chunk_crc<true>(T, lout, ulen, passv, (uint32_t*)ctl, tid);
+        const uint8_t* src = lout + pad;
+        uint32_t x0 = 0;
+        if (((oc | pad) & 15) == 0) {  // whole 16 B pieces, then the tail byte by byte
+          x0 = ulen & ~15u;
+          for (uint32_t x = 16 * tid; x < x0; x += 16 * T2_THREADS) *(u32x4*)(idec + oc + x) = *(const u32x4*)(src + x);
+        }
+        for (uint32_t x = x0 + tid; x < ulen; x += T2_THREADS) idec[oc + x] = src[x];
+      }
+    }
+    if (tid == 0) good = good && cok && mask32c(crc) == want;
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  if (tid == 0 && !good) iopen[2] = 1;  // (every writer stores the same 1)
+}
 }  // namespace lcrc_dev
 
 // ---------------------------------------------------------------------------------------------------
@@ -4177,14 +4644,25 @@ hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lc
   return hipGetLastError();
 }
 // a Snappy-framed index block decoded into idec (k_ts_open); 64 one-wave workgroups
+// scratch: T2_GRID x 65,536 words (k_ts_open2's pointer-jumping sources); nullptr: the one-wave k_ts_open
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uint32_t* tab_c, uint8_t* idec,
-                               uint64_t idec_cap, uint64_t* iopen, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_open,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::TO_LDS);
-  if (attr != hipSuccess) return attr;
-  LCRC_LAUNCH(lcrc_dev::k_ts_open, dim3(64), dim3(64), lcrc_dev::TO_LDS, s, file, file_len, tab_c, idec, idec_cap, iopen);
+                               uint64_t idec_cap, uint64_t* iopen, uint32_t* scratch, hipStream_t s) {
+  if (!scratch) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_open,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::TO_LDS);
+    if (attr != hipSuccess) return attr;
+    LCRC_LAUNCH(lcrc_dev::k_ts_open, dim3(64), dim3(64), lcrc_dev::TO_LDS, s, file, file_len, tab_c, idec, idec_cap,
+                iopen);
+    return hipGetLastError();
+  }
+  static const hipError_t attr2 = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_open2,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::T2_LDS);
+  if (attr2 != hipSuccess) return attr2;
+  LCRC_LAUNCH(lcrc_dev::k_ts_open2, dim3(lcrc_dev::T2_GRID), dim3(lcrc_dev::T2_THREADS), lcrc_dev::T2_LDS, s, file,
+              file_len, tab_c, idec, idec_cap, iopen, scratch);
   return hipGetLastError();
 }
+uint64_t lcrc_ts_open_scratch_words() { return (uint64_t)lcrc_dev::T2_GRID * 65536; }
 hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
                                const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t vcap, uint64_t bound, uint32_t gcap, const uint8_t* idec, uint64_t* iopen,

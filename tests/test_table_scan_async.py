@@ -467,3 +467,25 @@ def test_async_snappy_index_graph_replay(lcrc, orc):
             eng.graph_destroy(g)
         s.close()
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("v1", [0, 1])
+def test_async_snappy_index_decoders_agree(lcrc, orc, v1):
+    """The compressed index through k_ts_open2 (16 waves per chunk, the default) and the round-4 one-wave k_ts_open
+    (context option ts_open_v1): a multi-chunk index, clean and with a chunk that does not decode, the oracle's
+    result either way."""
+    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_open_v1=v1)
+    try:
+        f, blocks = orc.table_build(_seq_kvs(40000), block_size=128, compression=1)
+        off, size, _ = _index_block(f, blocks)
+        assert len(orc.snappy_frame_decode(f[off:off + size])) > 3 * 65536
+        assert _expect_async(lcrc, eng, orc, f, cap=len(blocks) + 4, snappy_index=True) == OK
+        g = bytearray(f)
+        g[off + size // 2] ^= 0x04
+        g[off + size + 1:off + size + 5] = orc.crc(bytes(g[off:off + size + 1]), 0).to_bytes(4, "little")
+        assert _expect_async(lcrc, eng, orc, bytes(g), cap=len(blocks) + 4, snappy_index=True) in (OK, CORRUPT, HOST)
+        got, err = _sync(lcrc, eng, bytes(g), None)
+        assert err == orc.table_scan_expect(bytes(g))[1]
+    finally:
+        eng.close()
