@@ -2066,7 +2066,10 @@ constexpr uint32_t SN_MAX = 16384;
 // staging TD_IN + TD_OUT made of the wave's four row areas); a chunk too large for that, lane-serially to the workspace.
 constexpr uint32_t TD_WAVES = 4;
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
-constexpr uint32_t TR_IN = 3008 + 16;    // a row's frame (+ the slack of its element-header reads)
+// a row's frame (+ the slack of its element-header reads): frames up to 2,701 B (db_bench-style 4 KiB blocks: <= 2,298).
+// Round 4 staged 3,008 B, which made the workgroup's LDS 163.6 KB: no room for the other stream's small scan kernels
+// (k_ts_index 344 B, k_ts_finish 4 KiB), which then waited for whole decode workgroups to retire
+constexpr uint32_t TR_IN = 2704 + 16;
 constexpr uint32_t TR_OUT = 5120;        // a row's decoded chunk (V: a multiple of 1 KiB)
 constexpr uint32_t TR_ROW_LDS = TR_IN + 16 + TR_OUT;
 constexpr uint32_t TD_WAVE_LDS = 4 * TR_ROW_LDS;
@@ -2076,7 +2079,7 @@ static_assert(TD_OUT % 1024 == 0, "the chunk CRC reads V in whole 1 KiB passes")
 static_assert(TR_OUT % 1024 == 0 && TR_ROW_LDS % 16 == 0, "row staging");
 static_assert(TD_IN + SN_SLACK + TD_OUT <= TD_WAVE_LDS, "the wave staging is the wave's row areas");
 constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
-static_assert(TD_LDS <= 163840, "k_ts_decode's LDS");
+static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish and k_ts_index");
 
 // `slow`: the decoded bytes (16-aligned) of the compressed chunks too large for k_ts_decode's LDS staging (TD_IN
 // compressed, TD_OUT decoded), which it decodes lane-serially into the table scan's workspace

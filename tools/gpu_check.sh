@@ -14,7 +14,12 @@ tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_fixed.json 2> gpurun_out/bench_fixed.err || { tail -20 gpurun_out/bench_fixed.err; exit 1; }
 cat gpurun_out/bench_fixed.json
 for c in ${CONFIGS:-mixed wal table tablez}; do
-  BC="--config $c"; [ "$c" = tablez ] && BC="--config table --compression 1"
+  case "$c" in
+    tablez) BC="--config table --compression 1" ;;
+    tablezv1) BC="--config table --compression 1 --engine-opt ts_open_v1=1" ;;
+    walop) BC="--config wal --engine-opt wal_onepass=1" ;;
+    *) BC="--config $c" ;;
+  esac
   timeout -k 10 300 python -u bench.py $BC > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || { tail -20 gpurun_out/bench_$c.err; exit 1; }
   cut -c1-1500 gpurun_out/bench_$c.json
 done

@@ -22,7 +22,12 @@ fi
 for c in $CONFIGS; do
   timeout -k 10 900 bash tools/profile_round.sh $R $c c > "$OUT/prof_$c.log" 2>&1 || { tail -20 "$OUT/prof_$c.log"; exit 1; }
   python3 -c "import json;s=json.load(open('profiles/${R}_${c}_c_summary.json'));print('$c profile:', s.get('kernel'), s.get('avg_us'), s.get('trace_launch_us'), 'agreement (profiled run)', s.get('agreement_profiled_run'))"
-  BC="--config $c"; [ "$c" = tablez ] && BC="--config table --compression 1"
+  case "$c" in
+    tablez) BC="--config table --compression 1" ;;
+    tablezv1) BC="--config table --compression 1 --engine-opt ts_open_v1=1" ;;
+    walop) BC="--config wal --engine-opt wal_onepass=1" ;;
+    *) BC="--config $c" ;;
+  esac
   timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 $BC --extra-out "$OUT/bench_${c}_full.json" > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }
   cut -c1-300 "$OUT/bench_$c.json"
   # the committed line is the profiled run's own line (the trace reproduces it); the un-profiled run of the same
