@@ -937,7 +937,9 @@ def main(argv=None):
         "pct_hbm_peak": round(100.0 * (w.nbytes * args.steps * world / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
         "per_gpu": per_gpu,
     }
-    prof_config = args.config + ("z" if args.compression else "")  # profiles/ tag (tablez: the compressed table)
+    # profiles/ tag (tablez: the compressed table; walop: the one-pass WAL scan; tablezv1: the round-4 index decoder)
+    prof_config = args.config + ("z" if args.compression else "") + \
+        ("op" if args.engine_opts.get("wal_onepass") else "") + ("v1" if args.engine_opts.get("ts_open_v1") else "")
     if timers and gpu_ms:
         one_stream = len(timers) == 1 and not w.per_step_sync
         launch_s = gpu_ms / 1e3 / cov_launches

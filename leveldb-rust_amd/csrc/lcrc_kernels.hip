@@ -4472,7 +4472,14 @@ __global__ void __launch_bounds__(T2_THREADS) k_ts_open2(const uint8_t* __restri
       }
       cok = r == 1;
       if (cok) {
-        for (uint32_t x = 16 * tid; x < pad; x += 16 * T2_THREADS) *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
+        // V[0, pad) zeroed for the CRC passes -- exactly: the output already starts at pad, which need not be 16-aligned
+        for (uint32_t x = 16 * tid; x < pad; x += 16 * T2_THREADS) {
+          if (x + 16 <= pad) {
+            *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
+          } else {
+            for (uint32_t b = x; b < pad; ++b) lout[b] = 0;
+          }
+        }
         stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, tid, T2_THREADS);
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
