@@ -1717,9 +1717,15 @@ __device__ __forceinline__ uint32_t wal_single(uint64_t b, uint32_t at, uint32_t
 // file (one half of its 32 KiB log block) is finished by the window pass itself (k_windows_wal), up to WAL_RMAX per
 // region in file order; the others -- records across the middle of their log block, and a region's records past
 // WAL_RMAX -- go to k_blocks. wal_route decides it identically in the parse (counts) and the emit (slots).
-__device__ __forceinline__ bool wal_route(uint32_t at, uint32_t length, uint32_t& n0, uint32_t& n1, uint32_t& half) {
+// Two more exclusions, both cases k_windows_wal cannot walk from its boundary windows: a record whose last bytes lie in
+// the file's last partial dword (the buffer range check returns a dword only when it lies wholly inside the file), and
+// a multi-window record with fewer than 4 bytes in its head window (the init register is injected into its first 4).
+__device__ __forceinline__ bool wal_route(uint32_t at, uint32_t length, uint64_t b, uint64_t file_len, uint32_t& n0,
+                                          uint32_t& n1, uint32_t& half) {
   const uint32_t s = at + 6, e = at + 7 + length;  // covered bytes [s, e), block-relative
   half = s >= 16384 ? 1u : 0u;
+  const bool single = (s >> 8) == ((e - 1) >> 8);
+  if (b * 32768ull + e > (file_len & ~3ull) || (!single && (s & 255) > 252)) return false;
   if (e <= 16384 && n0 < WAL_RMAX) return ++n0, true;
   if (s >= 16384 && n1 < WAL_RMAX) return ++n1, true;
   return false;
@@ -1762,7 +1768,7 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
     uint32_t one, tag;
     if constexpr (ONEPASS) {  // the high count: records for k_blocks; slot bits: 8 window pass, 9 half
       uint32_t half;
-      const bool wp = wal_route(consumed, length, n0, n1, half);
+      const bool wp = wal_route(consumed, length, b, file_len, n0, n1, half);
       one = wp ? 0u : 1u;
       tag = (wp ? 1u << 8 : 0u) | (half << 9);
     } else {  // the high count: one-window records
@@ -1880,7 +1886,7 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
                                               lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
                                               uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
                                               uint32_t bx, uint4* __restrict__ rl = nullptr,
-                                              uint64_t* __restrict__ n_kb = nullptr) {
+                                              uint64_t* __restrict__ n_kb = nullptr, uint64_t file_len = 0) {
   const uint64_t g = (uint64_t)bx * blockDim.x + threadIdx.x;
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
@@ -1941,7 +1947,7 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
         uint32_t type, half;
         wal_header(blk, at, length, type);
         const uint32_t r0 = n0, r1 = n1;
-        const bool wpj = wal_route(at, length, n0, n1, half);
+        const bool wpj = wal_route(at, length, b, file_len, n0, n1, half);
         const uint64_t oj = first + j;
         if (wpj) wal_region_slot(blk, rl, b, half, half ? r1 : r0, oj, at, length);
         wal_put(recs, descs, oj, wpj || oj >= max_recs ? ~0ull : first_kb + nk, max_recs, b * 32768ull + at, length,
@@ -1997,7 +2003,7 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
 }
 
 // the one-pass scan's emit: region lists for the window pass, packed k_blocks descriptors, their count in n_kb
-__global__ void __launch_bounds__(256) k_wal_emit1(const uint8_t* __restrict__ file, uint64_t nblocks,
+__global__ void __launch_bounds__(256) k_wal_emit1(const uint8_t* __restrict__ file, uint64_t file_len, uint64_t nblocks,
                                                    const uint32_t* __restrict__ counts,
                                                    const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
                                                    const uint64_t* __restrict__ local,
@@ -2007,7 +2013,7 @@ __global__ void __launch_bounds__(256) k_wal_emit1(const uint8_t* __restrict__ f
                                                    uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
                                                    uint4* __restrict__ rl, uint64_t* __restrict__ n_kb) {
   wal_emit_body<true>(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out,
-                      blockIdx.x, rl, n_kb);
+                      blockIdx.x, rl, n_kb, file_len);
 }
 
 __global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
@@ -4784,7 +4790,7 @@ hipError_t lcrc_launch_wal_onepass(int grid_a, int grid_b, const uint8_t* file, 
                 slots, stops, local, part, rl_cnt);
   const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
   const uint64_t g = (nt + 255) / 256;
-  LCRC_LAUNCH(lcrc_dev::k_wal_emit1, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
+  LCRC_LAUNCH(lcrc_dev::k_wal_emit1, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, file_len, nblocks, counts, slots,
               stops, local, part, recs, descs, max_recs, n_total, n_out, rl, n_kb);
   if (max_recs == 0) return hipGetLastError();
   const uint64_t nreg = (file_len + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
