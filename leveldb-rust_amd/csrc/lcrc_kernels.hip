@@ -3465,78 +3465,104 @@ __device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 
-// One Snappy chunk per row: the elements in[q, qe) decoded into o[0, ulen) (both the row's LDS staging). Every row
-// walks its own chain -- one element per iteration, its header a broadcast read of the row's staging -- and executes
-// it 16 bytes per lane pass (all of an element's reads before its writes: a literal's bytes, or earlier output; a copy
-// shorter-offset than it is long repeats its last `a` bytes, j mod a). Validation as the wave decoder's. Rows with
-// active = false only ride along. Returns the row's verdict (output ends exactly at ulen).
-__device__ __forceinline__ bool row_snappy_decode(const lds_u8* in, uint32_t q, uint32_t qe, lds_u8* o, uint32_t ulen,
-                                                  bool active, uint32_t g, lds_u8* dump) {
+// a select of two computed values (clang emits `c ? a : b` with non-trivial arms as a branch, which the optimiser
+// then keeps, sinking the arms' work into it: exec-mask juggling in a divergent loop)
+__device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
+
+// One Snappy chunk per row: the elements B[q, qe) decoded into B[OB, OB + ulen) (both in the row's LDS staging, B
+// its base). Every row walks its own chain -- one element per iteration, its header two dwords of the row's staging
+// read one element ahead (its position is known once the previous header is decoded; the input is never written) --
+// and decodes the header without branches (selects only: the round-4 decoder's divergent if/else cost more SALU exec
+// juggling than VALU work). An element is moved in destination-aligned dwords, 8 B per lane and 128 B per row pass:
+// each lane reads the three aligned dwords holding its 8 source bytes and funnel-shifts them (v_alignbyte); the row's
+// first dword keeps the bytes before the element from the dword already there; the bytes a row's last dword writes
+// past the element are overwritten by the next element's (in order: a wave's LDS operations execute in issue order),
+// and V's end is dword-aligned, so nothing past it is touched. A copy whose source overlaps its own destination
+// closer than a pass (offset < length, offset < 128: the Snappy repeat) goes bytewise, j mod offset. Validation as
+// the wave decoder's. Rows with active = false only ride along. Returns the row's verdict (output ends at ulen).
+__device__ __forceinline__ bool row_snappy_decode(lds_u8* B, uint32_t q, uint32_t qe, uint32_t OB, uint32_t ulen,
+                                                  bool active, uint32_t g, uint32_t dump) {
+  typedef __attribute__((address_space(3))) uint32_t lds_w32;
   uint32_t w = 0;
   bool ok = true;
-  // an element's header (5 bytes from in[q]): two dword reads; the next element's is issued before this one's bytes
-  // are moved (its position is known once this header is decoded; the input is never written), so the chain pays one
-  // LDS latency per element instead of two
-  auto header = [&](uint32_t at) {
+  uint32_t h0, h1, hs;
+  auto fetch = [&](uint32_t at) {
     const uint32_t ba = at & ~3u;
-    const uint32_t d0 = *(lds_cu32*)(in + ba), d1 = *(lds_cu32*)(in + ba + 4);
-    return (((uint64_t)d1 << 32) | d0) >> (8 * (at & 3));
+    h0 = *(lds_cu32*)(B + ba);
+    h1 = *(lds_cu32*)(B + ba + 4);
+    hs = at & 3;
   };
-  uint64_t x = header(active && q < qe ? q : 0u);
-  while (true) {
-    const bool live = active && ok && q < qe;
-    if (!__builtin_amdgcn_ballot_w64(live)) break;
-    const uint32_t qq = live ? q : 0u;
-    const uint32_t t = (uint32_t)x & 0xFFu, ext = (uint32_t)(x >> 8);
-    const uint32_t typ = t & 3, room = live ? qe - q : 0u;
-    uint32_t hdr, outlen, a;
-    bool good;
-    if (typ == 0) {
-      const uint32_t L = t >> 2;
-      const uint32_t nb = L >= 60 ? L - 59 : 0;
-      const uint32_t lm1 = nb ? (nb == 4 ? ext : ext & ((1u << (8 * nb)) - 1)) : L;
-      hdr = 1 + nb;
-      outlen = lm1 + 1;
-      a = qq + hdr;
-      good = room >= hdr && lm1 < room - hdr && (nb == 0 || room >= 5);  // (as snappy_wave_decode)
-    } else {
-      hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
-      outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
-      a = typ == 1 ? ((t >> 5) << 8) | (ext & 0xFFu) : typ == 2 ? (ext & 0xFFFFu) : ext;
-      good = room >= hdr;
+  fetch(active && q < qe ? q : 0u);
+  bool live = active && q < qe;
+  const uint32_t gmask = g == 0 ? ~0u : 0u;  // the row's first lane merges the element's first dword
+  // the first header waited for here, so the loop's own wait (for the next header, issued with the element's
+  // source reads) is the only one per element: never one for the writes of the element before
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  // one LDS round trip per element: the next header, the dword the element's first write merges with and the pass-0
+  // source dwords are issued together and waited for together; the writes are never waited for (only ordered)
+  while (__builtin_amdgcn_ballot_w64(live)) {
+    const uint32_t lo = __builtin_amdgcn_alignbyte(h1, h0, hs);                         // bytes q .. q + 3
+    const uint32_t ext = sel(hs == 3, h1, __builtin_amdgcn_alignbyte(h1, h0, hs + 1));  // bytes q + 1 .. q + 4
+    const uint32_t t = lo & 0xFFu, typ = t & 3, L = t >> 2;
+    const uint32_t room = qe - q;  // (q >= qe: live = false, nothing below counts)
+    // (bitwise & | on the conditions and selects of computed values: no short-circuit branches)
+    const bool lit = typ == 0, c1 = typ == 1, c2 = typ == 2;
+    // literal: L < 60: length L + 1; else L - 59 little-endian bytes of length - 1 follow the tag
+    const uint32_t nb = sel(L >= 60, L - 59, 0u);
+    const uint32_t lbits = __builtin_amdgcn_ubfe(ext, 0, 8 * nb);  // (nb = 4: width 32 reads as 0, selected away)
+    const uint32_t lm1 = sel(nb == 4, ext, sel(nb == 0, L, lbits));
+    // copies: 1-byte offset (tag bits 5..7 = offset bits 8..10, length 4..11), 2-byte, 4-byte offset
+    const uint32_t o1 = ((t >> 5) << 8) | (ext & 0xFFu), o2 = ext & 0xFFFFu;
+    const uint32_t off = sel(c1, o1, sel(c2, o2, ext));
+    const uint32_t hdr = sel(lit, 1 + nb, (0x5320u >> (4 * typ)) & 0xFu);  // 1 + nb | 2 | 3 | 5
+    const uint32_t n = sel(lit, lm1 + 1, sel(c1, 4 + (L & 7), L + 1));
+    const bool good = (room >= hdr) & (!lit | ((lm1 < room - hdr) & ((nb == 0) | (room >= 5))));
+    const bool bad = live & (!good | (n > ulen - w) | (!lit & ((off == 0) | (off > w))));  // (w <= ulen holds)
+    ok = ok & !bad;
+    const bool ex = live & !bad;
+    const uint32_t m = sel(ex, n, 0u);
+    const uint32_t qn = sel(ex, q + hdr + sel(lit, n, 0u), q);
+    fetch(qn);  // (qn <= qe: the 8 bytes from qe & ~3 lie in the row's input staging and its slack)
+    const uint32_t D = OB + w, S = sel(lit, q + hdr, D - off);
+    const bool pat = !lit & (off < m) & (off < 128);
+    const uint32_t mm = sel(pat, 0u, m), Da = D & ~3u, sh = D & 3u;
+    const uint32_t old = *(lds_cu32*)(B + Da);
+    // pass 0 (every row; a row with nothing to move writes at most the merged dword back: V's end is dword-aligned,
+    // so a finished row has sh = 0 and writes nothing; a repeat's merged dword is rewritten by its bytewise moves)
+    const int r0 = (int)(8 * g) - (int)sh;  // element-relative offset of the lane's first dword
+    const uint32_t sa = S + (uint32_t)r0, A = sa & ~3u, al = sa & 3u;
+    const uint32_t d0 = *(lds_cu32*)(B + A), d1 = *(lds_cu32*)(B + A + 4), d2 = *(lds_cu32*)(B + A + 8);
+    const uint32_t keep = ((1u << (8 * sh)) - 1) & gmask;  // (sh = 0: nothing kept)
+    const uint32_t v0 = (__builtin_amdgcn_alignbyte(d1, d0, al) & ~keep) | (old & keep);
+    const uint32_t v1 = __builtin_amdgcn_alignbyte(d2, d1, al);
+    const uint32_t a0 = Da + 8 * g;
+    *(lds_w32*)(B + sel(r0 < (int)mm, a0, dump)) = v0;
+    *(lds_w32*)(B + sel(r0 + 4 < (int)mm, a0 + 4, dump)) = v1;
+    if (__builtin_amdgcn_ballot_w64(sh + mm > 128)) {  // literals longer than a pass (copies: at most 64 B)
+      for (uint32_t b = 128; __builtin_amdgcn_ballot_w64(b < sh + mm); b += 128) {
+        const int r = (int)(b + 8 * g) - (int)sh;
+        const uint32_t sb = S + (uint32_t)r, Ab = sb & ~3u, ab = sb & 3u;
+        const uint32_t e0 = *(lds_cu32*)(B + Ab), e1 = *(lds_cu32*)(B + Ab + 4), e2 = *(lds_cu32*)(B + Ab + 8);
+        *(lds_w32*)(B + sel(r < (int)mm, Da + b + 8 * g, dump)) = __builtin_amdgcn_alignbyte(e1, e0, ab);
+        *(lds_w32*)(B + sel(r + 4 < (int)mm, Da + b + 8 * g + 4, dump)) = __builtin_amdgcn_alignbyte(e2, e1, ab);
+      }
     }
-    const bool bad = live && (!good || w > ulen || outlen > ulen - w || (typ != 0 && (a == 0 || a > w)));
-    if (bad) ok = false;
-    const bool ex = live && !bad;
-    const uint32_t n = ex ? outlen : 0u;
-    const bool fin = typ == 0;
-    const uint32_t per = (!fin && a < outlen) ? a : 0u;
-    const uint32_t sa = fin ? a : w - a;
-    const uint32_t qn = ex ? q + (fin ? hdr + outlen : hdr) : q;
-    x = header(qn < qe ? qn : 0u);
-    // (the pattern modulus only when some row copies a pattern: most iterations skip its VALU work)
-    const bool any_per = __builtin_amdgcn_ballot_w64(per != 0) != 0;
-    for (uint32_t b0 = 0; __builtin_amdgcn_ballot_w64(b0 < n); b0 += 64) {  // 64 bytes: four passes, reads first
+    if (__builtin_amdgcn_ballot_w64(pat)) {  // (pat: a copy, m <= 64)
       uint32_t v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t j = b0 + 16 * i + g;
-        uint32_t jj = j;
-        if (any_per) jj = per ? small_mod(j, per) : j;  // (per: a copy, n <= 64)
-        const uint32_t idx = j < n ? sa + jj : 0u;
-        v[i] = (fin ? in : (const lds_u8*)o)[idx];  // one read from whichever area holds the bytes
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t j = 4 * g + k;
+        v[k] = pat ? B[S + small_mod(j, off)] : 0u;
       }
-      // every lane stores (no exec-mask juggling): the lanes past the element into the slack byte after the row's
-      // input, which only ever feeds header reads past the input's end (never used)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t j = b0 + 16 * i + g;
-        lds_u8* const dst = j < n ? o + w + j : dump;
-        *dst = (uint8_t)v[i];
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t j = 4 * g + k;
+        B[pat && j < m ? D + j : dump] = (uint8_t)v[k];
       }
     }
     q = qn;
-    w += n;
+    w += m;
+    live = ex & (qn < qe);
   }
   return ok && w == ulen;
 }
@@ -3634,7 +3660,7 @@ __device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bo
     bool ok = true;
     if (__builtin_amdgcn_ballot_w64(have && type == 1))  // uncompressed: copied to V + pad
       for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += 16) o[pad + k] = in[q + k];
-    ok = row_snappy_decode(in, q, next, o + pad, ulen, have && type == 0, g, (lds_u8*)in + TR_IN + 15) ||
+    ok = row_snappy_decode(in, q, next, (uint32_t)(o - in) + pad, ulen, have && type == 0, g, TR_IN + 12) ||
          !(have && type == 0);
     const uint32_t crc = row_chunk_crc(T, o, ulen, have, g, lane);
     if (have) {

@@ -1,0 +1,131 @@
+"""Snappy element coverage of the whole-table scan's row decoder (k_ts_decode's row_snappy_decode): every element
+form the snap crate's decoder accepts (snap "1", the decompressor behind src/sstable/format.rs:194-206) at every
+destination alignment -- literals with 0..4 length bytes (minimal and not), 1-, 2- and 4-byte-offset copies, copies
+overlapping their own output (offset < length: the repeat), copies closer than a 128 B pass and farther, literals
+longer than a pass -- plus invalid streams (offset past the output, output past the preamble's length, a header cut
+by the end). Frames are sized for the row staging (<= 2,701 B compressed, <= 5,120 B decoded), stored as the data
+blocks of one table, and the device scan's verdict on each block must equal the oracle's read_block_from_file.
+
+The generator's own decode of each valid stream is checked against the oracle first (CPU), so the cases are what
+they claim to be.
+"""
+import numpy as np
+import pytest
+
+from test_snappy_snap_rules import STREAM, _chunk, _varu, frames_table
+from test_table_scan import _as_tuples
+
+
+def _lit_el(data, nb):
+    n = len(data)
+    if nb == 0:
+        return bytes([(n - 1) << 2]) + data
+    return bytes([(59 + nb) << 2]) + (n - 1).to_bytes(nb, "little") + data
+
+
+def _copy_el(off, n, kind):
+    if kind == 1:  # 1-byte offset: length 4..11, offset < 2048
+        return bytes([((off >> 8) << 5) | ((n - 4) << 2) | 1, off & 0xFF])
+    if kind == 2:
+        return bytes([((n - 1) << 2) | 2]) + off.to_bytes(2, "little")
+    return bytes([((n - 1) << 2) | 3]) + off.to_bytes(4, "little")
+
+
+def gen_stream(rng, target, lit_max=300):
+    """(payload after the preamble, decoded bytes or None): random elements until about `target` decoded bytes. None:
+    an extended-length literal's tag is followed by fewer than 4 bytes (snap reads its length as one 4-byte word)."""
+    out = bytearray()
+    pay = bytearray()
+    ext_tag = -1
+    while len(out) < target:
+        r = rng.random()
+        if not out or r < 0.35:
+            n = int(rng.choice([rng.integers(1, 9), rng.integers(50, 71), rng.integers(120, 140),
+                                rng.integers(1, lit_max + 1)]))
+            alphabet = int(rng.choice([2, 16, 256]))
+            data = bytes(rng.integers(0, alphabet, n, dtype=np.uint8))
+            nmin = 0 if n <= 60 else 1 if n <= 256 else 2
+            nb = int(rng.integers(nmin, 5)) if rng.random() < 0.3 else nmin
+            if nb:
+                ext_tag = len(pay)
+            pay += _lit_el(data, nb)
+            out += data
+            continue
+        kind = int(rng.choice([1, 2, 4]))
+        n = int(rng.integers(4, 12)) if kind == 1 else int(rng.integers(1, 65))
+        w = len(out)
+        lim = min(w, 2047 if kind == 1 else 65535)
+        pick = rng.random()
+        if pick < 0.3:
+            off = int(rng.integers(1, min(n, lim) + 1))        # overlapping its own output (or touching it)
+        elif pick < 0.6:
+            off = int(rng.integers(min(n, lim), min(130, lim) + 1))  # within a pass
+        else:
+            off = int(rng.integers(1, lim + 1))
+        pay += _copy_el(off, n, kind)
+        for _ in range(n):
+            out.append(out[-off])
+    return bytes(pay), (bytes(out) if ext_tag < 0 or len(pay) - ext_tag - 1 >= 4 else None)
+
+
+def _frame(orc, payload, decoded, ulen=None):
+    pre = _varu(len(decoded) if ulen is None else ulen, 2)
+    return STREAM + _chunk(orc, 0, pre + payload, decoded)
+
+
+def row_cases(orc, seed=11, count=160):
+    """[(frame, decoded or None)]: valid random streams (some frames with two chunks) and invalid ones."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    while len(cases) < count:
+        target = int(rng.choice([1, 7, 64, 129, 1000, 3000, 4096, 4700]))
+        pay, dec = gen_stream(rng, target, lit_max=int(rng.choice([60, 300])))
+        if dec is None:
+            continue
+        fr = _frame(orc, pay, dec)
+        if len(fr) > 2701 or len(dec) > 5120:
+            continue
+        r = rng.random()
+        if r < 0.1 and len(dec) > 10:  # a second chunk
+            pay2, dec2 = gen_stream(rng, 200)
+            fr2 = _frame(orc, pay2, dec2 or b"")[len(STREAM):]
+            if dec2 is not None and len(fr) + len(fr2) <= 2701:
+                cases.append((fr + fr2, dec + dec2))
+                continue
+        if r < 0.2:  # output past the preamble's length
+            cases.append((_frame(orc, pay, dec, ulen=len(dec) - 1), None))
+        elif r < 0.27:  # a copy reaching before the output's start
+            cases.append((_frame(orc, pay + _copy_el(len(dec) + 1, 4, 2), dec + b"\0" * 4), None))
+        elif r < 0.32:  # a header cut by the stream's end
+            cases.append((_frame(orc, pay + b"\x02\x01", dec), None))
+        elif r < 0.36:  # a wrong chunk CRC
+            fr = bytearray(fr)
+            fr[len(STREAM) + 4] ^= 1
+            cases.append((bytes(fr), None))
+        else:
+            cases.append((fr, dec))
+    return cases
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_row_cases_match_oracle(orc, lcrc, seed):
+    """The generator's decode is the oracle's (so each case is the element mix it claims), and the host decoder's."""
+    for fr, want in row_cases(orc, seed):
+        assert orc.snappy_frame_decode(fr) == want
+        assert lcrc.snappy_frame_decode(fr) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_row_decoder_elements(lcrc, orc, engines, seed):
+    from test_table_scan import _scan
+    from test_table_scan_async import _expect_async
+    cases = row_cases(orc, seed)
+    f = frames_table(orc, [fr for fr, _ in cases])
+    want, werr = orc.table_scan_expect(f)
+    assert werr is None
+    assert [w[4] for w in want if w[2] == 0] == [0 if d is not None else 3 for _, d in cases]
+    eng = engines[lcrc.MODE_REF]
+    assert _expect_async(lcrc, eng, orc, f) == 0
+    got, err = _scan(lcrc, eng, f)
+    assert err is None and _as_tuples(got) == want

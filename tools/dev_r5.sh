@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/dev5
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail 10 --timeout 120 --timeout-method thread ${@} > $O/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail 10 --timeout 120 --timeout-method thread "$@" > $O/pytest.log 2>&1
 rc=$?
 tail -15 $O/pytest.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc   # (1: test failures; anything else: a crash or timeout -- stop)
