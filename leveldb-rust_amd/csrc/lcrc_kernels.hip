@@ -4088,6 +4088,19 @@ static_assert(T2_LDS <= 163840 && T2_O_OUT % 16 == 0 && T2_O_E % 16 == 0 && T2_O
 enum { T2_FAIL = 0, T2_NE = 1, T2_NOUT = 2, T2_CRC = 3, T2_DONE = 4, T2_TYPE = 5, T2_Q = 6, T2_AT = 7, T2_ULEN = 8,
        T2_WANT = 9, T2_OCLO = 10, T2_OCHI = 11, T2_OK = 12, T2_LEN = 13 };
 constexpr uint32_t T2_FIN = 0x80000000u;  // scratch: the source is a literal input byte (else an output position)
+#ifdef LCRC_PROBE_CLOCK  // diagnostic build: k_ts_open2's phase stamps (thread 0, s_memrealtime, 100 MHz)
+#define T2_STAMP(i)                                                                                 \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) {                                                    \
+      __builtin_amdgcn_s_waitcnt(0);                                                                \
+      lcrc_dbg_stamp[(3072 + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();            \
+    }                                                                                               \
+  } while (0)
+#else
+#define T2_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 // the element that would start at in[i] (i < qe + 64: the staging's slack), as the wave decoder decodes it
 struct SnCand {
@@ -4187,8 +4200,8 @@ __device__ __forceinline__ uint32_t t2_chunk_crc(const uint32_t* T, const uint8_
 
 // the chunk's elements in[q0, qe) decoded into o[0, ulen) by the whole workgroup (A-F above). 1 decoded, 0 malformed,
 // 2 more elements than T2_ECAP. S: this workgroup's scratch (ulen words).
-__device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, lds_u8* o, uint32_t ulen, uint8_t* L,
-                                  uint32_t* __restrict__ S, uint32_t tid) {
+__device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, uint32_t ulen, uint8_t* L,
+                                  uint16_t* __restrict__ S, uint8_t* __restrict__ dst, uint32_t tid) {
   typedef __attribute__((address_space(3))) uint32_t lds_u32;
   typedef __attribute__((address_space(3))) uint16_t lds_u16;
   lds_u16* const xt = (lds_u16*)(L + T2_O_OUT);
@@ -4215,24 +4228,75 @@ __device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, ld
   }
   if (tid == 0) ctl[T2_FAIL] = 0;
   __syncthreads();
-  // B: entries
-  if (tid == 0) {
-    uint32_t pos = q0, bad = 0;
-    for (uint32_t w = 0; w < nw; ++w) {
+  T2_STAMP(2);
+  // B: entries, over super-windows of 16 windows (the serial walk over every window cost 40 us a chunk):
+  //  B1: for each super-window and each entry offset e in its first window, the exit reached through its windows
+  //      (lane e of a wave, 16 dependent LDS reads); the records area is free until E
+  const uint32_t nsw = (nw + 15) >> 4;
+  lds_u32* const swx = ea;
+  lds_u32* const swent = ea + 64 * ((T2_NWIN + 15) / 16);
+  for (uint32_t sw = wv; sw < nsw; sw += T2_WAVES) {
+    uint32_t pos = q0 + 1024 * sw + lane;
+    bool bad = false;
+    const uint32_t wend = 16 * sw + 16 < nw ? 16 * sw + 16 : nw;
+#pragma unroll 1
+    for (uint32_t w = 16 * sw; w < wend; ++w) {
       const uint32_t base = q0 + 64 * w;
-      uint32_t en = 0xFFFFu;
       if (!bad && pos < qe && pos < base + 64) {
-        en = pos - base;
-        const uint32_t x = xt[w * 64 + en];
-        if (x == 0xFFFFu) bad = 1;
-        else pos = x;
+        const uint32_t x = xt[w * 64 + (pos - base)];
+        bad = x == 0xFFFFu;
+        pos = bad ? pos : x;
       }
-      went[w] = (uint16_t)en;
+    }
+    swx[sw * 64 + lane] = bad ? 0xFFFFFFFFu : pos;
+  }
+  __syncthreads();
+  //  B2: thread 0 follows the chain from super-window to super-window (an entry past the first window -- a literal
+  //      longer than 64 B crossing into it -- walks that super-window's windows one by one)
+  if (tid == 0) {
+    uint32_t pos = q0;
+    bool bad = false;
+    for (uint32_t sw = 0; sw < nsw; ++sw) {
+      swent[sw] = pos;
+      if (bad || pos >= qe) continue;
+      const uint32_t b0 = q0 + 1024 * sw;
+      if (pos < b0 + 64) {
+        const uint32_t x = swx[sw * 64 + (pos - b0)];
+        bad = x == 0xFFFFFFFFu;
+        pos = bad ? pos : x;
+      } else {
+        const uint32_t wend = 16 * sw + 16 < nw ? 16 * sw + 16 : nw;
+        for (uint32_t w = 16 * sw; w < wend && !bad; ++w) {
+          const uint32_t base = q0 + 64 * w;
+          if (pos < qe && pos < base + 64) {
+            const uint32_t x = xt[w * 64 + (pos - base)];
+            bad = x == 0xFFFFu;
+            pos = bad ? pos : x;
+          }
+        }
+      }
     }
     ctl[T2_FAIL] = bad || pos != qe;
   }
   __syncthreads();
   if (ctl[T2_FAIL]) return 0;
+  //  B3: every window's entry, one thread per super-window walking its windows from the super-window's entry
+  if (tid < nsw) {
+    uint32_t pos = swent[tid];
+    const uint32_t wend = 16 * tid + 16 < nw ? 16 * tid + 16 : nw;
+#pragma unroll 1
+    for (uint32_t w = 16 * tid; w < wend; ++w) {
+      const uint32_t base = q0 + 64 * w;
+      uint32_t en = 0xFFFFu;
+      if (pos < qe && pos < base + 64) {
+        en = pos - base;
+        pos = xt[w * 64 + en];  // (a good chain: B2)
+      }
+      went[w] = (uint16_t)en;
+    }
+  }
+  __syncthreads();
+  T2_STAMP(3);
   // C: counts and output bytes per window
   for (uint32_t w = wv; w < nw; w += T2_WAVES) {
     const uint32_t en = went[w];
@@ -4328,7 +4392,10 @@ __device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, ld
     if (b < nblk) bpre[b] = (uint16_t)(before + inc - c);
   }
   __syncthreads();
-  // F2: sources
+  T2_STAMP(4);
+  // F2: every output byte's source: a literal's byte is written to dst at once and is its own source (a root); a
+  // copy's byte points at an earlier output position. The sources (16-bit: ulen <= 65536) go to the global scratch
+  // first: the LDS still holds the input, the bitmap and the records this pass reads
   uint64_t todo = 0;
 #pragma unroll 1  // (unrolled, the 64 per-thread addresses are hoisted out of the chunk loop and spill)
   for (uint32_t i = 0; i < 64; ++i) {
@@ -4339,44 +4406,58 @@ __device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, ld
     const uint32_t e = bpre[b] + (uint32_t)__builtin_popcountll(m & ((2ull << l) - 1)) - 1;
     const uint32_t A = ea[e], B = eb[e];
     const uint32_t ew = A & 0xFFFFu, elen = (A >> 16) + 1, off = x - ew;
-    uint32_t src;
+    uint32_t src = x;
     if (B & T2_FIN) {
-      src = T2_FIN | ((B & ~T2_FIN) + off);
+      dst[x] = in[(B & ~T2_FIN) + off];
     } else {
       const uint32_t per = B < elen ? B : 0u;  // (a copy is at most 64 bytes long: off < 64)
       src = per ? ew - B + small_mod(off, per) : x - B;
       todo |= 1ull << i;
     }
-    S[x] = src;
+    S[x] = (uint16_t)src;
   }
   __syncthreads();
-  // F3: pointer jumping (S[x] <- S[S[x]]) until every source is a literal's input byte
+  // F3: the sources into the LDS (its first 128 KiB: input, output staging, bitmap and records are dead), then
+  // pointer jumping there (S[x] <- S[S[x]]) until every copy byte points at a root. A copy of a copy of a copy -- an
+  // index block's keys -- converges in log2 of its chain's length rounds; each round costs two LDS latencies per 16
+  // positions instead of two global-memory latencies per 8 (round 4's scratch walk: 130 us a chunk)
+  lds_u16* const S16 = (lds_u16*)L;
+  for (uint32_t x = 8 * tid; x < ulen; x += 8 * T2_THREADS) *(__attribute__((address_space(3))) u32x4*)(S16 + x) =
+      *(const u32x4*)(S + x);
+  const uint64_t copies = todo;
+  __syncthreads();
+  T2_STAMP(5);
   while (__syncthreads_or(todo != 0)) {
 #pragma unroll 1
-    for (uint32_t i0 = 0; i0 < 64; i0 += 8) {
-      if (!((todo >> i0) & 0xFF)) continue;
-      uint32_t v[8];
+    for (uint32_t i0 = 0; i0 < 64; i0 += 16) {
+      if (!((todo >> i0) & 0xFFFF)) continue;
+      uint32_t v[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = ((todo >> (i0 + j)) & 1) ? S[tid + T2_THREADS * (i0 + j)] : 0u;
-      uint32_t u[8];
+      for (int j = 0; j < 16; ++j) v[j] = ((todo >> (i0 + j)) & 1) ? S16[tid + T2_THREADS * (i0 + j)] : 0u;
+      uint32_t u[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[j] = ((todo >> (i0 + j)) & 1) ? S[v[j]] : 0u;
+      for (int j = 0; j < 16; ++j) u[j] = ((todo >> (i0 + j)) & 1) ? S16[v[j]] : 0u;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < 16; ++j)
         if ((todo >> (i0 + j)) & 1) {
-          S[tid + T2_THREADS * (i0 + j)] = u[j];
-          if (u[j] & T2_FIN) todo &= ~(1ull << (i0 + j));
+          if (u[j] == v[j]) todo &= ~(1ull << (i0 + j));  // v is a root: a literal byte
+          else S16[tid + T2_THREADS * (i0 + j)] = (uint16_t)u[j];
         }
     }
   }
-  // F4: the bytes, at o[0, ulen)
+  T2_STAMP(6);
+  // F4: the copy bytes gathered from their roots in dst (written by F2, before the barriers)
 #pragma unroll 1
-  for (uint32_t i = 0; i < 64; ++i) {
-    const uint32_t x = tid + T2_THREADS * i;
-    if (x >= ulen) break;
-    o[x] = in[S[x] & ~T2_FIN];
+  for (uint32_t i0 = 0; i0 < 64; i0 += 16) {
+    if (!((copies >> i0) & 0xFFFF)) continue;
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = ((copies >> (i0 + j)) & 1) ? dst[S16[tid + T2_THREADS * (i0 + j)]] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if ((copies >> (i0 + j)) & 1) dst[tid + T2_THREADS * (i0 + j)] = (uint8_t)v[j];
   }
+  __threadfence_block();
   __syncthreads();
   return 1;
 }
@@ -4392,9 +4473,9 @@ __global__ void __launch_bounds__(T2_THREADS) k_ts_open2(const uint8_t* __restri
   uint32_t* const T = (uint32_t*)(t2_lds + T2_O_E);
   uint32_t* const passv = (uint32_t*)(t2_lds + T2_O_PASS);
   lds_u32* const ctl = (lds_u32*)(t2_lds + T2_O_CTL);
-  uint32_t* const S = scratch + (uint64_t)blockIdx.x * 65536;
+  uint16_t* const S = (uint16_t*)(scratch + (uint64_t)blockIdx.x * 65536);
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  // the footer's index handle and the framing walk, by wave 0 (as k_ts_open)
+  // the footer's index handle, by wave 0 (as k_ts_open)
   if (tid < 64) {
     uint64_t io = 0, is = 0;
     bool framed = false;
@@ -4408,58 +4489,71 @@ __global__ void __launch_bounds__(T2_THREADS) k_ts_open2(const uint8_t* __restri
       if (p != ~0u) p = dev_varint<64>(f, p, 48, &is);
       framed = p != ~0u && io <= file_len && is + 5 <= file_len - io && is + 1 <= 0x7FFFFFFFull && file[io + is] == 1;
     }
-    uint64_t total = 0, chunks = 0, padded;
-    uint32_t mi, mo;
-    const bool ok = framed && snappy_frame_size(file + io, (uint32_t)is, total, chunks, mi, mo, padded);
-    const bool fits = total <= idec_cap;
-    if (blockIdx.x == 0 && lane == 0) {
-      iopen[1] = ok ? total : 0;
-      iopen[0] = (framed ? 1u : 0u) | (ok && fits ? 2u : 0u) | (ok && !fits ? 4u : 0u);
-    }
     if (lane == 0) {
-      ctl[T2_OK] = ok && fits && blockIdx.x < chunks;
+      ctl[T2_OK] = framed;
       ctl[T2_OCLO] = (uint32_t)io;
       ctl[T2_OCHI] = (uint32_t)(io >> 32);
       ctl[T2_LEN] = (uint32_t)is;
     }
   }
   __syncthreads();
-  if (!ctl[T2_OK]) return;  // (uniform)
+  const bool framed = ctl[T2_OK] != 0;
   const uint8_t* const p = file + ((uint64_t)ctl[T2_OCHI] << 32 | ctl[T2_OCLO]);
   const uint32_t len = ctl[T2_LEN];
-  uint32_t at = 0, k = 0;  // (thread 0) the framing walk's position and data-chunk count
+  // the frame's verdict (snap's framing walk: sizes, types, preambles) by the last workgroup's wave 1 -- the only walk
+  // over the whole frame; the others find their own chunks without it (their decode is only used when it says so)
+  if (blockIdx.x == gridDim.x - 1 && tid >= 64 && tid < 128) {
+    uint64_t total = 0, chunks = 0, padded;
+    uint32_t mi, mo;
+    const bool ok = framed && snappy_frame_size(p, len, total, chunks, mi, mo, padded);
+    const bool fits = total <= idec_cap;
+    if (lane == 0) {
+      iopen[1] = ok ? total : 0;
+      iopen[0] = (framed ? 1u : 0u) | (ok && fits ? 2u : 0u) | (ok && !fits ? 4u : 0u);
+    }
+  }
+  if (!framed) return;  // (uniform)
+  T2_STAMP(0);
+  // wave 0's walk to this workgroup's chunks (k % gridDim == blockIdx): each hop's header, stored CRC and preamble
+  // (20 bytes) loaded by 20 lanes at once and read with v_readlane -- one memory latency a hop. Bounded by the frame:
+  // a malformed frame ends the walk (its verdict is the last workgroup's)
+  uint32_t at = 0, k = 0;  // (wave 0)
   uint64_t o = 0;
   bool good = true;  // (thread 0)
   while (true) {
     __syncthreads();
-    if (tid == 0) {
-      ctl[T2_DONE] = 1;
-      while (at < len) {  // the next data chunk of this workgroup (the framing is good: snappy_frame_size)
-        const uint32_t type = ld_u8(p + at);
-        const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
+    if (tid < 64) {
+      uint32_t done = 1;
+      while (at < len && len - at >= 4) {
+        const uint32_t bv = lane < 20 && lane < len - at ? ld_u8(p + at + lane) : 0u;
+        auto B = [&](uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)bv, (int)i); };
+        const uint32_t type = B(0), cl = B(1) | (B(2) << 8) | (B(3) << 16);
         const uint32_t body = at + 4;
+        if (cl > len - body || cl > SN_MAX_CHUNK) break;
         at = body + cl;
         if (type > 1) continue;
-        uint32_t ulen = cl - 4, q = body + 4;
+        if (cl < 4) break;
+        uint32_t ulen = cl - 4, q = body + 4, used = 0;
         if (type == 0) {
-          uint32_t used = 0;
-          snappy_preamble([&](uint32_t i) { return ld_u8(p + q + i); }, at - q, ulen, used);
+          if (!snappy_preamble([&](uint32_t i) { return B(8 + i); }, cl - 4, ulen, used)) break;
           q += used;
         }
         const uint64_t oc = o;
         o += ulen;
-        if (k++ % gridDim.x != blockIdx.x) continue;
-        ctl[T2_DONE] = 0;
-        ctl[T2_TYPE] = type;
-        ctl[T2_Q] = q;
-        ctl[T2_AT] = at;
-        ctl[T2_ULEN] = ulen;
-        ctl[T2_WANT] = ld_u8(p + body) | (ld_u8(p + body + 1) << 8) | (ld_u8(p + body + 2) << 16) |
-                       ((uint32_t)ld_u8(p + body + 3) << 24);
-        ctl[T2_OCLO] = (uint32_t)oc;
-        ctl[T2_OCHI] = (uint32_t)(oc >> 32);
+        if (k++ % gridDim.x != blockIdx.x || oc + ulen > idec_cap) continue;  // (over the workspace: verdict 4)
+        if (lane == 0) {
+          ctl[T2_TYPE] = type;
+          ctl[T2_Q] = q;
+          ctl[T2_AT] = at;
+          ctl[T2_ULEN] = ulen;
+          ctl[T2_WANT] = B(4) | (B(5) << 8) | (B(6) << 16) | (B(7) << 24);
+          ctl[T2_OCLO] = (uint32_t)oc;
+          ctl[T2_OCHI] = (uint32_t)(oc >> 32);
+        }
+        done = 0;
         break;
       }
+      if (lane == 0) ctl[T2_DONE] = done;
     }
     __syncthreads();
     if (ctl[T2_DONE]) break;
@@ -4493,38 +4587,47 @@ __global__ void __launch_bounds__(T2_THREADS) k_ts_open2(const uint8_t* __restri
       stage_to_lds((const uint32_t*)(zs - d), (lds_u8*)lin, ndw, tid, T2_THREADS);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
-      uint32_t r = sn_par_decode((const lds_u8*)lin, d, d + (ae - q), (lds_u8*)(lout + pad), ulen, t2_lds, S, tid);
-      if (r == 2) {  // more elements than the records hold: the wave decoder, on wave 0
+      T2_STAMP(1);
+      const uint32_t r = sn_par_decode((const lds_u8*)lin, d, d + (ae - q), ulen, t2_lds, S, idec + oc, tid);
+      if (r == 2) {  // more elements than the records hold: the wave decoder, on wave 0, in the LDS staging
         if (tid < 64) {
           const bool w_ok = snappy_wave_decode(lin, d, d + (ae - q), lout + pad, ulen, lane);
           if (lane == 0) ctl[T2_FAIL] = !w_ok;
         }
         __syncthreads();
-        r = ctl[T2_FAIL] ? 0u : 1u;
-      }
-      cok = r == 1;
-      if (cok) {
-        // V[0, pad) zeroed for the CRC passes -- exactly: the output already starts at pad, which need not be 16-aligned
-        for (uint32_t x = 16 * tid; x < pad; x += 16 * T2_THREADS) {
-          if (x + 16 <= pad) {
-            *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
-          } else {
-            for (uint32_t b = x; b < pad; ++b) lout[b] = 0;
+        cok = !ctl[T2_FAIL];
+        if (cok) {
+          // V[0, pad) zeroed for the CRC passes -- exactly: the output starts at pad, which need not be 16-aligned
+          for (uint32_t x = 16 * tid; x < pad; x += 16 * T2_THREADS) {
+            if (x + 16 <= pad) {
+              *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
+            } else {
+              for (uint32_t b = x; b < pad; ++b) lout[b] = 0;
+            }
           }
+          stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, tid, T2_THREADS);
+          __builtin_amdgcn_s_waitcnt(0);
+          __syncthreads();
+          crc = t2_chunk_crc<true>(T, lout, ulen, passv, (uint32_t*)ctl, tid);
+          const uint8_t* src = lout + pad;
+          uint32_t x0 = 0;
+          if (((oc | pad) & 15) == 0) {  // whole 16 B pieces, then the tail byte by byte
+            x0 = ulen & ~15u;
+            for (uint32_t x = 16 * tid; x < x0; x += 16 * T2_THREADS) *(u32x4*)(idec + oc + x) = *(const u32x4*)(src + x);
+          }
+          for (uint32_t x = x0 + tid; x < ulen; x += T2_THREADS) idec[oc + x] = src[x];
         }
-        stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, tid, T2_THREADS);
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        crc = t2_chunk_crc<true>(T, lout, ulen, passv, (uint32_t*)ctl, tid);
-        const uint8_t* src = lout + pad;
-        uint32_t x0 = 0;
-        if (((oc | pad) & 15) == 0) {  // whole 16 B pieces, then the tail byte by byte
-          x0 = ulen & ~15u;
-          for (uint32_t x = 16 * tid; x < x0; x += 16 * T2_THREADS) *(u32x4*)(idec + oc + x) = *(const u32x4*)(src + x);
+      } else {
+        cok = r == 1;
+        if (cok) {  // decoded into the workspace: checksummed there
+          stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, tid, T2_THREADS);
+          __builtin_amdgcn_s_waitcnt(0);
+          __syncthreads();
+          crc = t2_chunk_crc<false>(T, idec + oc, ulen, passv, (uint32_t*)ctl, tid);
         }
-        for (uint32_t x = x0 + tid; x < ulen; x += T2_THREADS) idec[oc + x] = src[x];
       }
     }
+    T2_STAMP(7);
     if (tid == 0) good = good && cok && mask32c(crc) == want;
     __builtin_amdgcn_s_waitcnt(0);
   }
