@@ -3567,13 +3567,14 @@ __device__ __forceinline__ bool row_snappy_decode(lds_u8* B, uint32_t q, uint32_
   return ok && w == ulen;
 }
 
-// The CRC-32C of V[pad, pad + len) per row, V = o[0, 1024 np) with o[0, pad) zero (pad = 1024 np - len): per 1 KiB
-// pass each lane walks 64 B (slice-by-4, the init register injected into the first min(4, len) bytes of M), the row
+// The CRC-32C of V[pad, pad + len) per row, V = o[0, 1024 np) with o[0, pad) zero (pad = 1024 np - len) and the init
+// register already XORed into the first min(4, len) bytes of M by the caller (the decoded bytes are not kept): per 1 KiB
+// pass each lane walks 64 B (slice-by-4), the row
 // tree joins the lanes with Z64, Z128, Z256, Z512, and the passes chain with Z1024 -- a quarter of the passes (and of
 // their tree and broadcast) of 16 B per lane.
 __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, uint32_t len, bool active,
                                                   uint32_t g, uint32_t lane) {
-  const uint32_t np = active ? (len + 1023) >> 10 : 0u, pad = (np << 10) - len, q4 = len < 4 ? len : 4u;
+  const uint32_t np = active ? (len + 1023) >> 10 : 0u;
   uint32_t acc = 0;
   for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
     const bool on = k < np;
@@ -3581,8 +3582,7 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
 #pragma unroll
     for (int sp = 0; sp < 4; ++sp) {
       const uint32_t x0 = 1024 * k + 64 * g + 16 * sp;
-      u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
-      w = td_inject(w, x0, pad, q4);
+      const u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
       cv = step4(T, cv, w.x);
       cv = step4(T, cv, w.y);
       cv = step4(T, cv, w.z);
@@ -3612,17 +3612,45 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
   return acc ^ 0xFFFFFFFFu;
 }
 
+// A row's frame staging through registers: the next group's frames are loaded (row_stage_load, 16 B units, lane g of
+// the row taking units g, g + 16, ...) while this group decodes, and stored to the row's input area when its turn
+// comes (row_stage_store) -- the global-memory latency of the staging off the decode's path
+constexpr int TR_UNITS = 11;  // 16 lanes x 11 x 16 B >= the row's input staging
+static_assert(16 * TR_UNITS * 16 >= TR_IN, "row staging units");
+struct RowStage {
+  u32x4 t[TR_UNITS];
+  uint32_t tail;
+};
+__device__ __forceinline__ void row_stage_load(RowStage& s, const uint32_t* za, uint32_t ndw, uint32_t g) {
+  const uint32_t units = ndw >> 2;
+#pragma unroll
+  for (int i = 0; i < TR_UNITS; ++i) {
+    const uint32_t u = g + 16 * i;
+    if (u < units) s.t[i] = *(const u32x4_ua*)(za + 4 * u);
+  }
+  // (unconditional: a select or an exec-masked load into the register would make the compiler wait for every load
+  // in flight here; a frame's last dword +12 B stays inside the file, the data blocks being followed by the index
+  // block and the footer)
+  s.tail = za[4 * units + (g & 3)];
+}
+__device__ __forceinline__ void row_stage_store(const RowStage& s, lds_u8* dst, uint32_t ndw, uint32_t g) {
+  typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
+  typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+  const uint32_t units = ndw >> 2;
+#pragma unroll
+  for (int i = 0; i < TR_UNITS; ++i) {
+    const uint32_t u = g + 16 * i;
+    if (u < units) *(lds_u32x4_t*)(dst + 16 * u) = s.t[i];
+  }
+  if (g < (ndw & 3)) ((lds_u32_t*)dst)[4 * units + g] = s.tail;
+}
+
 // One frame per row (p[0, len) in the file; `elig` rows only): staged whole into the row's input area, its chunks
 // walked there, each data chunk decoded (or, uncompressed, copied) into the row's output area and checksummed. Returns
 // 0 good, 1 bad, 2 deferred to the whole wave (a chunk larger than the row staging).
-__device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bool elig, const uint32_t* T, lds_u8* in,
+__device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool elig, const uint32_t* T, lds_u8* in,
                                               lds_u8* o, uint32_t g, uint32_t lane) {
-  const uint32_t d = elig ? (uint32_t)((uintptr_t)p & 3) : 0u;
-  const uint32_t* za = (const uint32_t*)(p - d);
-  const uint32_t ndw = elig ? (d + len + 3) >> 2 : 0u;
-  stage_to_lds(za, in, ndw, g, 16);
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
+  // (staged at in[d, d + len) by the caller: row_stage_load / row_stage_store)
   // the framing was validated by k_ts_finish: headers and lengths are in bounds, preambles are sane
   uint32_t pos = d, res = 0;
   const uint32_t end = d + (elig ? len : 0u);
@@ -3662,6 +3690,7 @@ __device__ __forceinline__ uint32_t row_frame(const uint8_t* p, uint32_t len, bo
       for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += 16) o[pad + k] = in[q + k];
     ok = row_snappy_decode(in, q, next, (uint32_t)(o - in) + pad, ulen, have && type == 0, g, TR_IN + 12) ||
          !(have && type == 0);
+    if (have && g < (ulen < 4 ? ulen : 4u)) o[pad + g] ^= 0xFFu;  // the CRC-32C init register, injected
     const uint32_t crc = row_chunk_crc(T, o, ulen, have, g, lane);
     if (have) {
       if (!ok || mask32c(crc) != want) res = 1;
@@ -3733,15 +3762,50 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     const uint32_t r = lane >> 4, g = lane & 15;
     lds_u8* const rin = (lds_u8*)(lin + r * TR_ROW_LDS);
     lds_u8* const rout = rin + TR_IN + 16;
-    for (uint64_t f0 = lo + 4 * wv; f0 < hi; f0 += 4 * TD_WAVES) {
-      const uint64_t f = f0 + r;
-      const bool valid = f < hi;
-      const uint32_t len = valid ? frames[f].length : 0u;
-      const bool live = len && !fstatus[f];
-      const bool elig = live && len + 3 <= TR_IN - 16;
-      const uint32_t v = row_frame(file + (valid ? frames[f].offset : 0), len, elig, T, rin, rout, g, lane);
-      if (live && g == 0) bad[f - lo] = elig ? (uint8_t)v : 2;
-      __builtin_amdgcn_s_waitcnt(0);
+    // the wave's frames lo + 4 wv + 16 k + r (k < 16): their descriptors loaded at once, lane 4 k + r holding frame k's
+    // of row r; each group's frames staged through registers one group ahead (RowStage)
+    uint64_t d_off = 0;
+    uint32_t d_len = 0;
+    {
+      const uint64_t f = lo + 4 * wv + 16 * (lane >> 2) + (lane & 3);
+      if (f < hi) {
+        d_len = frames[f].length;
+        d_off = frames[f].offset;
+        if (fstatus[f]) d_len |= 0x80000000u;  // (a frame whose framing walk failed: not live)
+      }
+    }
+    auto group = [&](uint32_t k, uint32_t& len, bool& live, bool& elig, uint32_t& d, const uint32_t*& za,
+                     uint32_t& ndw) {
+      const int src = (int)(4 * (k & 15) + r) * 4;
+      const uint32_t lw = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)d_len);
+      const uint64_t of = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)d_off) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(d_off >> 32)) << 32);
+      const bool valid = lo + 4 * wv + 16 * k + r < hi && k < 16;
+      len = valid ? lw & 0x7FFFFFFFu : 0u;
+      live = len && !(lw >> 31);
+      elig = live && len + 3 <= TR_IN - 16;
+      const uint8_t* pf = file + (valid ? of : 0);
+      d = elig ? (uint32_t)((uintptr_t)pf & 3) : 0u;
+      za = (const uint32_t*)(pf - d);
+      ndw = elig ? (d + len + 3) >> 2 : 0u;
+    };
+    RowStage stg;
+    uint32_t len, d, ndw;
+    bool live, elig;
+    const uint32_t* za;
+    group(0, len, live, elig, d, za, ndw);
+    row_stage_load(stg, za, ndw, g);
+    uint32_t k = 0;
+    for (uint64_t f0 = lo + 4 * wv; f0 < hi; f0 += 4 * TD_WAVES, ++k) {
+      const uint32_t len_c = len, d_c = d;
+      const bool live_c = live, elig_c = elig;
+      row_stage_store(stg, rin, ndw, g);
+      group(k + 1, len, live, elig, d, za, ndw);
+      row_stage_load(stg, za, ndw, g);  // (in flight while this group decodes)
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t v = row_frame(d_c, len_c, elig_c, T, rin, rout, g, lane);
+      if (live_c && g == 0) bad[f0 + r - lo] = elig_c ? (uint8_t)v : 2;
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the next group's loads stay in flight
       __builtin_amdgcn_wave_barrier();  // (the next round overwrites the row staging)
     }
     for (uint64_t f0 = lo + 4 * wv; f0 < hi; f0 += 4 * TD_WAVES)
