@@ -3469,6 +3469,51 @@ typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 // then keeps, sinking the arms' work into it: exec-mask juggling in a divergent loop)
 __device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
 
+// An element's bytes moved within a row's staging: m bytes to D from S = Sl (a literal, the input) or D - off (a copy,
+// earlier output); the pass layout and the repeat as row_snappy_decode describes.
+__device__ __forceinline__ void row_move(lds_u8* B, uint32_t D, uint32_t Sl, uint32_t m, uint32_t off, bool lit,
+                                         uint32_t gmask, uint32_t g, uint32_t dump) {
+  typedef __attribute__((address_space(3))) uint32_t lds_w32;
+  const uint32_t S = sel(lit, Sl, D - off);
+  const bool pat = !lit & (off < m) & (off < 128);
+  const uint32_t mm = sel(pat, 0u, m), Da = D & ~3u, sh = D & 3u;
+  const uint32_t old = *(lds_cu32*)(B + Da);
+  // pass 0 (every row; a row with nothing to move -- finished, inactive, or a repeat, which goes bytewise below --
+  // writes nothing: its first lane's merged dword would carry garbage past D into bytes the row's uncompressed-chunk
+  // copy has written)
+  const int r0 = (int)(8 * g) - (int)sh;  // element-relative offset of the lane's first dword
+  const uint32_t sa = S + (uint32_t)r0, A = sa & ~3u, al = sa & 3u;
+  const uint32_t d0 = *(lds_cu32*)(B + A), d1 = *(lds_cu32*)(B + A + 4), d2 = *(lds_cu32*)(B + A + 8);
+  const uint32_t keep = ((1u << (8 * sh)) - 1) & gmask;  // (sh = 0: nothing kept)
+  const uint32_t v0 = (__builtin_amdgcn_alignbyte(d1, d0, al) & ~keep) | (old & keep);
+  const uint32_t v1 = __builtin_amdgcn_alignbyte(d2, d1, al);
+  const uint32_t a0 = Da + 8 * g;
+  *(lds_w32*)(B + sel((mm != 0) & (r0 < (int)mm), a0, dump)) = v0;
+  *(lds_w32*)(B + sel(r0 + 4 < (int)mm, a0 + 4, dump)) = v1;
+  if (__builtin_amdgcn_ballot_w64(sh + mm > 128)) {  // literals longer than a pass (copies: at most 64 B)
+    for (uint32_t b = 128; __builtin_amdgcn_ballot_w64(b < sh + mm); b += 128) {
+      const int r = (int)(b + 8 * g) - (int)sh;
+      const uint32_t sb = S + (uint32_t)r, Ab = sb & ~3u, ab = sb & 3u;
+      const uint32_t e0 = *(lds_cu32*)(B + Ab), e1 = *(lds_cu32*)(B + Ab + 4), e2 = *(lds_cu32*)(B + Ab + 8);
+      *(lds_w32*)(B + sel(r < (int)mm, Da + b + 8 * g, dump)) = __builtin_amdgcn_alignbyte(e1, e0, ab);
+      *(lds_w32*)(B + sel(r + 4 < (int)mm, Da + b + 8 * g + 4, dump)) = __builtin_amdgcn_alignbyte(e2, e1, ab);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(pat)) {  // (pat: a copy, m <= 64)
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t j = 4 * g + k;
+      v[k] = pat ? B[S + small_mod(j, off)] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t j = 4 * g + k;
+      B[pat && j < m ? D + j : dump] = (uint8_t)v[k];
+    }
+  }
+}
+
 // One Snappy chunk per row: the elements B[q, qe) decoded into B[OB, OB + ulen) (both in the row's LDS staging, B
 // its base). Every row walks its own chain -- one element per iteration, its header two dwords of the row's staging
 // read one element ahead (its position is known once the previous header is decoded; the input is never written) --
@@ -3482,7 +3527,6 @@ __device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return
 // the wave decoder's. Rows with active = false only ride along. Returns the row's verdict (output ends at ulen).
 __device__ __forceinline__ bool row_snappy_decode(lds_u8* B, uint32_t q, uint32_t qe, uint32_t OB, uint32_t ulen,
                                                   bool active, uint32_t g, uint32_t dump) {
-  typedef __attribute__((address_space(3))) uint32_t lds_w32;
   uint32_t w = 0;
   bool ok = true;
   uint32_t h0, h1, hs;
@@ -3523,43 +3567,7 @@ __device__ __forceinline__ bool row_snappy_decode(lds_u8* B, uint32_t q, uint32_
     const uint32_t m = sel(ex, n, 0u);
     const uint32_t qn = sel(ex, q + hdr + sel(lit, n, 0u), q);
     fetch(qn);  // (qn <= qe: the 8 bytes from qe & ~3 lie in the row's input staging and its slack)
-    const uint32_t D = OB + w, S = sel(lit, q + hdr, D - off);
-    const bool pat = !lit & (off < m) & (off < 128);
-    const uint32_t mm = sel(pat, 0u, m), Da = D & ~3u, sh = D & 3u;
-    const uint32_t old = *(lds_cu32*)(B + Da);
-    // pass 0 (every row; a row with nothing to move writes at most the merged dword back: V's end is dword-aligned,
-    // so a finished row has sh = 0 and writes nothing; a repeat's merged dword is rewritten by its bytewise moves)
-    const int r0 = (int)(8 * g) - (int)sh;  // element-relative offset of the lane's first dword
-    const uint32_t sa = S + (uint32_t)r0, A = sa & ~3u, al = sa & 3u;
-    const uint32_t d0 = *(lds_cu32*)(B + A), d1 = *(lds_cu32*)(B + A + 4), d2 = *(lds_cu32*)(B + A + 8);
-    const uint32_t keep = ((1u << (8 * sh)) - 1) & gmask;  // (sh = 0: nothing kept)
-    const uint32_t v0 = (__builtin_amdgcn_alignbyte(d1, d0, al) & ~keep) | (old & keep);
-    const uint32_t v1 = __builtin_amdgcn_alignbyte(d2, d1, al);
-    const uint32_t a0 = Da + 8 * g;
-    *(lds_w32*)(B + sel(r0 < (int)mm, a0, dump)) = v0;
-    *(lds_w32*)(B + sel(r0 + 4 < (int)mm, a0 + 4, dump)) = v1;
-    if (__builtin_amdgcn_ballot_w64(sh + mm > 128)) {  // literals longer than a pass (copies: at most 64 B)
-      for (uint32_t b = 128; __builtin_amdgcn_ballot_w64(b < sh + mm); b += 128) {
-        const int r = (int)(b + 8 * g) - (int)sh;
-        const uint32_t sb = S + (uint32_t)r, Ab = sb & ~3u, ab = sb & 3u;
-        const uint32_t e0 = *(lds_cu32*)(B + Ab), e1 = *(lds_cu32*)(B + Ab + 4), e2 = *(lds_cu32*)(B + Ab + 8);
-        *(lds_w32*)(B + sel(r < (int)mm, Da + b + 8 * g, dump)) = __builtin_amdgcn_alignbyte(e1, e0, ab);
-        *(lds_w32*)(B + sel(r + 4 < (int)mm, Da + b + 8 * g + 4, dump)) = __builtin_amdgcn_alignbyte(e2, e1, ab);
-      }
-    }
-    if (__builtin_amdgcn_ballot_w64(pat)) {  // (pat: a copy, m <= 64)
-      uint32_t v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t j = 4 * g + k;
-        v[k] = pat ? B[S + small_mod(j, off)] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t j = 4 * g + k;
-        B[pat && j < m ? D + j : dump] = (uint8_t)v[k];
-      }
-    }
+    row_move(B, OB + w, q + hdr, m, off, lit, gmask, g, dump);
     q = qn;
     w += m;
     live = ex & (qn < qe);

@@ -3,7 +3,8 @@ form the snap crate's decoder accepts (snap "1", the decompressor behind src/sst
 destination alignment -- literals with 0..4 length bytes (minimal and not), 1-, 2- and 4-byte-offset copies, copies
 overlapping their own output (offset < length: the repeat), copies closer than a 128 B pass and farther, literals
 longer than a pass -- plus invalid streams (offset past the output, output past the preamble's length, a header cut
-by the end). Frames are sized for the row staging (<= 2,701 B compressed, <= 5,120 B decoded), stored as the data
+by the end) and uncompressed chunks of every length mod 4 in rows beside compressed ones (a row the decoder skips
+must see none of its stores). Frames are sized for the row staging (<= 2,701 B compressed, <= 5,120 B decoded), stored as the data
 blocks of one table, and the device scan's verdict on each block must equal the oracle's read_block_from_file.
 
 The generator's own decode of each valid stream is checked against the oracle first (CPU), so the cases are what
@@ -86,6 +87,10 @@ def row_cases(orc, seed=11, count=160):
         if len(fr) > 2701 or len(dec) > 5120:
             continue
         r = rng.random()
+        if rng.random() < 0.12:  # an uncompressed chunk (copied in the row, beside rows decoding compressed ones)
+            data = bytes(rng.integers(0, 256, int(rng.integers(1, 2600)), dtype=np.uint8))
+            cases.append((STREAM + _chunk(orc, 1, data, data), data))
+            continue
         if r < 0.1 and len(dec) > 10:  # a second chunk
             pay2, dec2 = gen_stream(rng, 200)
             fr2 = _frame(orc, pay2, dec2 or b"")[len(STREAM):]
