@@ -226,7 +226,9 @@ struct lcrc_ctx {
   uint64_t ts_out_cap = 0;  // the decode workspace: ts_decoded_cap + the 16-alignment of its (large) chunks
   // lcrc_ctx_options (lcrc_ctx_create_ex; tests and measurement only -- the library reads no environment variable)
   uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (tests reach the tile loops with a small one)
-  int ts_blocks_div = 1;  // k_blocks grid divisor of the table scan
+  // k_blocks grid divisor of the table scan: half the range pass's usual grid co-runs with the other stream's
+  // window pass (raw table on two streams: 3,130-3,158 GiB/s against 2,806-2,926 with the full grid; alone +2 us)
+  int ts_blocks_div = 2;
   bool wal_onepass = false;  // lcrc_ctx_options.wal_onepass
   uint32_t batch_grid_b = 0;  // lcrc_batch's k_blocks grid (0: 2 per CU)
   uint32_t wal_grid_b = 0;    // the WAL scan's k_blocks grid (0: every resident workgroup)
