@@ -2066,24 +2066,26 @@ constexpr uint32_t SN_MAX_CHUNK = 76490;
 // bytes, each at most SN_MAX (k_snappy_decode_wave sizes them from the batch's largest chunk)
 constexpr uint32_t SN_SLACK = 128;
 constexpr uint32_t SN_MAX = 16384;
-// k_ts_decode (the whole-table scan's decode): TD_WAVES waves per 256-block tile, each with this LDS staging
-// Each wave of k_ts_decode decodes four frames at once, one per 16-lane row (row staging: the whole frame, TR_IN
-// bytes, and one decoded chunk, TR_OUT); a frame that does not fit goes through the whole wave (the wave decoder, its
-// staging TD_IN + TD_OUT made of the wave's four row areas); a chunk too large for that, lane-serially to the workspace.
-constexpr uint32_t TD_WAVES = 4;
+// k_ts_decode (the whole-table scan's decode): TD_WAVES waves per 256-block tile. Each wave decodes four frames at once,
+// one per 16-lane row. A row (TR_ROW bytes of LDS) decodes IN PLACE: the frame is staged at the row's end and the
+// chunk decoded from the row's start, the output growing towards the unread input (round 5: 5,136 B a row instead of
+// 7,856 with separate input and output areas -- six waves a CU instead of four, so two SIMDs hold two waves and hide
+// each other's LDS and dependency latency). A frame of over TR_IN bytes (the register staging), a chunk of over TR_OUT,
+// or one whose output would reach its own unread input goes through the whole-wave decoder afterwards, in the LDS of
+// two waves' rows (TD_IN + TD_OUT); a chunk too large for that, lane-serially to the workspace.
+constexpr uint32_t TD_WAVES = 6;
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
-// a row's frame (+ the slack of its element-header reads): frames up to 2,701 B (db_bench-style 4 KiB blocks: <= 2,298).
-// Round 4 staged 3,008 B, which made the workgroup's LDS 163.6 KB: no room for the other stream's small scan kernels
-// (k_ts_index 344 B, k_ts_finish 4 KiB), which then waited for whole decode workgroups to retire
+// a row's frame (+ the slack of its element-header reads): frames up to 2,701 B (db_bench-style 4 KiB blocks: <= 2,298)
 constexpr uint32_t TR_IN = 2704 + 16;
-constexpr uint32_t TR_OUT = 5120;        // a row's decoded chunk (V: a multiple of 1 KiB)
-constexpr uint32_t TR_ROW_LDS = TR_IN + 16 + TR_OUT;
-constexpr uint32_t TD_WAVE_LDS = 4 * TR_ROW_LDS;
-constexpr uint32_t TD_IN = 12288 + 16;   // the whole wave's staging: compressed bytes (+ 4 for the tail dword)
+constexpr uint32_t TR_OUT = 5120;        // a row's decoded chunk, walked by the CRC in whole 1 KiB passes
+constexpr uint32_t TR_ROW = TR_OUT + 16;  // + 16 B of slack: header reads past the input, the dump dword
+constexpr uint32_t TD_WAVE_LDS = 4 * TR_ROW;
+constexpr uint32_t TD_IN = 12288 + 16;   // the whole-wave decoder's staging: compressed bytes (+ 4 for the tail dword)
 constexpr uint32_t TD_OUT = 16384;       // decoded bytes (a multiple of 1 KiB: V fits as is)
 static_assert(TD_OUT % 1024 == 0, "the chunk CRC reads V in whole 1 KiB passes");
-static_assert(TR_OUT % 1024 == 0 && TR_ROW_LDS % 16 == 0, "row staging");
-static_assert(TD_IN + SN_SLACK + TD_OUT <= TD_WAVE_LDS, "the wave staging is the wave's row areas");
+static_assert(TR_OUT % 1024 == 0 && TR_ROW % 16 == 0 && TR_IN + 16 <= TR_ROW, "row staging");
+static_assert(TD_WAVES % 2 == 0 && TD_IN + SN_SLACK + TD_OUT <= 2 * TD_WAVE_LDS,
+              "the whole-wave decoder's staging is two waves' row areas");
 constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
 static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish and k_ts_index");
 
@@ -3524,11 +3526,12 @@ __device__ __forceinline__ void row_move(lds_u8* B, uint32_t D, uint32_t Sl, uin
 // past the element are overwritten by the next element's (in order: a wave's LDS operations execute in issue order),
 // and V's end is dword-aligned, so nothing past it is touched. A copy whose source overlaps its own destination
 // closer than a pass (offset < length, offset < 128: the Snappy repeat) goes bytewise, j mod offset. Validation as
-// the wave decoder's. Rows with active = false only ride along. Returns the row's verdict (output ends at ulen).
-__device__ __forceinline__ bool row_snappy_decode(lds_u8* B, uint32_t q, uint32_t qe, uint32_t OB, uint32_t ulen,
-                                                  bool active, uint32_t g, uint32_t dump) {
+// the wave decoder's. Rows with active = false only ride along. Returns the row's verdict: 0 good (output ends at
+// ulen), 1 malformed, 2 given up (the in-place output would reach unread input).
+__device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uint32_t qe, uint32_t OB, uint32_t ulen,
+                                                      bool active, uint32_t g, uint32_t dump) {
   uint32_t w = 0;
-  bool ok = true;
+  bool ok = true, spill = false;
   uint32_t h0, h1, hs;
   auto fetch = [&](uint32_t at) {
     const uint32_t ba = at & ~3u;
@@ -3563,25 +3566,31 @@ __device__ __forceinline__ bool row_snappy_decode(lds_u8* B, uint32_t q, uint32_
     const bool good = (room >= hdr) & (!lit | ((lm1 < room - hdr) & ((nb == 0) | (room >= 5))));
     const bool bad = live & (!good | (n > ulen - w) | (!lit & ((off == 0) | (off > w))));  // (w <= ulen holds)
     ok = ok & !bad;
-    const bool ex = live & !bad;
+    // in place (output and input in one row area, the output from its start): every dword this element writes lies
+    // before the input not yet read -- from the next element on (its header is read before these writes), and for a
+    // literal longer than a pass, before its own bytes' later passes. Else the row gives the frame up (spill)
+    const uint32_t qn0 = q + hdr + sel(lit, n, 0u);
+    const bool sp = live & !bad & ((((OB + w + n + 3) & ~3u) > qn0) | (lit & (OB + w + 8 > q + hdr)));
+    spill = spill | sp;
+    const bool ex = live & !bad & !sp;
     const uint32_t m = sel(ex, n, 0u);
-    const uint32_t qn = sel(ex, q + hdr + sel(lit, n, 0u), q);
+    const uint32_t qn = sel(ex, qn0, q);
     fetch(qn);  // (qn <= qe: the 8 bytes from qe & ~3 lie in the row's input staging and its slack)
     row_move(B, OB + w, q + hdr, m, off, lit, gmask, g, dump);
     q = qn;
     w += m;
     live = ex & (qn < qe);
   }
-  return ok && w == ulen;
+  return spill ? 2u : ok && w == ulen ? 0u : 1u;
 }
 
-// The CRC-32C of V[pad, pad + len) per row, V = o[0, 1024 np) with o[0, pad) zero (pad = 1024 np - len) and the init
-// register already XORed into the first min(4, len) bytes of M by the caller (the decoded bytes are not kept): per 1 KiB
-// pass each lane walks 64 B (slice-by-4), the row
+// The CRC-32C of M = V[0, len) per row, V = o[0, 1024 np) with V[len, 1024 np) zero (z = 1024 np - len bytes, undone
+// at the end by one GF(2) multiply with invz = x^(-8z)) and the init register already XORed into the first min(4, len)
+// bytes of M by the caller (the decoded bytes are not kept): per 1 KiB pass each lane walks 64 B (slice-by-4), the row
 // tree joins the lanes with Z64, Z128, Z256, Z512, and the passes chain with Z1024 -- a quarter of the passes (and of
 // their tree and broadcast) of 16 B per lane.
 __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, uint32_t len, bool active,
-                                                  uint32_t g, uint32_t lane) {
+                                                  uint32_t g, uint32_t lane, uint32_t invz) {
   const uint32_t np = active ? (len + 1023) >> 10 : 0u;
   uint32_t acc = 0;
   for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
@@ -3616,6 +3625,8 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
     const uint32_t pass = row_bcast0(cv, lane);
     if (on) acc = k ? zl(T, TAB_ZWIN + 2048, acc) ^ pass : pass;
   }
+  // M sits at V's start and zeros follow it to the pass end: walk(M || 0^z) = Z_z(walk(M)), undone by x^(-8z)
+  if (__builtin_amdgcn_ballot_w64(active && (len & 1023) != 0)) acc = (len & 1023) ? gf_mul(invz, acc, 0x82F63B78u) : acc;
   if (len < 4) acc ^= len ? 0xFFFFFFFFu >> (8 * len) : 0xFFFFFFFFu;
   return acc ^ 0xFFFFFFFFu;
 }
@@ -3653,12 +3664,13 @@ __device__ __forceinline__ void row_stage_store(const RowStage& s, lds_u8* dst, 
   if (g < (ndw & 3)) ((lds_u32_t*)dst)[4 * units + g] = s.tail;
 }
 
-// One frame per row (p[0, len) in the file; `elig` rows only): staged whole into the row's input area, its chunks
-// walked there, each data chunk decoded (or, uncompressed, copied) into the row's output area and checksummed. Returns
-// 0 good, 1 bad, 2 deferred to the whole wave (a chunk larger than the row staging).
-__device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool elig, const uint32_t* T, lds_u8* in,
-                                              lds_u8* o, uint32_t g, uint32_t lane) {
-  // (staged at in[d, d + len) by the caller: row_stage_load / row_stage_store)
+// One frame per row (`elig` rows only), staged by the caller at B[ib + d, ib + d + len) (row_stage_load / _store), its
+// chunks walked there, each data chunk decoded in place (or, uncompressed, copied forward) to B[0, ulen) and
+// checksummed. Returns 0 good, 1 bad, 2 deferred to the whole-wave decoder (a chunk over TR_OUT, an in-place decode
+// that would reach unread input, or a chunk's CRC zeros that would reach a later chunk's input).
+__device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool elig, const uint32_t* T, lds_u8* B,
+                                              uint32_t ib, uint32_t g, uint32_t lane, const uint32_t* __restrict__ inv) {
+  lds_u8* const in = B + ib;
   // the framing was validated by k_ts_finish: headers and lengths are in bounds, preambles are sane
   uint32_t pos = d, res = 0;
   const uint32_t end = d + (elig ? len : 0u);
@@ -3686,20 +3698,31 @@ __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool eli
         snappy_preamble([&](uint32_t i) { return (uint32_t)in[q + i]; }, next - q, ulen, used);
         q += used;
       }
-      if (ulen > TR_OUT) {
-        res = 2;  // too large for the row: the whole wave decodes this frame
+      const uint32_t vend = (ulen + 1023) & ~1023u;
+      // too large for the row, or the CRC's zeros after M would overwrite a later chunk's input: the whole wave
+      if (ulen > TR_OUT || (next < end && vend > ib + next)) {
+        res = 2;
         have = false;
       }
     }
-    const uint32_t pad = have ? ((ulen + 1023) & ~1023u) - ulen : 0u;
-    for (uint32_t k = 16 * g; k < pad; k += 256) *(__attribute__((address_space(3))) u32x4*)(o + k) = u32x4{0, 0, 0, 0};
-    bool ok = true;
-    if (__builtin_amdgcn_ballot_w64(have && type == 1))  // uncompressed: copied to V + pad
-      for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += 16) o[pad + k] = in[q + k];
-    ok = row_snappy_decode(in, q, next, (uint32_t)(o - in) + pad, ulen, have && type == 0, g, TR_IN + 12) ||
-         !(have && type == 0);
-    if (have && g < (ulen < 4 ? ulen : 4u)) o[pad + g] ^= 0xFFu;  // the CRC-32C init register, injected
-    const uint32_t crc = row_chunk_crc(T, o, ulen, have, g, lane);
+    const uint32_t z = have ? ((ulen + 1023) & ~1023u) - ulen : 0u;
+    const uint32_t invz = inv[z];  // x^(-8z) (loaded now, used after the decode)
+    if (__builtin_amdgcn_ballot_w64(have && type == 1))  // uncompressed: copied forward to B[0, ulen) (in place: the
+      // destination is below the source, and each byte is read before anything is stored at or above it)
+      for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += 16) B[k] = in[q + k];
+    const bool dec = have && type == 0;
+    const uint32_t rd = row_snappy_decode(B, ib + q, ib + next, 0u, ulen, dec, g, TR_ROW - 4);
+    const bool ok = !dec || rd == 0;
+    if (dec && rd == 2) {
+      res = 2;  // given up in place: the whole wave decodes the frame from the file
+      have = false;
+    }
+    // V[ulen, 1024 np) zeroed (input bytes already consumed), then the init register injected into M's first bytes
+    const uint32_t u4 = (ulen + 3) & ~3u;
+    for (uint32_t x = ulen + g; x < (have ? u4 : 0u); x += 16) B[x] = 0;
+    for (uint32_t x = u4 + 4 * g; x < (have ? ulen + z : 0u); x += 64) *(__attribute__((address_space(3))) uint32_t*)(B + x) = 0;
+    if (have && g < (ulen < 4 ? ulen : 4u)) B[g] ^= 0xFFu;
+    const uint32_t crc = row_chunk_crc(T, B, ulen, have, g, lane, invz);
     if (have) {
       if (!ok || mask32c(crc) != want) res = 1;
       pos = next;
@@ -3762,21 +3785,30 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     for (uint32_t i = threadIdx.x; i < TD_TAB_WORDS / 4; i += blockDim.x) ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i];
   __syncthreads();
   if (dec) {
-    uint8_t* const lin = td_lds + TD_TAB_WORDS * 4 + wv * TD_WAVE_LDS;
-    uint8_t* const lout = lin + TD_IN + SN_SLACK;
-    // this tile's frames (the last three blocks excluded): four per wave at a time, one per row; a frame the row
-    // staging cannot hold (bad[] = 2) then through the whole wave; then the last workgroup's wave 0 the last three
+    // this tile's frames (the last three blocks excluded): four per wave at a time, one per row, over a static share of
+    // the tile's 64 groups of four -- waves 2 and 3 take 12, the others 10: the hardware puts a workgroup's waves on
+    // the SIMDs in order, so waves 0/4 and 1/5 share a SIMD (issue rate ~1.6x one wave's, measured with rows of
+    // fewer frames) and 2 and 3 have one each. A frame the row cannot decode (bad[] = 2) then through the whole wave,
+    // in two waves' row areas; then the last workgroup's wave 0 the last three blocks.
     const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
     const uint32_t r = lane >> 4, g = lane & 15;
-    lds_u8* const rin = (lds_u8*)(lin + r * TR_ROW_LDS);
-    lds_u8* const rout = rin + TR_IN + 16;
-    // the wave's frames lo + 4 wv + 16 k + r (k < 16): their descriptors loaded at once, lane 4 k + r holding frame k's
-    // of row r; each group's frames staged through registers one group ahead (RowStage)
+#ifndef LCRC_TD_SPLIT
+#define LCRC_TD_SPLIT 10, 10, 12, 12, 10, 10  // (a probe build may try another share)
+#endif
+    constexpr uint32_t gsplit[TD_WAVES] = {LCRC_TD_SPLIT};
+    uint32_t gbeg = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < TD_WAVES; ++i) gbeg += i < wv ? gsplit[i] : 0u;
+    const uint32_t gcnt = gsplit[wv];
+    lds_u8* const rb = (lds_u8*)(td_lds + TD_TAB_WORDS * 4 + wv * TD_WAVE_LDS + r * TR_ROW);
+    const uint32_t* const inv = tab_c + TAB_INV;
+    // the wave's frames lo + 4 (gbeg + k) + r (k < gcnt): their descriptors loaded at once, lane 4 k + r holding frame
+    // k's of row r; each group's frames staged through registers one group ahead (RowStage)
     uint64_t d_off = 0;
     uint32_t d_len = 0;
     {
-      const uint64_t f = lo + 4 * wv + 16 * (lane >> 2) + (lane & 3);
-      if (f < hi) {
+      const uint64_t f = lo + 4 * (gbeg + (lane >> 2)) + (lane & 3);
+      if ((lane >> 2) < gcnt && f < hi) {
         d_len = frames[f].length;
         d_off = frames[f].offset;
         if (fstatus[f]) d_len |= 0x80000000u;  // (a frame whose framing walk failed: not live)
@@ -3788,7 +3820,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
       const uint32_t lw = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)d_len);
       const uint64_t of = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)d_off) |
                           ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(d_off >> 32)) << 32);
-      const bool valid = lo + 4 * wv + 16 * k + r < hi && k < 16;
+      const bool valid = k < gcnt && lo + 4 * (gbeg + k) + r < hi;
       len = valid ? lw & 0x7FFFFFFFu : 0u;
       live = len && !(lw >> 31);
       elig = live && len + 3 <= TR_IN - 16;
@@ -3803,21 +3835,28 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     const uint32_t* za;
     group(0, len, live, elig, d, za, ndw);
     row_stage_load(stg, za, ndw, g);
-    uint32_t k = 0;
-    for (uint64_t f0 = lo + 4 * wv; f0 < hi; f0 += 4 * TD_WAVES, ++k) {
+    for (uint32_t k = 0; k < gcnt && lo + 4 * (gbeg + k) < hi; ++k) {
       const uint32_t len_c = len, d_c = d;
       const bool live_c = live, elig_c = elig;
-      row_stage_store(stg, rin, ndw, g);
+      // the frame staged at the row's end (16-aligned), the decoded chunk growing from the row's start towards it
+      const uint32_t ib = (TR_ROW - 16 - 4 * ndw) & ~15u;
+      row_stage_store(stg, rb + ib, ndw, g);
       group(k + 1, len, live, elig, d, za, ndw);
       row_stage_load(stg, za, ndw, g);  // (in flight while this group decodes)
       __builtin_amdgcn_wave_barrier();
-      const uint32_t v = row_frame(d_c, len_c, elig_c, T, rin, rout, g, lane);
-      if (live_c && g == 0) bad[f0 + r - lo] = elig_c ? (uint8_t)v : 2;
+      const uint32_t v = row_frame(d_c, len_c, elig_c, T, rb, ib, g, lane, inv);
+      if (live_c && g == 0) bad[4 * (gbeg + k) + r] = elig_c ? (uint8_t)v : 2;
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the next group's loads stay in flight
       __builtin_amdgcn_wave_barrier();  // (the next round overwrites the row staging)
     }
-    for (uint64_t f0 = lo + 4 * wv; f0 < hi; f0 += 4 * TD_WAVES)
-      for (uint64_t f = f0; f < f0 + 4 && f < hi; ++f)
+  }
+  __syncthreads();  // every row done: the whole-wave decoder takes two waves' row areas
+  if (dec) {
+    const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
+    uint8_t* const lin = td_lds + TD_TAB_WORDS * 4 + (wv & ~1u) * TD_WAVE_LDS;
+    uint8_t* const lout = lin + TD_IN + SN_SLACK;
+    if ((wv & 1) == 0)
+      for (uint64_t f = lo + wv / 2; f < hi; f += TD_WAVES / 2)
         if (bad[f - lo] == 2) {
           const bool ok = td_frame(file + frames[f].offset, frames[f].length, T, lin, lout, out, out_off[f] + before, lane);
           __builtin_amdgcn_s_waitcnt(0);
