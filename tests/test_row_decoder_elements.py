@@ -112,6 +112,58 @@ def row_cases(orc, seed=11, count=160):
     return cases
 
 
+def in_place_cases(orc, seed=5):
+    """Frames the row decodes in place only up to a point (k_ts_decode stages a frame at its row's end and decodes from
+    the row's start): a compressible head then a long literal tail, so the output reaches the literal's unread bytes
+    (the row gives the frame to the whole-wave decoder); and two-chunk frames whose first chunk's CRC zeros would reach
+    the second chunk's input. Each must decode as the oracle does."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    for head, total in ((2900, 5100), (3000, 5110), (3100, 5116), (3200, 5118), (3300, 5112), (3400, 5119),
+                        (2600, 5119), (3600, 5117)):
+        tail = total - head
+        pay = _lit_el(bytes(rng.integers(0, 256, 8, dtype=np.uint8)), 0)
+        dec = bytearray(pay[1:])
+        while len(dec) + 64 <= head:
+            pay += _copy_el(8, 64, 2)
+            for _ in range(64):
+                dec.append(dec[-8])
+        lit = bytes(rng.integers(0, 256, tail, dtype=np.uint8))
+        pay += _lit_el(lit, 2)
+        dec += lit
+        cases.append((_frame(orc, bytes(pay), bytes(dec)), bytes(dec)))
+    for first in (2500, 3000, 3500):
+        pay = _lit_el(b"abcdefgh", 0)
+        dec = bytearray(b"abcdefgh")
+        while len(dec) + 64 <= first:
+            pay += _copy_el(8, 64, 2)
+            dec += dec[-8:] * 8
+        second = bytes(rng.integers(0, 256, 2200, dtype=np.uint8))
+        fr = _frame(orc, bytes(pay), bytes(dec)) + _frame(orc, _lit_el(second, 2), second)[len(STREAM):]
+        cases.append((fr, bytes(dec) + second))
+    return cases
+
+
+def test_in_place_cases_match_oracle(orc, lcrc):
+    for fr, want in in_place_cases(orc):
+        assert len(fr) <= 2701
+        assert orc.snappy_frame_decode(fr) == want
+        assert lcrc.snappy_frame_decode(fr) == want
+
+
+@pytest.mark.gpu
+def test_row_decoder_in_place_limits(lcrc, orc, engines):
+    from test_table_scan import _scan
+    from test_table_scan_async import _expect_async
+    cases = in_place_cases(orc) + row_cases(orc, 21, 40)
+    f = frames_table(orc, [fr for fr, _ in cases])
+    want, werr = orc.table_scan_expect(f)
+    assert werr is None and [w[4] for w in want if w[2] == 0] == [0 if d is not None else 3 for _, d in cases]
+    assert _expect_async(lcrc, engines[lcrc.MODE_REF], orc, f) == 0
+    got, err = _scan(lcrc, engines[lcrc.MODE_REF], f)
+    assert err is None and _as_tuples(got) == want
+
+
 @pytest.mark.parametrize("seed", [11, 12, 13])
 def test_row_cases_match_oracle(orc, lcrc, seed):
     """The generator's decode is the oracle's (so each case is the element mix it claims), and the host decoder's."""
