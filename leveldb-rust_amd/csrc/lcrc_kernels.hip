@@ -3530,8 +3530,7 @@ __device__ __forceinline__ void row_move(lds_u8* B, uint32_t D, uint32_t Sl, uin
 // ulen), 1 malformed, 2 given up (the in-place output would reach unread input).
 __device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uint32_t qe, uint32_t OB, uint32_t ulen,
                                                       bool active, uint32_t g, uint32_t dump) {
-  uint32_t w = 0;
-  bool ok = true, spill = false;
+  uint32_t w = 0, res = 0;  // res: 1 malformed, 2 given up in place (the row stops at either)
   uint32_t h0, h1, hs;
   auto fetch = [&](uint32_t at) {
     const uint32_t ba = at & ~3u;
@@ -3540,14 +3539,16 @@ __device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uin
     hs = at & 3;
   };
   fetch(active && q < qe ? q : 0u);
-  bool live = active && q < qe;
+  // (the loop state in VGPRs: a bool carried around a divergent loop costs lane-mask merges every iteration)
+  uint32_t livef = active && q < qe ? 1u : 0u;
   const uint32_t gmask = g == 0 ? ~0u : 0u;  // the row's first lane merges the element's first dword
   // the first header waited for here, so the loop's own wait (for the next header, issued with the element's
   // source reads) is the only one per element: never one for the writes of the element before
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   // one LDS round trip per element: the next header, the dword the element's first write merges with and the pass-0
   // source dwords are issued together and waited for together; the writes are never waited for (only ordered)
-  while (__builtin_amdgcn_ballot_w64(live)) {
+  while (__builtin_amdgcn_ballot_w64(livef != 0)) {
+    const bool live = livef != 0;
     const uint32_t lo = __builtin_amdgcn_alignbyte(h1, h0, hs);                         // bytes q .. q + 3
     const uint32_t ext = sel(hs == 3, h1, __builtin_amdgcn_alignbyte(h1, h0, hs + 1));  // bytes q + 1 .. q + 4
     const uint32_t t = lo & 0xFFu, typ = t & 3, L = t >> 2;
@@ -3564,14 +3565,14 @@ __device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uin
     const uint32_t hdr = sel(lit, 1 + nb, (0x5320u >> (4 * typ)) & 0xFu);  // 1 + nb | 2 | 3 | 5
     const uint32_t n = sel(lit, lm1 + 1, sel(c1, 4 + (L & 7), L + 1));
     const bool good = (room >= hdr) & (!lit | ((lm1 < room - hdr) & ((nb == 0) | (room >= 5))));
-    const bool bad = live & (!good | (n > ulen - w) | (!lit & ((off == 0) | (off > w))));  // (w <= ulen holds)
-    ok = ok & !bad;
+    // (w <= ulen holds; off - 1 >= w: a copy's offset 0 or past the output)
+    const bool bad = live & (!good | (n > ulen - w) | (!lit & (off - 1u >= w)));
     // in place (output and input in one row area, the output from its start): every dword this element writes lies
     // before the input not yet read -- from the next element on (its header is read before these writes), and for a
     // literal longer than a pass, before its own bytes' later passes. Else the row gives the frame up (spill)
     const uint32_t qn0 = q + hdr + sel(lit, n, 0u);
     const bool sp = live & !bad & ((((OB + w + n + 3) & ~3u) > qn0) | (lit & (OB + w + 8 > q + hdr)));
-    spill = spill | sp;
+    res = sel(bad, 1u, sel(sp, 2u, res));
     const bool ex = live & !bad & !sp;
     const uint32_t m = sel(ex, n, 0u);
     const uint32_t qn = sel(ex, qn0, q);
@@ -3579,9 +3580,9 @@ __device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uin
     row_move(B, OB + w, q + hdr, m, off, lit, gmask, g, dump);
     q = qn;
     w += m;
-    live = ex & (qn < qe);
+    livef = sel(ex & (qn < qe), 1u, 0u);
   }
-  return spill ? 2u : ok && w == ulen ? 0u : 1u;
+  return res ? res : w == ulen ? 0u : 1u;
 }
 
 // The CRC-32C of M = V[0, len) per row, V = o[0, 1024 np) with V[len, 1024 np) zero (z = 1024 np - len bytes, undone
