@@ -4324,6 +4324,9 @@ __device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, ui
   lds_u32* const wout = (lds_u32*)(L + T2_O_WOUT);
   lds_u16* const went = (lds_u16*)(L + T2_O_WENT);
   lds_u32* const ctl = (lds_u32*)(L + T2_O_CTL);
+  // each window's chain of element starts (C), kept for E in the output area (the exit table's, dead after B)
+  typedef __attribute__((address_space(3))) uint64_t lds_u64;
+  lds_u64* const wmask = (lds_u64*)(L + T2_O_OUT);
   const uint32_t lane = tid & 63, wv = tid >> 6;
   const uint32_t nw = (qe - q0 + 63) >> 6;
   // A: exits
@@ -4421,6 +4424,7 @@ __device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, ui
       const bool sel = (mask >> lane) & 1;
       cnt = (uint32_t)__builtin_popcountll(mask);
       out = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(sel ? c.outlen : 0u, lane), 63);
+      if (lane == 0) wmask[w] = mask;
     }
     if (lane == 0) {
       wcnt[w] = cnt;
@@ -4470,8 +4474,8 @@ __device__ uint32_t sn_par_decode(const lds_u8* in, uint32_t q0, uint32_t qe, ui
     if (en == 0xFFFFu) continue;
     const uint32_t base = q0 + 64 * w, lim = qe - base < 64 ? qe - base : 64u;
     const SnCand c = sn_cand(in, base + lane, qe);
-    const uint32_t nxt = c.good ? lane + c.size : 0x7FFFFFFFu;
-    const uint64_t mask = sn_chain(nxt, en, lim);
+    const uint64_t mask = wmask[w];  // (C's chain)
+    (void)lim;
     const bool sel = (mask >> lane) & 1;
     const uint32_t v = sel ? c.outlen : 0u;
     const uint32_t wpos = wout[w] + wave_incl_scan(v, lane) - v;
