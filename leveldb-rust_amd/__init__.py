@@ -89,7 +89,8 @@ class _WJob(ctypes.Structure):
 class _CtxOptions(ctypes.Structure):
     _fields_ = [("size", ctypes.c_uint32), ("general", ctypes.c_int32), ("batch_grid_b", ctypes.c_uint32),
                 ("wal_grid_b", ctypes.c_uint32), ("ts_grid", ctypes.c_uint32), ("ts_blocks_div", ctypes.c_uint32),
-                ("wal_onepass", ctypes.c_uint32), ("ts_open_v1", ctypes.c_uint32)]
+                ("wal_onepass", ctypes.c_uint32), ("ts_open_v1", ctypes.c_uint32),
+                ("ts_unfused", ctypes.c_uint32)]
 
 
 GENERAL_PATHS = {"auto": 0, "ranges": 1, "blocks": 2}
@@ -420,7 +421,8 @@ class Engine:
             for k, v in options.items():
                 if k == "general":
                     v = GENERAL_PATHS[v] if isinstance(v, str) else int(v)
-                elif k not in ("batch_grid_b", "wal_grid_b", "ts_grid", "ts_blocks_div", "wal_onepass", "ts_open_v1"):
+                elif k not in ("batch_grid_b", "wal_grid_b", "ts_grid", "ts_blocks_div", "wal_onepass", "ts_open_v1",
+                               "ts_unfused"):
                     raise TypeError(f"Engine: unknown option {k!r}")
                 setattr(o, k, int(v))
             _check(lib().lcrc_ctx_create_ex(ctypes.byref(ctx), device, mode, flags, ctypes.byref(o)),

@@ -49,6 +49,11 @@ hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tsca
                                const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
                                uint64_t vcap, uint64_t bound, uint32_t gcap, const uint8_t* idec, uint64_t* iopen,
                                hipStream_t s);
+hipError_t lcrc_launch_ts_windows(int grid, const uint8_t* file, uint64_t file_len, const uint32_t* gtab, uint32_t* win,
+                                  const lcrc_tscan_key* key, uint64_t cap, uint64_t vcap, lcrc_tscan_dev* st,
+                                  uint64_t* local_c, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
+                                  const uint64_t* iopen_r, uint64_t* iopen, lcrc_tblk_dev* out, lcrc_desc_dev* descs,
+                                  uint64_t* agg, uint32_t nidx_cap, hipStream_t s);
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
                                  uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, lcrc_tscan_dev* st,
@@ -216,8 +221,11 @@ struct lcrc_ctx {
   DevBuf<lcrc_tscan_dev> ts_state;
   DevBuf<uint8_t> ts_idx;    // table scan: a Snappy-framed index block decoded on the device (k_ts_open)
   DevBuf<uint64_t> ts_open;  // k_ts_open's verdict words (zeroed when allocated)
+  DevBuf<uint64_t> ts_agg;   // k_ts_windows' index workgroups: their entry counts and arrival count (zeroed when
+                             // allocated; the last arrival zeroes them again)
   DevBuf<uint32_t> ts_open_scr;  // k_ts_open2's per-workgroup source arrays (pointer jumping)
   bool ts_open_v1 = false;       // lcrc_ctx_options.ts_open_v1: the one-wave k_ts_open instead
+  bool ts_unfused = false;       // lcrc_ctx_options.ts_unfused: k_ts_index + k_ts_emit as launches of their own
   DevBuf<lcrc_tblk_dev> ts_blocks;
   DevBuf<uint64_t> ts_count;
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
@@ -412,6 +420,7 @@ int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, con
     if (opt->ts_blocks_div) ctx->ts_blocks_div = (int)opt->ts_blocks_div;
     if (opt->size >= offsetof(lcrc_ctx_options, wal_onepass) + sizeof(uint32_t)) ctx->wal_onepass = opt->wal_onepass != 0;
     if (opt->size >= offsetof(lcrc_ctx_options, ts_open_v1) + sizeof(uint32_t)) ctx->ts_open_v1 = opt->ts_open_v1 != 0;
+    if (opt->size >= offsetof(lcrc_ctx_options, ts_unfused) + sizeof(uint32_t)) ctx->ts_unfused = opt->ts_unfused != 0;
   }
   *out = ctx;
   return LCRC_OK;
@@ -474,6 +483,7 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->ts_state.release();
   ctx->ts_idx.release();
   ctx->ts_open.release();
+  ctx->ts_agg.release();
   ctx->ts_open_scr.release();
   ctx->ts_blocks.release();
   ctx->ts_count.release();
@@ -1376,6 +1386,8 @@ static uint64_t ts_verify_cap(size_t max_blocks, uint64_t file_len) {
 
 // the device-only scan's workspace (every buffer its launches touch; nothing else: the host-assisted scan and
 // lcrc_snappy_frames size their own)
+constexpr uint32_t TS_AGG_WORDS = 257;  // k_ts_windows: at most 256 index workgroups, then the arrival count
+
 static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap) {
   int rc = set_device(ctx);
   if (rc) return rc;
@@ -1393,6 +1405,10 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
   if (!ctx->ts_open.p) {
     if ((rc = ctx->ts_open.ensure(4))) return rc;
     HIPCHK(hipMemset(ctx->ts_open.p, 0, 4 * sizeof(uint64_t)));
+  }
+  if (!ctx->ts_agg.p) {
+    if ((rc = ctx->ts_agg.ensure(TS_AGG_WORDS))) return rc;
+    HIPCHK(hipMemset(ctx->ts_agg.p, 0, TS_AGG_WORDS * sizeof(uint64_t)));
   }
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   ctx->ts_decoded_cap = decoded_cap;
@@ -1444,22 +1460,33 @@ int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
     HIPCHK(lcrc_launch_ts_open(file, file_len, tab_c, ctx->ts_idx.p, ctx->ts_idx.cap, ctx->ts_open.p,
                                ctx->ts_open_v1 ? nullptr : ctx->ts_open_scr.p, st));
   const uint64_t vcap = ts_verify_cap(cap, file_len);
-  HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
-                              ctx->ts_grid, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p, sidx ? ctx->ts_open.p : nullptr,
-                              st));
-  // the handles and the verify descriptors
-  HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_count.p, ctx->sn_part.p, blk, ctx->tbl_descs.p, cap, vcap, cap,
-                             ctx->ts_grid, ctx->ts_idx.p, ctx->ts_open.p, st));
-  // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
   const uint64_t* nver = &S->n_verify;
+  const bool fused = cap && ctx->general != 1 && !ctx->ts_unfused;
+  if (fused) {
+    // the file's window pass with the index walk and the handles beside it (k_ts_windows: the window values do not
+    // depend on the handles)
+    HIPCHK(lcrc_launch_ts_windows(ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, &key, cap, vcap, S,
+                                  ctx->idx_count.p, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p,
+                                  sidx ? ctx->ts_open.p : nullptr, ctx->ts_open.p, blk, ctx->tbl_descs.p, ctx->ts_agg.p,
+                                  std::min<uint32_t>(ctx->ts_grid, TS_AGG_WORDS - 1), st));
+  } else {
+    HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
+                                ctx->ts_grid, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p,
+                                sidx ? ctx->ts_open.p : nullptr, st));
+    // the handles and the verify descriptors
+    HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_count.p, ctx->sn_part.p, blk, ctx->tbl_descs.p, cap, vcap,
+                               cap, ctx->ts_grid, ctx->ts_idx.p, ctx->ts_open.p, st));
+  }
+  // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
   if (cap) {
     if (ctx->general == 1) {  // options.general = 1: the one-pass kernel
       HIPCHK(lcrc_launch_ranges(false, ctx->grid_a, file, file_len, ctx->tbl_descs.p, vcap, 0, 0, nullptr, ctx->d_tab,
                                 ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     } else {
-      HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr, nullptr,
-                                 st));
+      if (!fused)
+        HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr,
+                                   nullptr, st));
       HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / ctx->ts_blocks_div, file, file_len, ctx->tbl_descs.p, vcap, 0, 0,
                                 nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));

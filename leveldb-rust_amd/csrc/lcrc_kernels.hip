@@ -421,13 +421,13 @@ struct Share {
   }
 };
 
-__device__ __forceinline__ Share make_share(uint64_t nreg) {
+__device__ __forceinline__ Share make_share(uint64_t nreg, uint32_t nwg = 0) {
   Share sh;
   // regions dealt round-robin over the workgroups: at any moment the whole chip streams one contiguous
   // stretch of the buffer (memory skeleton: 39.9 us per 256 MiB against 41.4-42.0 with a contiguous
   // range per workgroup, tools/probe/probe_skel.hip). No ticket count: a 64-bit division in the prologue.
   sh.lo = blockIdx.x;
-  sh.step = gridDim.x;
+  sh.step = nwg ? nwg : gridDim.x;  // nwg: the launch's window workgroups (k_ts_windows: the first nwg)
   sh.end = nreg;
   return sh;
 }
@@ -674,12 +674,12 @@ __device__ __forceinline__ uint32_t expect_of(const Src& src, uint64_t t, uint32
 
 template <bool FINAL, bool SHIFT, class Src>
 __device__ __forceinline__ void windows_body(const Src& src, const uint32_t* __restrict__ gtab, uint32_t fin,
-                                             uint32_t flags, uint32_t* L, uint32_t* wg_ticket_p) {
+                                             uint32_t flags, uint32_t* L, uint32_t* wg_ticket_p, uint32_t nwg = 0) {
   uint32_t& wg_ticket = *wg_ticket_p;
   const uint32_t lane = __lane_id();
   const uint32_t tid = threadIdx.x;
   const uint64_t nreg = src.regions();
-  const Share share = make_share(nreg);  // this workgroup's regions
+  const Share share = make_share(nreg, nwg);  // this workgroup's regions
 #ifdef LCRC_PROBE_CLOCK
   const unsigned long long s_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long s_first = 0;
@@ -2824,16 +2824,24 @@ enum { TSM_SHORT = 1, TSM_MAGIC = 2, TSM_VARINT = 3, TSM_CHECKSUM = 4, TSM_TYPE 
 
 // footer, index block header and (meta) the metaindex filter entry, by one thread; key: 256 B of LDS
 // idec / iopen: k_ts_open's decoded index and its verdict (nullptr when the scan has no LCRC_TSCAN_SNAPPY_INDEX)
-__device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_len, const lcrc_tscan_key& fkey,
+// pre (k_ts_windows, nullable): every value this walk loads, loaded beforehand by the workgroup in parallel rounds
+// (a chain of dependent loads costs ~5 us a link under the window stream), each under the condition its use here has
+struct TsPre {
+  const uint8_t* foot;       // the file's last 48 bytes (LDS)
+  const uint8_t* meta_copy;  // the metaindex block with its type byte (LDS), or nullptr: read from the file
+  uint64_t io[3];            // iopen[0..2] (when iopen is given)
+  uint32_t itype, nres_raw, nres_dec;  // the index block's type byte; the restart count of its raw / decoded contents
+};
+__device__ __forceinline__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_len, const lcrc_tscan_key& fkey,
                               uint64_t seg_cap, uint8_t* __restrict__ key, bool meta, const uint8_t* __restrict__ idec,
-                              const uint64_t* __restrict__ iopen, lcrc_tscan_dev& s) {
+                              const uint64_t* __restrict__ iopen, lcrc_tscan_dev& s, const TsPre* pre = nullptr) {
   s = {};
   if (file_len < 48) {
     s.status = TS_CORRUPT;
     s.code = TSM_SHORT;
     return;
   }
-  const uint8_t* f = file + file_len - 48;
+  const uint8_t* f = pre ? pre->foot : file + file_len - 48;
   const uint64_t magic = (uint64_t)load_le32(f + 40) | ((uint64_t)load_le32(f + 44) << 32);
   if (magic != 0xdb4775248b80fb57ull) {
     s.status = TS_CORRUPT;
@@ -2854,24 +2862,25 @@ __device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_le
     s.status = TS_HOST;  // "truncated block read" and its kin: the host walk
     return;
   }
-  const uint8_t itype = file[s.idx_off + s.idx_size];
+  const uint8_t itype = pre ? (uint8_t)pre->itype : file[s.idx_off + s.idx_size];
   const uint8_t* ic = file + s.idx_off;  // the index block's contents
   uint64_t clen = s.idx_size;
   if (itype == 1) {
     // a Snappy-framed index block: its contents are what k_ts_open decoded, when it decoded them all; otherwise the
     // host path decodes it (and gives the reference's message) -- after the workspace grows, when that was the reason
-    const uint64_t o0 = iopen ? iopen[0] : 0;
-    if (!(o0 & 2) || iopen[2] || iopen[1] > 0x7FFFFFFFull) {
+    const uint64_t o0 = iopen ? (pre ? pre->io[0] : iopen[0]) : 0;
+    const uint64_t o1 = o0 ? (pre ? pre->io[1] : iopen[1]) : 0, o2 = o0 ? (pre ? pre->io[2] : iopen[2]) : 0;
+    if (!(o0 & 2) || o2 || o1 > 0x7FFFFFFFull) {
       if (o0 & 4) {
         s.gate = 1;
-        s.need_out = iopen[1];
+        s.need_out = o1;
       }
       s.status = TS_HOST;
       return;
     }
     s.idx_dec = 1;
     ic = idec;
-    clen = iopen[1];
+    clen = o1;
   }
   s.idx_clen = clen;
   if (itype > 1) {
@@ -2879,7 +2888,7 @@ __device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_le
   } else if (clen < 4) {
     s.pcode = TSM_SMALL;
   } else {
-    const uint32_t nres = load_le32(ic + clen - 4);
+    const uint32_t nres = pre ? (s.idx_dec ? pre->nres_dec : pre->nres_raw) : load_le32(ic + clen - 4);
     if ((uint64_t)nres > (clen - 4) / 4) {
       s.pcode = TSM_CONTENTS;
     } else if (nres == 0 || (clen - 4) / nres > 4096) {
@@ -2896,7 +2905,7 @@ __device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_le
   // read_meta (only with a filter policy): the first metaindex key >= "filter" + name; a malformed
   // metaindex yields no filter, as the reference swallows read_meta's errors
   if (meta && fkey.len && s.meta_off <= file_len && s.meta_size + 5 <= file_len - s.meta_off && s.meta_size <= 0xFFFFFFFFull) {
-    const uint8_t* d = file + s.meta_off;
+    const uint8_t* d = pre && pre->meta_copy ? pre->meta_copy : file + s.meta_off;
     const uint64_t n = s.meta_size;
     const uint8_t mtype = d[n];
     if (mtype == 1) {
@@ -2946,8 +2955,9 @@ __device__ void ts_open_state(const uint8_t* __restrict__ file, uint64_t file_le
   }
 }
 
-// Workgroup-wide exclusive scan of two u64 values per thread (256 threads): e* = the sums over the threads
-// before this one, t* = the workgroup's totals. s*: 4 words of LDS each.
+// Workgroup-wide exclusive scan of two u64 values per thread (NWAVE waves): e* = the sums over the threads
+// before this one, t* = the workgroup's totals. s*: NWAVE words of LDS each.
+template <int NWAVE = 4>
 __device__ __forceinline__ void wg_scan2(uint64_t va, uint64_t vb, uint64_t* sa, uint64_t* sb, uint64_t& ea,
                                          uint64_t& eb, uint64_t& ta, uint64_t& tb) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -2966,7 +2976,7 @@ __device__ __forceinline__ void wg_scan2(uint64_t va, uint64_t vb, uint64_t* sa,
   __syncthreads();
   uint64_t pa = 0, pb = 0;
   ta = tb = 0;
-  for (uint32_t k = 0; k < 4; ++k) {
+  for (uint32_t k = 0; k < NWAVE; ++k) {
     if (k < w) {
       pa += sa[k];
       pb += sb[k];
@@ -3050,27 +3060,22 @@ __global__ void __launch_bounds__(256) k_ts_index(const uint8_t* __restrict__ fi
   }
 }
 
-// after pass 1: the data-block total, the capacity check and the fallback flags (decided alike by every
-// workgroup from the tile totals; workgroup 0 records them), then pass 2 writes the handles (slot = the tiles
-// before + the segment's place in its tile) and thread 0 appends the filter, metaindex and index blocks with
-// their descriptors
-__global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                 lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ local_c,
-                                                 const uint64_t* __restrict__ part, lcrc_tblk_dev* __restrict__ out,
-                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap, uint64_t vcap,
-                                                 const uint8_t* __restrict__ idec, uint64_t* __restrict__ iopen) {
-  __shared__ uint64_t sa[4], sb[4];
-  const uint32_t status = st->status;  // as k_ts_index left it
-  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-  if (lead) iopen[2] = 0;  // k_ts_open's failure mark, read by k_ts_index: clear for the next scan
-  if (status != TS_OK) {
+// After pass 1, from the totals (nd: the data blocks the index names, nflag: segments the device walk cannot vouch
+// for): the capacity check and the fallback flags (decided alike by every workgroup; `lead` records them), then
+// pass 2 writes the handles (seg(d, len, nres): this workgroup's segments at their slots) and, in workgroup 0
+// (wg0), threads 0..2 append the filter, metaindex and index blocks with their descriptors. s: the state
+// ts_open_state left (k_ts_emit: from st; k_ts_windows: the workgroup's own).
+template <class Seg>
+__device__ void ts_emit_body(const lcrc_tscan_dev& s, lcrc_tscan_dev* __restrict__ st, bool lead, bool wg0,
+                             uint64_t nd, uint64_t nflag, const uint8_t* __restrict__ file, uint64_t file_len,
+                             lcrc_tblk_dev* __restrict__ out, lcrc_desc_dev* __restrict__ descs, uint64_t cap,
+                             uint64_t vcap, const uint8_t* __restrict__ idec, Seg seg) {
+  if (s.status != TS_OK) {
     if (lead) st->n_total = 0;
     return;
   }
-  const uint64_t nres = st->nres;
-  uint64_t nd = 0, nflag = 0;
-  wg_sum_parts(part, 0, (nres + 255) / 256, sa, sb, nd, nflag);
-  const bool hf = st->has_filter;
+  const uint64_t nres = s.nres;
+  const bool hf = s.has_filter;
   const uint64_t ntot = nd + (hf ? 3 : 2);
   if (nres && nflag) {
     // a segment the device walk cannot vouch for. The reference checks the index block's checksum before its
@@ -3084,13 +3089,13 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
       }
       st->idx_only = 1;
       lcrc_tblk_dev b = {};
-      b.offset = st->idx_off;
-      b.size = st->idx_size;
+      b.offset = s.idx_off;
+      b.size = s.idx_size;
       b.kind = 3;  // LCRC_TBLK_INDEX
       lcrc_desc_dev dd;
-      dd.offset = st->idx_off;
-      dd.length = (uint32_t)(st->idx_size + 1);  // in the file: checked by k_ts_index
-      dd.expect_rel = (int32_t)(st->idx_size + 1);
+      dd.offset = s.idx_off;
+      dd.length = (uint32_t)(s.idx_size + 1);  // in the file: checked by ts_open_state
+      dd.expect_rel = (int32_t)(s.idx_size + 1);
       out[0] = b;
       descs[0] = dd;
     }
@@ -3110,8 +3115,8 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
   uint64_t npieces = 0;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    offk[k] = k == 0 ? st->filt_off : k == 1 ? st->meta_off : st->idx_off;
-    sizek[k] = k == 0 ? st->filt_size : k == 1 ? st->meta_size : st->idx_size;
+    offk[k] = k == 0 ? s.filt_off : k == 1 ? s.meta_off : s.idx_off;
+    sizek[k] = k == 0 ? s.filt_size : k == 1 ? s.meta_size : s.idx_size;
     ink[k] = (k > 0 || hf) && offk[k] <= file_len && sizek[k] + 5 <= file_len - offk[k] && sizek[k] + 1 <= 0x7FFFFFFFull;
     npk[k] = ink[k] && sizek[k] + 1 > LCRC_TS_PIECE ? (sizek[k] + LCRC_TS_PIECE) / LCRC_TS_PIECE : 0;
     npieces += npk[k];
@@ -3122,28 +3127,23 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     st->n_total = ntot;
     st->n_verify = ntot + (split ? npieces : 0);
   }
-  const uint8_t* d = st->idx_dec ? idec : file + st->idx_off;
-  const uint32_t len = (uint32_t)st->idx_clen;
-  for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
-    uint64_t base, bf;
-    wg_sum_parts(part, 0, t0 / 256, sa, sb, base, bf);
-    const uint64_t i = t0 + threadIdx.x;
-    bool bad;
-    if (i < nres) idx_segment<true>(d, len, (uint32_t)nres, file_len, base + local_c[i], out, descs, i, bad);
-  }
-  if (blockIdx.x == 0 && threadIdx.x < 3) {
+  seg(s.idx_dec ? idec : file + s.idx_off, (uint32_t)s.idx_clen, nres);
+  if (wg0 && threadIdx.x < 3) {
     const uint32_t k = threadIdx.x;  // 0 filter (if any), then metaindex, index
     if (k == 0 && !hf) return;
     const uint64_t at = nd + (hf ? k : k - 1);
-    const uint64_t off = offk[k], size = sizek[k];
-    const bool in = ink[k];
-    if (split && npk[k]) {
+    // (selects, not a runtime index into the arrays: those would live in scratch)
+    const uint64_t off = k == 0 ? offk[0] : k == 1 ? offk[1] : offk[2];
+    const uint64_t size = k == 0 ? sizek[0] : k == 1 ? sizek[1] : sizek[2];
+    const uint64_t np = k == 0 ? npk[0] : k == 1 ? npk[1] : npk[2];
+    const bool in = k == 0 ? ink[0] : k == 1 ? ink[1] : ink[2];
+    if (split && np) {
       // the first piece takes the remainder, so that every later piece is joined by the same Z65536
       const uint64_t first = ntot + (k > 0 ? npk[0] : 0) + (k > 1 ? npk[1] : 0);
-      const uint64_t r = size + 1 - (npk[k] - 1) * LCRC_TS_PIECE;
+      const uint64_t r = size + 1 - (np - 1) * LCRC_TS_PIECE;
       st->pbase[k] = (uint32_t)first;
-      st->pcnt[k] = (uint32_t)npk[k];
-      for (uint64_t q = 0; q < npk[k]; ++q) {
+      st->pcnt[k] = (uint32_t)np;
+      for (uint64_t q = 0; q < np; ++q) {
         lcrc_desc_dev pd;
         pd.offset = q ? off + r + (q - 1) * LCRC_TS_PIECE : off;
         pd.length = (uint32_t)(q ? LCRC_TS_PIECE : r);
@@ -3160,7 +3160,7 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     b.status = 0;
     b.reserved = 0;
     lcrc_desc_dev dd;
-    const bool whole = in && !(split && npk[k]);  // a split block's own descriptor is empty
+    const bool whole = in && !(split && np);  // a split block's own descriptor is empty
     dd.offset = in ? off : 0;
     dd.length = whole ? (uint32_t)(size + 1) : 0;
     dd.expect_rel = whole ? (int32_t)(size + 1) : LCRC_NO_EXPECT_DEV;
@@ -3171,6 +3171,320 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
     out[at] = b;
     descs[at] = dd;
   }
+}
+
+// after k_ts_index: the totals of its tiles, then ts_emit_body with the tiles dealt over the workgroups (slot = the
+// tiles before + the segment's place in its tile)
+__global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
+                                                 lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ local_c,
+                                                 const uint64_t* __restrict__ part, lcrc_tblk_dev* __restrict__ out,
+                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap, uint64_t vcap,
+                                                 const uint8_t* __restrict__ idec, uint64_t* __restrict__ iopen) {
+  __shared__ uint64_t sa[4], sb[4];
+  const lcrc_tscan_dev s = *st;  // as k_ts_index left it (the fields read below are not written here)
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  if (lead) iopen[2] = 0;  // k_ts_open's failure mark, read by k_ts_index: clear for the next scan
+  uint64_t nd = 0, nflag = 0;
+  if (s.status == TS_OK) wg_sum_parts(part, 0, (s.nres + 255) / 256, sa, sb, nd, nflag);
+  ts_emit_body(s, st, lead, blockIdx.x == 0, nd, nflag, file, file_len, out, descs, cap, vcap, idec,
+               [&](const uint8_t* d, uint32_t len, uint64_t nres) {
+                 for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
+                   uint64_t base, bf;
+                   wg_sum_parts(part, 0, t0 / 256, sa, sb, base, bf);
+                   const uint64_t i = t0 + threadIdx.x;
+                   bool bad;
+                   if (i < nres)
+                     idx_segment<true>(d, len, (uint32_t)nres, file_len, base + local_c[i], out, descs, i, bad);
+                 }
+               });
+}
+
+// The table scan's first launch when the batch goes through the window pass (lcrc_table_scan_async_ex): the file's
+// window pass (k_windows<false>: its values do not depend on the index) in workgroups [0, nwg), and k_ts_index +
+// k_ts_emit in the nidx workgroups after them, which run beside the window stream instead of before it (two
+// dependent launches less). Index workgroup j walks a contiguous range of the restart segments; the ranges' entry
+// counts meet through agg[j] (a ready bit, a fallback bit, the count), published once and read by every index
+// workgroup (all of them are resident: they follow the window workgroups in dispatch order and wait on nothing
+// but each other, and nidx <= the CUs); the last one to have read them zeroes agg and the arrival count for the
+// next scan. Each index workgroup computes the footer state itself (the metaindex walk included), so that none
+// reads another's. The totals travel inside the atomic words themselves, so the atomics are relaxed: an
+// acquire/release at agent scope would write back / invalidate the XCD's L2 on every poll, under the window stream.
+// (The reset cannot overtake a reader: each workgroup's arrival depends on the values it loaded.)
+constexpr uint64_t TSA_READY = 1ull << 63, TSA_BAD = 1ull << 62, TSA_COUNT = (1ull << 62) - 1;
+struct TsIdxArgs {
+  const uint8_t* file;
+  uint64_t file_len;
+  uint64_t seg_cap, cap, vcap, nzero;
+  lcrc_tscan_dev* st;
+  uint64_t* local_c;
+  uint32_t* zero;  // the batch's mismatch bitmap (nzero words)
+  const uint8_t* idec;
+  const uint64_t* iopen_r;  // k_ts_open's verdict (nullptr: no Snappy-framed index)
+  uint64_t* iopen;          // its failure mark is cleared once every workgroup has read it
+  lcrc_tblk_dev* out;
+  lcrc_desc_dev* descs;
+  uint64_t* agg;  // nidx words, then the arrival count
+};
+
+// bytes [src1, src1 + n1) and [src2, src2 + n2) of global memory into dst1[0, n1) and dst2[0, n2) (LDS), by the
+// whole workgroup: aligned dword loads (the dwords holding a range's first and last bytes stay inside its
+// allocation), up to 8 a thread issued before any of its stores, so that up to 16 KiB of both is one load round trip
+__device__ __forceinline__ void wg_copy_bytes(uint8_t* dst1, const uint8_t* __restrict__ src1, uint32_t n1,
+                                              uint8_t* dst2 = nullptr, const uint8_t* __restrict__ src2 = nullptr,
+                                              uint32_t n2 = 0) {
+  const uint32_t mis1 = (uint32_t)((uintptr_t)src1 & 3), mis2 = (uint32_t)((uintptr_t)src2 & 3);
+  const uint32_t* __restrict__ w1 = (const uint32_t*)(src1 - mis1);
+  const uint32_t* __restrict__ w2 = (const uint32_t*)(src2 - mis2);
+  const uint32_t nd1 = n1 ? (mis1 + n1 + 3) / 4 : 0, nd2 = n2 ? (mis2 + n2 + 3) / 4 : 0, nd = nd1 + nd2;
+  for (uint32_t base = 0; base < nd; base += 8 * A_THREADS) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t k = base + u * A_THREADS + threadIdx.x;
+      v[u] = k < nd1 ? w1[k] : k < nd ? w2[k - nd1] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t k = base + u * A_THREADS + threadIdx.x;
+      const bool first = k < nd1;
+      const uint32_t kk = first ? k : k - nd1, mis = first ? mis1 : mis2, n = first ? n1 : n2;
+      uint8_t* dst = first ? dst1 : dst2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t o = 4 * kk + q - mis;  // (wraps below 0: out of range)
+        if (k < nd && o < n) dst[o] = (uint8_t)(v[u] >> (8 * q));
+      }
+    }
+  }
+}
+
+#ifdef LCRC_PROBE_CLOCK  // diagnostic build: index workgroup j's phase stamps in lcrc_dbg_stamp row 2048 + j
+#define TSI_STAMP(k)                                                                       \
+  if (threadIdx.x == 0 && j < 2048) lcrc_dbg_stamp[(2048 + j) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define TSI_STAMP(k)
+#endif
+// Index workgroup j of k_ts_windows. Under the window stream a load takes ~5 us, so every value the walk needs is
+// loaded in four parallel rounds instead of chains: (1) the footer and k_ts_open's verdict words; (2) the metaindex
+// block, the index block's type byte and its restart count (raw and decoded: the type picks); (3) the workgroup's
+// slice of the restart array; (4) the bytes of its segments. Its restart segments [lo, hi) are then a block of their
+// own in LDS (stage): the bytes [s0, E) -- s0 = the first segment's start (0 in workgroup 0, so that segment 0 must
+// start at 0), E = the next range's start or the restart array -- followed by the range's offsets minus s0 and
+// their count, so that idx_segment reads it as it reads the whole block, with local segment numbers. Rebasing is
+// exact once the offsets are non-decreasing, within the restart array and rst(0) = 0; a violation is a segment the
+// whole-block walk finds bad too (start > end, or end past the restarts), so it only raises the fallback bit. A
+// range too long for the LDS is walked in place.
+__device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint32_t j, uint32_t nidx,
+                            uint32_t* L) {
+  TSI_STAMP(0);
+#ifndef LCRC_TSI_PRIO
+#define LCRC_TSI_PRIO 3
+#endif
+  if (LCRC_TSI_PRIO) __builtin_amdgcn_s_setprio(LCRC_TSI_PRIO);  // issue ahead of the window waves on the CU: this
+                                                                // walk is the launch's critical path
+  constexpr int NT = A_THREADS, NWAVE = A_THREADS / 64;
+  constexpr uint32_t META_STAGE = 4096, RSL_AT = 6144, RSL_CAP = 16384, STAGE_AT = RSL_AT + RSL_CAP;
+  constexpr uint32_t STAGE_CAP = A_LDS_BYTES - STAGE_AT;
+  uint8_t* key = (uint8_t*)L;  // 256 B
+  lcrc_tscan_dev* S = (lcrc_tscan_dev*)(L + 64);
+  static_assert(sizeof(lcrc_tscan_dev) <= 256, "state slot");
+  uint64_t* sa = (uint64_t*)(L + 128);
+  uint64_t* sb = sa + NWAVE;
+  uint64_t* tot = sb + NWAVE;
+  uint64_t* io_l = tot + 4;                     // iopen[0..2]
+  uint32_t* pre_l = (uint32_t*)(io_l + 3);      // type byte, restart counts
+  uint32_t* flags = pre_l + 4;
+  uint8_t* foot = (uint8_t*)(L + 256);          // 48 B
+  uint8_t* mcopy = (uint8_t*)(L + 272);         // META_STAGE + 1 B
+  uint8_t* rsl = (uint8_t*)L + RSL_AT;          // the restart array slice
+  uint8_t* stage = (uint8_t*)L + STAGE_AT;
+  static_assert(512 + 16 * 8 + 8 * 7 + 4 * 5 <= 1024 && 1088 + META_STAGE + 1 <= RSL_AT && STAGE_CAP >= 32768,
+                "index workgroup LDS");
+  const uint32_t tid = threadIdx.x;
+  const uint64_t file_len = a.file_len;
+  for (uint64_t i = (uint64_t)j * NT + tid; i < a.nzero; i += (uint64_t)nidx * NT) a.zero[i] = 0;
+  // round 1
+  if (tid < 48 && file_len >= 48) foot[tid] = a.file[file_len - 48 + tid];
+  if (a.iopen_r && tid >= 64 && tid < 67) io_l[tid - 64] = a.iopen_r[tid - 64];
+  if (tid == 0) *flags = 0;
+  __syncthreads();
+  TSI_STAMP(1);
+  // round 2, each load under the condition of its use in ts_open_state
+  uint64_t mo = 0, ms = 0, io = 0, is = 0;
+  uint32_t p = file_len >= 48 ? dev_varint<64>(foot, 0, 48, &mo) : ~0u;
+  if (p != ~0u) p = dev_varint<64>(foot, p, 48, &ms);
+  if (p != ~0u) p = dev_varint<64>(foot, p, 48, &io);
+  if (p != ~0u) p = dev_varint<64>(foot, p, 48, &is);
+  const bool iin = p != ~0u && io <= file_len && is + 5 <= file_len - io && is + 1 <= 0x7FFFFFFFull;
+  const bool mstage = p != ~0u && mo <= file_len && ms + 5 <= file_len - mo && ms + 1 <= META_STAGE;
+  uint32_t pv = 0;
+  if (tid == 0 && iin) pv = a.file[io + is];
+  if (tid == 1 && iin && is >= 4) pv = load_le32(a.file + io + is - 4);
+  if (tid == 2 && a.iopen_r && (io_l[0] & 2) && !io_l[2] && io_l[1] >= 4 && io_l[1] <= 0x7FFFFFFFull)
+    pv = load_le32(a.idec + io_l[1] - 4);
+  if (mstage) wg_copy_bytes(mcopy, a.file + mo, (uint32_t)ms + 1);
+  if (tid < 3) pre_l[tid] = pv;
+  __syncthreads();
+  TSI_STAMP(2);
+  if (tid == 0) {
+    const TsPre pre{foot, mstage ? mcopy : nullptr, {io_l[0], io_l[1], io_l[2]}, pre_l[0], pre_l[1], pre_l[2]};
+    lcrc_tscan_dev st0;
+    ts_open_state(a.file, file_len, fkey, a.seg_cap, key, true, a.idec, a.iopen_r, st0, &pre);
+    *S = st0;
+  }
+  __syncthreads();
+  const lcrc_tscan_dev& s = *S;  // (read in place: a private copy would go to scratch)
+  const uint64_t nres = s.nres;  // 0 unless the index block can be walked
+  const uint8_t* d = s.idx_dec ? a.idec : a.file + s.idx_off;
+  const uint32_t len = (uint32_t)s.idx_clen;
+  const uint64_t per = (nres + nidx - 1) / nidx;
+  const uint64_t lo = min(nres, (uint64_t)j * per), hi = min(nres, lo + per);
+  const uint64_t m = hi - lo;
+  const uint32_t restarts = len - (uint32_t)(1 + nres) * 4;
+  // round 3: the offsets rst(lo .. min(hi, nres - 1)) (rst(nres) is the restart array's offset) and, speculatively,
+  // the bytes around restarts * [lo, hi) / nres (where index entries of even size put the range)
+  const bool rstage = nres && 4 * (m + 1) <= RSL_CAP;
+  const uint32_t nrs = hi < nres ? (uint32_t)m + 1 : (uint32_t)m;
+  uint64_t sp_lo = 0, sp_n = 0;
+  if (rstage && m) {
+    const uint64_t e0 = (uint64_t)restarts * lo / nres, e1 = (uint64_t)restarts * hi / nres;
+    const uint64_t mg = (e1 - e0) / 8 + 64;
+    sp_lo = e0 > mg ? e0 - mg : 0;
+    sp_n = min((uint64_t)restarts, e1 + mg) - sp_lo;
+    if (sp_n + 4 * (m + 1) > STAGE_CAP) sp_n = 0;
+  }
+  if (rstage) wg_copy_bytes(rsl, d + restarts + 4 * lo, 4 * nrs, stage, d + sp_lo, (uint32_t)sp_n);
+  __syncthreads();
+  auto rs = [&](uint64_t k) {  // rst(lo + k), k <= m
+    return lo + k < nres ? (rstage ? load_le32(rsl + 4 * k) : load_le32(d + restarts + 4 * (lo + k))) : restarts;
+  };
+  const uint32_t s0 = lo == 0 ? 0u : rs(0), E = rs(m);
+  const uint64_t bytes = (uint64_t)E - s0;
+  const bool rbad = nres && (s0 > E || E > restarts);
+  const bool staged = rstage && !rbad && bytes + 4 * (m + 1) <= STAGE_CAP;
+  const bool covered = staged && sp_n && s0 >= sp_lo && E <= sp_lo + sp_n;
+  const uint32_t voff = covered ? (uint32_t)(s0 - sp_lo) : 0u;  // the range's first byte in stage
+  TSI_STAMP(7);
+  // round 4 (unless the speculative bytes cover the range): the segments' bytes, then the rebased offsets after them
+  // (idx_segment reads bytes; past E the speculative bytes are not needed)
+  if (staged) {
+    if (!covered) wg_copy_bytes(stage, d + s0, (uint32_t)bytes);
+    uint8_t* sr = stage + voff + bytes;
+    auto put = [&](uint64_t k, uint32_t v) {
+      sr[4 * k] = (uint8_t)v;
+      sr[4 * k + 1] = (uint8_t)(v >> 8);
+      sr[4 * k + 2] = (uint8_t)(v >> 16);
+      sr[4 * k + 3] = (uint8_t)(v >> 24);
+    };
+    uint32_t mybad = 0;
+    for (uint64_t k = tid; k < m; k += NT) {
+      const uint32_t x = rs(k), y = rs(k + 1);
+      mybad |= (x > y || y > restarts || (lo + k == 0 && x != 0) || x < s0) ? 1u : 0u;
+      put(k, x - s0);
+    }
+    if (tid == 0) put(m, (uint32_t)m);
+    if (mybad) *flags = 1;
+  }
+  __syncthreads();
+  const bool vbad = rbad || (staged && *flags);
+  TSI_STAMP(3);
+  // pass 1 over the walk's view: the staged range (an LDS pointer, local numbering; the entry offsets within the range
+  // kept in the dead restart slice) or the block in place (global numbering, offsets in local_c). Two call sites, so
+  // that the staged one reads LDS directly and neither waits on global stores
+  uint32_t* loc = (uint32_t*)rsl;
+  uint64_t run = 0, nbad = vbad ? 1 : 0;
+  auto pass1 = [&](const uint8_t* vd, uint32_t vlen, uint64_t vn, uint64_t v0, bool inl) {
+    for (uint64_t t0 = lo; t0 < hi; t0 += NT) {
+      const uint64_t i = t0 + tid;
+      uint64_t c = 0, f = 0;
+      if (i < hi) {
+        bool bad;
+        const uint64_t n = idx_segment<false>(vd, vlen, (uint32_t)vn, file_len, 0, nullptr, nullptr, i - v0, bad);
+        c = bad ? 0 : n;
+        f = bad ? 1 : 0;
+      }
+      uint64_t ec, ef, tc, tf;
+      wg_scan2<NWAVE>(c, f, sa, sb, ec, ef, tc, tf);
+      if (i < hi) {
+        if (inl)
+          loc[i - lo] = (uint32_t)(run + ec);
+        else
+          a.local_c[i] = run + ec;
+      }
+      run += tc;
+      nbad += tf;
+    }
+  };
+  if (staged)
+    pass1(stage + voff, (uint32_t)(bytes + 4 * (m + 1)), m, lo, true);
+  else
+    pass1(d, len, nres, 0, false);
+  TSI_STAMP(4);
+  if (tid == 0)
+    __hip_atomic_store(a.agg + j, TSA_READY | (nbad ? TSA_BAD : 0) | run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < 64) {
+    uint64_t before = 0, total = 0, anyb = 0;
+    for (uint32_t k = tid; k < nidx; k += 64) {
+      uint64_t v;
+      do {
+        v = __hip_atomic_load(a.agg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } while (!(v & TSA_READY));
+      total += v & TSA_COUNT;
+      before += k < j ? (v & TSA_COUNT) : 0;
+      anyb |= v & TSA_BAD;
+    }
+    for (int m = 1; m < 64; m <<= 1) {
+      before += __shfl_xor((unsigned long long)before, m, 64);
+      total += __shfl_xor((unsigned long long)total, m, 64);
+      anyb |= __shfl_xor((unsigned long long)anyb, m, 64);
+    }
+    if (tid == 0) {
+      tot[0] = before;
+      tot[1] = total;
+      tot[2] = anyb;
+      // every workgroup has published and read the totals once all nidx arrived here: the last one resets them
+      uint32_t* arrived = (uint32_t*)(a.agg + nidx);
+      if (__hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nidx - 1) {
+        for (uint32_t k = 0; k < nidx; ++k) __hip_atomic_store(a.agg + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(arrived, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  __syncthreads();
+  TSI_STAMP(5);
+  const uint64_t base = tot[0], nd = tot[1], nflag = tot[2];
+  const bool lead = j == 0 && tid == 0;
+  if (lead) {
+    *a.st = s;
+    a.iopen[2] = 0;  // k_ts_open's failure mark (every workgroup read it before publishing): clear for the next scan
+  }
+  ts_emit_body(s, a.st, lead, j == 0, nd, nflag, a.file, a.file_len, a.out, a.descs, a.cap, a.vcap, a.idec,
+               [&](const uint8_t*, uint32_t, uint64_t) {
+                 bool bad;
+                 if (staged) {
+                   for (uint64_t i = lo + tid; i < hi; i += NT)
+                     idx_segment<true>(stage + voff, (uint32_t)(bytes + 4 * (m + 1)), (uint32_t)m, file_len,
+                                       base + loc[i - lo], a.out, a.descs, i - lo, bad);
+                 } else {
+                   for (uint64_t i = lo + tid; i < hi; i += NT)
+                     idx_segment<true>(d, len, (uint32_t)nres, file_len, base + a.local_c[i], a.out, a.descs, i, bad);
+                 }
+               });
+  TSI_STAMP(6);
+}
+
+__global__ void __launch_bounds__(A_THREADS) k_ts_windows(const uint8_t* __restrict__ base, uint64_t span,
+                                                         uint64_t nreg, const uint32_t* __restrict__ gtab,
+                                                         uint32_t* __restrict__ out, uint32_t nwg,
+                                                         const lcrc_tscan_key fkey, const TsIdxArgs ia) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
+  __shared__ uint32_t wg_ticket;
+  if (blockIdx.x >= nwg) {
+    ts_index_wg(ia, fkey, blockIdx.x - nwg, gridDim.x - nwg, L);
+    return;
+  }
+  WinOne src{base, span, nreg, out, 0, nullptr, nullptr};
+  windows_body<false, false>(src, gtab, 0, 0, L, &wg_ticket, nwg);
 }
 
 // read_block_from_file's type dispatch for every block (k_tbl_finish) and, in the same thread, the framing
@@ -4931,6 +5245,27 @@ hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tsca
   const uint64_t g = bound / 256 + 1;
   LCRC_LAUNCH(lcrc_dev::k_ts_emit, dim3((unsigned)(g < gcap ? g : gcap)), dim3(256), 0, s, file, file_len, st,
               local_c, part, out, descs, cap, vcap, idec, iopen);
+  return hipGetLastError();
+}
+// the file's window pass with k_ts_index + k_ts_emit beside it (k_ts_windows): `grid` = CUs; nidx_cap: the index
+// workgroups' cap (lcrc_ctx_options.ts_grid; never more than the CUs, so that they are all resident); agg: nidx_cap +
+// 1 words, zero
+hipError_t lcrc_launch_ts_windows(int grid, const uint8_t* file, uint64_t file_len, const uint32_t* gtab, uint32_t* win,
+                                  const lcrc_tscan_key* key, uint64_t cap, uint64_t vcap, lcrc_tscan_dev* st,
+                                  uint64_t* local_c, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
+                                  const uint64_t* iopen_r, uint64_t* iopen, lcrc_tblk_dev* out, lcrc_desc_dev* descs,
+                                  uint64_t* agg, uint32_t nidx_cap, hipStream_t s) {
+  const uint64_t nreg = (file_len + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
+  const uint64_t need = (nreg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
+  const uint64_t gw = (uint64_t)grid * lcrc_dev::A_WG_PER_CU;
+  const uint32_t nwg = (uint32_t)(need < gw ? need : gw);
+  uint64_t nidx = cap / lcrc_dev::A_THREADS + 1;
+  if (nidx > nidx_cap) nidx = nidx_cap;
+  if (nidx > (uint64_t)grid) nidx = (uint64_t)grid;
+  if (nidx == 0) nidx = 1;
+  lcrc_dev::TsIdxArgs ia{file, file_len, cap, cap, vcap, nzero, st, local_c, zero, idec, iopen_r, iopen, out, descs, agg};
+  LCRC_LAUNCH(lcrc_dev::k_ts_windows, dim3((unsigned)(nwg + nidx)), dim3(lcrc_dev::A_THREADS), 0, s, file, file_len,
+              nreg, gtab, win, nwg, *key, ia);
   return hipGetLastError();
 }
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,

@@ -285,11 +285,14 @@ def test_async_long_meta_blocks(lcrc, orc, mode, masked):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("unfused", [0, 1])
 @pytest.mark.parametrize("grid", [1, 3])
-def test_async_tile_loops(lcrc, orc, grid):
-    """k_ts_index / k_ts_emit with fewer workgroups than 256-segment tiles (the context option ts_grid caps their
-    grid): a workgroup scans several tiles and emit adds the totals of every tile before each one."""
-    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_grid=grid)
+def test_async_tile_loops(lcrc, orc, grid, unfused):
+    """The index walk with fewer workgroups than tiles (the context option ts_grid caps their grid). Separate
+    launches (ts_unfused, k_ts_index / k_ts_emit): a workgroup scans several 256-segment tiles and emit adds the
+    totals of every tile before each one. Beside the window pass (k_ts_windows): a workgroup walks a range of
+    several 512-segment chunks, and the ranges' counts meet through the per-workgroup totals."""
+    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_grid=grid, ts_unfused=unfused)
     try:
         f, blocks = orc.table_build(_kvs(6000, 41), block_size=256, compression=1, index_restart_interval=1,
                                     filter_name=FILTER, filter_block=b"z" * 100)
@@ -489,3 +492,85 @@ def test_async_snappy_index_decoders_agree(lcrc, orc, v1):
         assert err == orc.table_scan_expect(bytes(g))[1]
     finally:
         eng.close()
+
+
+def _skewed_kvs(n, seed):
+    """Keys whose index entries differ tenfold in size: the first three quarters short, the rest sharing a 200-byte
+    prefix (so that the index separators keep it)."""
+    rng = np.random.default_rng(seed)
+    keys = [b"a%08d" % i for i in range(3 * n // 4)] + [b"z" + b"q" * 200 + b"%08d" % i for i in range(n - 3 * n // 4)]
+    return [(k, rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()) for k in keys]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("skew", [False, True])
+@pytest.mark.parametrize("grid", [0, 1, 5])
+def test_async_index_ranges(lcrc, orc, grid, skew):
+    """The index walk beside the window pass (k_ts_windows): each index workgroup stages its range of restart
+    segments in LDS with the range's offsets rebased (a range too long for the LDS is walked in place: one workgroup,
+    grid 1, over this ~120 KB index). Restart arrays and entries corrupted at range boundaries and inside ranges, the
+    index block re-sealed so that the walk must judge them: the verdict, count and blocks equal those of the separate
+    k_ts_index / k_ts_emit launches (ts_unfused), and the synchronous scan gives the oracle's answer. The skewed
+    table's ranges lie far from where even entries would put them (the walk's speculative load of a range's bytes
+    misses, and a second round loads them)."""
+    kvs = _skewed_kvs(16000, 17) if skew else _kvs(16000, 17)
+    f, blocks = orc.table_build(kvs, block_size=128, compression=0, index_restart_interval=1)
+    off, size, _ = _index_block(f, blocks)
+    nres = int.from_bytes(f[off + size - 4:off + size], "little")
+    assert f[off + size] == 0 and size > 80_000 and nres > 5000
+    ra = off + size - 4 * (1 + nres)
+    cap = len(blocks) + 4
+    opts = {"ts_grid": grid} if grid else {}
+    fused, unfused = lcrc.Engine(0, lcrc.MODE_REF, **opts), lcrc.Engine(0, lcrc.MODE_REF, ts_unfused=1, **opts)
+
+    def rst(g, k):
+        return int.from_bytes(g[ra + 4 * k:ra + 4 * k + 4], "little")
+
+    def put(g, k, v):
+        g[ra + 4 * k:ra + 4 * k + 4] = (v & 0xFFFFFFFF).to_bytes(4, "little")
+
+    def reseal(g):
+        g[off + size + 1:off + size + 5] = orc.crc(bytes(g[off:off + size + 1]), 0).to_bytes(4, "little")
+        return bytes(g)
+
+    cases = {"clean": f}
+    nidx = min(cap // 512 + 1, grid or 256)  # the index workgroups (lcrc_launch_ts_windows)
+    per = -(-nres // nidx)  # segments per range
+    for k in (1, per - 1, per, per + 1, nres // 2, nres - 1):
+        g = bytearray(f)
+        put(g, k, rst(g, k - 1) - 1)
+        cases[f"rst {k} before its predecessor"] = reseal(g)
+        g = bytearray(f)
+        put(g, k, rst(g, k) + 1)
+        cases[f"rst {k} + 1"] = reseal(g)
+    g = bytearray(f)
+    put(g, 0, 1)
+    cases["rst 0 = 1"] = reseal(g)
+    g = bytearray(f)
+    put(g, nres - 1, ra - off + 3)
+    cases["last rst past the array"] = reseal(g)
+    for k in (per, nres // 3):
+        g = bytearray(f)
+        g[off + rst(g, k) + 1] = 0xFF  # an entry's non_shared varint
+        cases[f"entry {k} varint"] = reseal(g)
+    try:
+        for name, case in cases.items():
+            res = []
+            for eng in (fused, unfused):
+                eng.table_scan_reserve(len(case), cap, 1 << 20)
+                s = _Scan(lcrc, case, cap)
+                try:
+                    res.append(s.run(eng))
+                finally:
+                    s.close()
+            (st, code, n, got), (ust, ucode, un, ugot) = res
+            assert (st, code, n) == (ust, ucode, un), name
+            assert (got is None and ugot is None) or _as_tuples(got) == _as_tuples(ugot), name
+            if name == "clean":
+                assert st == OK and _as_tuples(got) == orc.table_scan_expect(case)[0]
+            got, err = _sync(lcrc, fused, case, None)
+            want, werr = orc.table_scan_expect(case, None)
+            assert err == werr and (got is None or _as_tuples(got) == want), name
+    finally:
+        fused.close()
+        unfused.close()
