@@ -144,7 +144,7 @@ typedef struct lcrc_ctx_options {
   uint32_t wal_grid_b;    /* the WAL scan's range-pass workgroups (0: every resident one) */
   uint32_t ts_grid;       /* the table scan's index/emit workgroup cap (0: 4096; beside the window pass: at most
                              the CUs and 256) */
-  uint32_t ts_blocks_div; /* divisor of the table scan's range-pass grid (0: 2) */
+  uint32_t ts_blocks_div; /* divisor of the table scan's range-pass grid (0: 1, or 2 with ts_unfused) */
   uint32_t wal_onepass;   /* 1: the WAL scan finishes the records that lie in one 16 KiB region inside its window pass
                              (k_windows_wal), k_blocks only the others (0: window pass + range pass over all) */
   uint32_t ts_open_v1;    /* 1: the compressed index decoded by the one-wave k_ts_open (round 4) instead of k_ts_open2 */

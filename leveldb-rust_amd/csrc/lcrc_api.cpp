@@ -234,9 +234,11 @@ struct lcrc_ctx {
   uint64_t ts_out_cap = 0;  // the decode workspace: ts_decoded_cap + the 16-alignment of its (large) chunks
   // lcrc_ctx_options (lcrc_ctx_create_ex; tests and measurement only -- the library reads no environment variable)
   uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (tests reach the tile loops with a small one)
-  // k_blocks grid divisor of the table scan: half the range pass's usual grid co-runs with the other stream's
-  // window pass (raw table on two streams: 3,130-3,158 GiB/s against 2,806-2,926 with the full grid; alone +2 us)
-  int ts_blocks_div = 2;
+  // k_blocks grid divisor of the table scan (0: auto). With the index walk in separate launches half the range
+  // pass's usual grid co-ran best with the other stream's window pass (raw table on two streams: 3,130-3,158 GiB/s
+  // against 2,806-2,926 with the full grid); with the walk beside the window pass (k_ts_windows) the full grid is
+  // faster both alone (79.6 against 81.4 us) and on two streams (3,521-3,543 against 3,416-3,436 GiB/s)
+  int ts_blocks_div = 0;
   bool wal_onepass = false;  // lcrc_ctx_options.wal_onepass
   uint32_t batch_grid_b = 0;  // lcrc_batch's k_blocks grid (0: 2 per CU)
   uint32_t wal_grid_b = 0;    // the WAL scan's k_blocks grid (0: every resident workgroup)
@@ -1487,7 +1489,8 @@ int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
       if (!fused)
         HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr,
                                    nullptr, st));
-      HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / ctx->ts_blocks_div, file, file_len, ctx->tbl_descs.p, vcap, 0, 0,
+      const int div = ctx->ts_blocks_div ? ctx->ts_blocks_div : fused ? 1 : 2;
+      HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / div, file, file_len, ctx->tbl_descs.p, vcap, 0, 0,
                                 nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     }

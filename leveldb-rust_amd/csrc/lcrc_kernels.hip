@@ -3211,6 +3211,7 @@ __global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ fil
 // acquire/release at agent scope would write back / invalidate the XCD's L2 on every poll, under the window stream.
 // (The reset cannot overtake a reader: each workgroup's arrival depends on the values it loaded.)
 constexpr uint64_t TSA_READY = 1ull << 63, TSA_BAD = 1ull << 62, TSA_COUNT = (1ull << 62) - 1;
+static_assert(A_THREADS >= 256, "a thread per index workgroup's total (at most 256)");
 struct TsIdxArgs {
   const uint8_t* file;
   uint64_t file_len;
@@ -3422,32 +3423,27 @@ __device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint
   TSI_STAMP(4);
   if (tid == 0)
     __hip_atomic_store(a.agg + j, TSA_READY | (nbad ? TSA_BAD : 0) | run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid < 64) {
-    uint64_t before = 0, total = 0, anyb = 0;
-    for (uint32_t k = tid; k < nidx; k += 64) {
-      uint64_t v;
-      do {
-        v = __hip_atomic_load(a.agg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } while (!(v & TSA_READY));
-      total += v & TSA_COUNT;
-      before += k < j ? (v & TSA_COUNT) : 0;
-      anyb |= v & TSA_BAD;
-    }
-    for (int m = 1; m < 64; m <<= 1) {
-      before += __shfl_xor((unsigned long long)before, m, 64);
-      total += __shfl_xor((unsigned long long)total, m, 64);
-      anyb |= __shfl_xor((unsigned long long)anyb, m, 64);
-    }
-    if (tid == 0) {
-      tot[0] = before;
-      tot[1] = total;
-      tot[2] = anyb;
-      // every workgroup has published and read the totals once all nidx arrived here: the last one resets them
-      uint32_t* arrived = (uint32_t*)(a.agg + nidx);
-      if (__hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nidx - 1) {
-        for (uint32_t k = 0; k < nidx; ++k) __hip_atomic_store(a.agg + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(arrived, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+  // every workgroup's word polled by a thread of its own (one load round trip per poll, all in flight together),
+  // then summed over the workgroup
+  uint64_t v = 0;
+  if (tid < nidx) {
+    do {
+      v = __hip_atomic_load(a.agg + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while (!(v & TSA_READY));
+  }
+  const uint64_t cnt = v & TSA_COUNT;
+  uint64_t e1, e2, total, before;
+  wg_scan2<NWAVE>(cnt, tid < j ? cnt : 0, sa, sb, e1, e2, total, before);
+  const int anyb = __syncthreads_or((v & TSA_BAD) != 0);
+  if (tid == 0) {
+    tot[0] = before;
+    tot[1] = total;
+    tot[2] = anyb ? 1 : 0;
+    // every workgroup has published and read the totals once all nidx arrived here: the last one resets them
+    uint32_t* arrived = (uint32_t*)(a.agg + nidx);
+    if (__hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nidx - 1) {
+      for (uint32_t k = 0; k < nidx; ++k) __hip_atomic_store(a.agg + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(arrived, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
