@@ -3484,23 +3484,19 @@ __global__ void __launch_bounds__(A_THREADS) k_ts_windows(const uint8_t* __restr
 }
 
 // read_block_from_file's type dispatch for every block (k_tbl_finish) and, in the same thread, the framing
-// walk of the block's Snappy frame (k_snappy_size)
-// The frames' workspace sizes (the decoded bytes of chunks too large for k_ts_decode's LDS staging, see
-// snappy_frame_size) and chunk counts are scanned within the workgroup
-// (out_off, choff) with the workgroup totals in part[2 b], part[2 b + 1]: k_ts_decode's workgroup of a tile adds the
-// totals of the tiles before it (no scan launch between), and sums them all for its gate only when a tile had frames
-// (any_frame).
-__global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
-                                                   const uint32_t* __restrict__ crc,
-                                                   const uint32_t* __restrict__ mismatch,
-                                                   const uint8_t* __restrict__ file, lcrc_desc_dev* __restrict__ frames,
-                                                   uint64_t* __restrict__ out_off, uint64_t* __restrict__ choff,
-                                                   uint64_t* __restrict__ part, uint64_t* __restrict__ nchunks,
-                                                   uint8_t* __restrict__ fstatus, lcrc_tscan_dev* __restrict__ st,
-                                                   const uint32_t* __restrict__ gtab, uint32_t flags) {
-  __shared__ uint32_t z64k[1024];
-  __shared__ uint64_t sa[4], sb[4];
-  n = st->n_total < n ? st->n_total : n;
+// walk of the block's Snappy frame (k_snappy_size), for tile t (blocks [256 t, 256 t + 256)) by a workgroup of NWAVE
+// waves (threads past 256 take part in the scan with nothing). The frames' workspace sizes (the decoded bytes of
+// chunks too large for k_ts_decode's LDS staging, see snappy_frame_size) and chunk counts are scanned within the tile
+// (out_off, choff) with the tile totals in part[2 t], part[2 t + 1] and returned (to, tc). z64k: 1024 words of LDS;
+// sa, sb: NWAVE words each.
+template <int NWAVE>
+__device__ void ts_finish_tile(uint64_t t, lcrc_tblk_dev* __restrict__ blk, uint64_t n, const uint32_t* __restrict__ crc,
+                               const uint32_t* __restrict__ mismatch, const uint8_t* __restrict__ file,
+                               lcrc_desc_dev* __restrict__ frames, uint64_t* __restrict__ out_off,
+                               uint64_t* __restrict__ choff, uint64_t* __restrict__ part, uint64_t* __restrict__ nchunks,
+                               uint8_t* __restrict__ fstatus, lcrc_tscan_dev* __restrict__ st,
+                               const uint32_t* __restrict__ gtab, uint32_t flags, uint32_t* z64k, uint64_t* sa,
+                               uint64_t* sb, uint64_t& to, uint64_t& tc) {
   const uint64_t nd = st->n_data;
   const bool hf = st->has_filter;
   // the workgroup holding a split block's entry stages Z65536 in LDS (uniform decision)
@@ -3508,16 +3504,16 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
 #pragma unroll
   for (uint32_t k = 0; k < 3; ++k) {
     const uint64_t e = nd + k - (hf ? 0 : 1);
-    stage |= st->pcnt[k] && (k > 0 || hf) && e < n && e / blockDim.x == blockIdx.x;
+    stage |= st->pcnt[k] && (k > 0 || hf) && e < n && e / 256 == t;
   }
   if (stage) {
-    for (uint32_t j = threadIdx.x; j < 1024; j += blockDim.x) z64k[j] = gtab[TAB_Z64K + j];
+    for (uint32_t j = threadIdx.x; j < 1024; j += 64 * NWAVE) z64k[j] = gtab[TAB_Z64K + j];
     __syncthreads();
   }
-  if ((uint64_t)blockIdx.x * blockDim.x >= n) return;  // a whole workgroup past the count (uniform)
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = t * 256 + threadIdx.x;
+  const bool mine = threadIdx.x < 256 && i < n;
   uint64_t fsize = 0, fch = 0;
-  if (i < n) {
+  if (mine) {
     lcrc_tblk_dev b = blk[i];
     uint32_t flen = 0;
     if (b.status != 2) {
@@ -3562,17 +3558,38 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
     nchunks[i] = fch;
     fstatus[i] = ok ? 0 : 1;
   }
-  uint64_t eo, ec, to, tc;
-  wg_scan2(fsize, fch, sa, sb, eo, ec, to, tc);
-  if (i < n) {
+  uint64_t eo, ec;
+  wg_scan2<NWAVE>(fsize, fch, sa, sb, eo, ec, to, tc);
+  if (mine) {
     out_off[i] = eo;
     choff[i] = ec;
   }
   if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = to;
-    part[2 * blockIdx.x + 1] = tc;
+    part[2 * t] = to;
+    part[2 * t + 1] = tc;
     if (to | tc) st->any_frame = 1u;  // tiles with frames only (every writer stores the same 1: no atomic)
   }
+}
+
+// The table scan's finish: one workgroup per tile; k_ts_decode's workgroup of a tile adds the totals of the tiles
+// before it (no scan launch between), and sums them all for its gate only when a tile had frames (any_frame).
+// (Run as k_ts_decode's first phase instead, with the tiles' totals met by a decoupled look-back: 81.2 against
+// 78.6-79.4 us per raw scan alone -- the last tile's workgroup waits for every other tile's finish either way.)
+__global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ blk, uint64_t n,
+                                                   const uint32_t* __restrict__ crc,
+                                                   const uint32_t* __restrict__ mismatch,
+                                                   const uint8_t* __restrict__ file, lcrc_desc_dev* __restrict__ frames,
+                                                   uint64_t* __restrict__ out_off, uint64_t* __restrict__ choff,
+                                                   uint64_t* __restrict__ part, uint64_t* __restrict__ nchunks,
+                                                   uint8_t* __restrict__ fstatus, lcrc_tscan_dev* __restrict__ st,
+                                                   const uint32_t* __restrict__ gtab, uint32_t flags) {
+  __shared__ uint32_t z64k[1024];
+  __shared__ uint64_t sa[4], sb[4];
+  n = st->n_total < n ? st->n_total : n;
+  if ((uint64_t)blockIdx.x * 256 >= n) return;  // a whole workgroup past the count (uniform)
+  uint64_t to, tc;
+  ts_finish_tile<4>(blockIdx.x, blk, n, crc, mismatch, file, frames, out_off, choff, part, nchunks, fstatus, st, gtab,
+                    flags, z64k, sa, sb, to, tc);
 }
 
 // the reference's order of outcomes, once every checksum is known; the count and the status for the caller
@@ -4057,15 +4074,26 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   // the block count from fields ts_final leaves alone (it may shrink n_total while later workgroups start)
   const bool live = st->status == TS_OK && !st->idx_only;
   const uint64_t n = live ? st->n_data + (st->has_filter ? 3 : 2) : 0;
-  const uint64_t tiles = (n + 255) / 256, tail = n > 3 ? n - 3 : 0, t = blockIdx.x;
-  const bool last = n && t == (n - 1) / 256;
+  // one workgroup per 256 frames below the last three blocks (filter, metaindex, index: the last workgroup's); a
+  // table of 65,536 data blocks is then 256 workgroups, all resident at once (one per CU), not 257
+  const uint64_t tail = n > 3 ? n - 3 : 0, tiles = n ? (tail + 255) / 256 + (tail ? 0 : 1) : 0, t = blockIdx.x;
+  const bool last = n && t == tiles - 1;
   if (t >= tiles && t != 0) return;  // (workgroup 0 runs ts_final when nothing is live)
+#ifdef LCRC_PROBE_CLOCK  // diagnostic build: phase stamps of workgroup t in lcrc_dbg_stamp row 2304 + t
+#define TD_STAMP(k) \
+  if (threadIdx.x == 0 && t < 768) lcrc_dbg_stamp[(2304 + t) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define TD_STAMP(k)
+#endif
+  TD_STAMP(0);
+  uint64_t before = 0, total = 0, chunks = 0;
+  bool over = false;
   // the gate: the decoded total and the chunk count the frames need against the workspace (decided alike by every
   // workgroup from the tile totals; workgroup 0 records it -- over: the host path). No frames: no sums.
-  uint64_t before = 0, total = 0, chunks = 0;
   if (n && st->any_frame) {
     unsigned long long xb = 0, xo = 0, xc = 0;
-    for (uint64_t w = lane; w < tiles; w += 64) {
+    for (uint64_t w = lane; w < (n + 255) / 256; w += 64) {  // (k_ts_finish's tiles: the last may hold only some
+      // of the last three blocks)
       const uint64_t v = tparts[2 * w];
       xo += v;
       xc += tparts[2 * w + 1];
@@ -4080,7 +4108,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     total = xo;
     chunks = xc;
   }
-  const bool over = total > ts_out_cap;
+  over = total > ts_out_cap;
   // recorded by workgroup 0 and by the last tile's workgroup (the same values): the last one runs ts_final and is the
   // only one that changes st->status, so its `live` is always the scan's own; workgroup 0 may read a status the last
   // one has already set to TS_HOST (frames over the workspace) and skip the record
@@ -4090,6 +4118,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     st->gate = over ? 1u : chunks == 0 ? 2u : 0u;
     st->n_chunks = over ? 0 : chunks;
   }
+  TD_STAMP(3);
   const bool dec = !over && chunks;
   for (uint32_t i = threadIdx.x; i < 256 + 16; i += blockDim.x) bad[i] = 0;
   if (dec)
@@ -4179,7 +4208,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
         const uint64_t tb = (f / 256 == t) ? before : 0;  // (a frame among the last three in an earlier tile: its
         // workspace offset is that tile's; the tiles before it are summed here)
         uint64_t base_o = tb;
-        if (f / 256 != t) {
+        if (f / 256 != t) {  // (the tile after this workgroup's: k_ts_finish's tiles are 256 blocks)
           unsigned long long xb = 0;
           for (uint64_t w = lane; w < f / 256; w += 64) xb += tparts[2 * w];
           for (int d = 1; d < 64; d <<= 1) xb += __shfl_xor(xb, d, 64);
@@ -4199,11 +4228,13 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   };
   const uint64_t j = t * 256 + threadIdx.x;
   if (threadIdx.x < 256 && j < tail) content(j, bad[threadIdx.x] != 0);
+  TD_STAMP(4);
   if (threadIdx.x == 0 && (last || (n == 0 && t == 0))) {
     for (uint64_t k = tail; k < n; ++k) content(k, bad[256 + (k - tail)] != 0);
     if (over && st->status == TS_OK) st->status = TS_HOST;
     ts_final(st, blk, n_out, status_out);
   }
+  TD_STAMP(5);
 }
 
 #ifndef LCRC_TO_TWO_PHASE  // k_ts_open's index chunks through the two-phase decoder (0: the wave decoder)

@@ -574,3 +574,25 @@ def test_async_index_ranges(lcrc, orc, grid, skew):
     finally:
         fused.close()
         unfused.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("unfused", [0, 1])
+def test_async_last_three_at_tile_edges(lcrc, orc, unfused):
+    """The last three blocks (filter as a Snappy frame, metaindex, Snappy-framed index) at every position across a
+    256-block tile edge: k_ts_decode's last workgroup finishes, decodes and judges them -- fused, also the finish of a
+    tile that holds only some of them -- and the workspace offsets of their frames follow the tiles before."""
+    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_unfused=unfused)
+    try:
+        for k in (1, 2, 252, 253, 254, 255, 256, 257, 509, 510, 511, 512, 513):
+            f, blocks = orc.table_build(_seq_kvs(k), block_size=1, compression=1, filter_name=FILTER,
+                                        filter_block=b"f" * 300)
+            assert [b[2] for b in blocks].count(0) == k and f[sum(blocks[-3][:2])] == 1  # the filter: a frame
+            assert _expect_async(lcrc, eng, orc, f, FILTER, cap=len(blocks) + 4, snappy_index=True) == OK, k
+            g = bytearray(f)
+            off, n, _ = blocks[-3]
+            g[off + n // 2] ^= 0x40  # the filter's frame corrupted, its block trailer re-sealed
+            g[off + n + 1:off + n + 5] = orc.crc(bytes(g[off:off + n + 1]), 0).to_bytes(4, "little")
+            assert _expect_async(lcrc, eng, orc, bytes(g), FILTER, cap=len(blocks) + 4, snappy_index=True) == OK, k
+    finally:
+        eng.close()
