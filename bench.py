@@ -53,8 +53,9 @@ QMAX = 32  # batches per queued launch (MAX_QJOBS in lcrc_kernels.hip)
 MIXED_QUEUE = 1  # mixed config: steps per lcrc_batch_queue submission (1: one lcrc_batch per step)
 WAL_QUEUE = 1  # wal config: scans per lcrc_wal_scan_queue submission (1: one lcrc_wal_scan_async per step)
 WAL_KERNELS = 4  # lcrc_wal_scan_async: header walk, record emit, window pass, range pass
-TABLE_KERNELS = 6  # lcrc_table_scan_async: index, emit, windows, blocks, finish, decode + chunk checks + close
-# (+ 1 with LCRC_TSCAN_SNAPPY_INDEX: the compressed table's Snappy-framed index decoded first, k_ts_open)
+TABLE_KERNELS = 4  # lcrc_table_scan_async: window pass with the index walk beside it (k_ts_windows), range pass,
+# finish, decode + chunk checks + close (+ 2 with the context option ts_unfused: the index walk and the handles as
+# launches of their own; + 1 with LCRC_TSCAN_SNAPPY_INDEX: the Snappy-framed index decoded first, k_ts_open2)
 
 
 def parse(argv=None):
@@ -670,7 +671,7 @@ def workload_table(m, synth, engs, rank, device, args):
            "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async",
            "snappy_index": bool(args.compression and framed[kinds == m.TBLK_INDEX].any())}
     w = Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, sample, lambda: scanned["crc"].copy(),
-                 per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si),
+                 per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si) + 2 * int(bool(args.engine_opts.get("ts_unfused"))),
                  kernel_events=not (args.table_sync or args.graph))
     w.single = single
     # the compressed scan's decoders are bound by instruction issue (SQ counters: VALU + SALU per element, DESIGN.md
