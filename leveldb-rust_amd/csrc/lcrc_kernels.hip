@@ -4069,14 +4069,16 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
                                                             uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t td_lds[];
   uint32_t* const T = (uint32_t*)td_lds;
-  uint8_t* const bad = td_lds + TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // 256 tile flags + the last three
+  uint8_t* const bad = td_lds + TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // 256 tile flags + the meta blocks
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
   // the block count from fields ts_final leaves alone (it may shrink n_total while later workgroups start)
   const bool live = st->status == TS_OK && !st->idx_only;
   const uint64_t n = live ? st->n_data + (st->has_filter ? 3 : 2) : 0;
-  // one workgroup per 256 frames below the last three blocks (filter, metaindex, index: the last workgroup's); a
-  // table of 65,536 data blocks is then 256 workgroups, all resident at once (one per CU), not 257
-  const uint64_t tail = n > 3 ? n - 3 : 0, tiles = n ? (tail + 255) / 256 + (tail ? 0 : 1) : 0, t = blockIdx.x;
+  // one workgroup per 256 data blocks; the meta blocks after them (filter, metaindex, index) are the last workgroup's
+  // (its wave 0, after the rows). A table of 65,536 data blocks is then 256 workgroups, all resident at once (one per
+  // CU), not 257; and a table without a filter keeps its last data block in the rows (as one of "the last three" it
+  // went through the whole-wave decoder alone, after the rows: ~35 us of the scan's tail)
+  const uint64_t tail = live ? st->n_data : 0, tiles = n ? (tail + 255) / 256 + (tail ? 0 : 1) : 0, t = blockIdx.x;
   const bool last = n && t == tiles - 1;
   if (t >= tiles && t != 0) return;  // (workgroup 0 runs ts_final when nothing is live)
 #ifdef LCRC_PROBE_CLOCK  // diagnostic build: phase stamps of workgroup t in lcrc_dbg_stamp row 2304 + t
@@ -4093,7 +4095,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   if (n && st->any_frame) {
     unsigned long long xb = 0, xo = 0, xc = 0;
     for (uint64_t w = lane; w < (n + 255) / 256; w += 64) {  // (k_ts_finish's tiles: the last may hold only some
-      // of the last three blocks)
+      // of the meta blocks)
       const uint64_t v = tparts[2 * w];
       xo += v;
       xc += tparts[2 * w + 1];
@@ -4125,11 +4127,11 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     for (uint32_t i = threadIdx.x; i < TD_TAB_WORDS / 4; i += blockDim.x) ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i];
   __syncthreads();
   if (dec) {
-    // this tile's frames (the last three blocks excluded): four per wave at a time, one per row, over a static share of
+    // this tile's frames (the meta blocks excluded): four per wave at a time, one per row, over a static share of
     // the tile's 64 groups of four -- waves 2 and 3 take 12, the others 10: the hardware puts a workgroup's waves on
     // the SIMDs in order, so waves 0/4 and 1/5 share a SIMD (issue rate ~1.6x one wave's, measured with rows of
     // fewer frames) and 2 and 3 have one each. A frame the row cannot decode (bad[] = 2) then through the whole wave,
-    // in two waves' row areas; then the last workgroup's wave 0 the last three blocks.
+    // in two waves' row areas; then the last workgroup's wave 0 the meta blocks.
     const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
     const uint32_t r = lane >> 4, g = lane & 15;
 #ifndef LCRC_TD_SPLIT
@@ -4205,8 +4207,8 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
         }
     if (last && wv == 0)
       for (uint64_t f = tail; f < n; ++f) {
-        const uint64_t tb = (f / 256 == t) ? before : 0;  // (a frame among the last three in an earlier tile: its
-        // workspace offset is that tile's; the tiles before it are summed here)
+        const uint64_t tb = (f / 256 == t) ? before : 0;  // (a meta block in k_ts_finish's tile after this
+        // workgroup's: its workspace offset is that tile's; the tiles before it are summed here)
         uint64_t base_o = tb;
         if (f / 256 != t) {  // (the tile after this workgroup's: k_ts_finish's tiles are 256 blocks)
           unsigned long long xb = 0;
