@@ -3496,7 +3496,10 @@ __device__ void ts_finish_tile(uint64_t t, lcrc_tblk_dev* __restrict__ blk, uint
                                uint64_t* __restrict__ choff, uint64_t* __restrict__ part, uint64_t* __restrict__ nchunks,
                                uint8_t* __restrict__ fstatus, lcrc_tscan_dev* __restrict__ st,
                                const uint32_t* __restrict__ gtab, uint32_t flags, uint32_t* z64k, uint64_t* sa,
-                               uint64_t* sb, uint64_t& to, uint64_t& tc) {
+                               uint64_t* sb, uint64_t& to, uint64_t& tc, const lcrc_tblk_dev& b0, uint32_t c0,
+                               uint32_t m0) {
+  // b0, c0, m0: this thread's block record, CRC and mismatch word, loaded by the caller before the state
+  const uint64_t i = t * 256 + threadIdx.x;
   const uint64_t nd = st->n_data;
   const bool hf = st->has_filter;
   // the workgroup holding a split block's entry stages Z65536 in LDS (uniform decision)
@@ -3510,16 +3513,15 @@ __device__ void ts_finish_tile(uint64_t t, lcrc_tblk_dev* __restrict__ blk, uint
     for (uint32_t j = threadIdx.x; j < 1024; j += 64 * NWAVE) z64k[j] = gtab[TAB_Z64K + j];
     __syncthreads();
   }
-  const uint64_t i = t * 256 + threadIdx.x;
   const bool mine = threadIdx.x < 256 && i < n;
   uint64_t fsize = 0, fch = 0;
   if (mine) {
-    lcrc_tblk_dev b = blk[i];
+    lcrc_tblk_dev b = b0;
     uint32_t flen = 0;
     if (b.status != 2) {
-      b.crc = crc[i];
+      b.crc = c0;
       b.type = file[b.offset + b.size];
-      b.status = (mismatch[i >> 5] >> (i & 31)) & 1;
+      b.status = (m0 >> (i & 31)) & 1;
       const uint32_t k = i < nd ? 3u : (uint32_t)(i - nd) + (hf ? 0u : 1u);
       if (k < 3 && st->pcnt[k]) {
         // a block verified as pieces: crc(A || B) = Z_|B|(crc(A)) ^ crc(B) (init = xorout = ~0); every piece
@@ -3585,11 +3587,21 @@ __global__ void __launch_bounds__(256) k_ts_finish(lcrc_tblk_dev* __restrict__ b
                                                    const uint32_t* __restrict__ gtab, uint32_t flags) {
   __shared__ uint32_t z64k[1024];
   __shared__ uint64_t sa[4], sb[4];
+  // the block's record, CRC and mismatch word loaded before the state (the count) is known, in the same round trip
+  // (every index below n, the arrays' length, may be read)
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  lcrc_tblk_dev b0 = {};
+  uint32_t c0 = 0, m0 = 0;
+  if (i < n) {
+    b0 = blk[i];
+    c0 = crc[i];
+    m0 = mismatch[i >> 5];
+  }
   n = st->n_total < n ? st->n_total : n;
   if ((uint64_t)blockIdx.x * 256 >= n) return;  // a whole workgroup past the count (uniform)
   uint64_t to, tc;
   ts_finish_tile<4>(blockIdx.x, blk, n, crc, mismatch, file, frames, out_off, choff, part, nchunks, fstatus, st, gtab,
-                    flags, z64k, sa, sb, to, tc);
+                    flags, z64k, sa, sb, to, tc, b0, c0, m0);
 }
 
 // the reference's order of outcomes, once every checksum is known; the count and the status for the caller
