@@ -4078,9 +4078,19 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
                                                             lcrc_tscan_dev* __restrict__ st, lcrc_tblk_dev* __restrict__ blk,
                                                             const uint32_t* __restrict__ tab_c, uint64_t ts_out_cap,
                                                             const uint64_t* __restrict__ tparts,
-                                                            uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out) {
+                                                            uint64_t* __restrict__ n_out, uint32_t* __restrict__ status_out,
+                                                            uint64_t bound) {
   extern __shared__ __attribute__((aligned(16))) uint8_t td_lds[];
   uint32_t* const T = (uint32_t*)td_lds;
+  // the content verdict's inputs for this thread's block, loaded with the state (bound: the arrays' length)
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint8_t fs_j = 0;
+  uint64_t off_j = 0, off_p = 0;
+  if (threadIdx.x < 256 && j < bound) {
+    fs_j = fstatus[j];
+    off_j = blk[j].offset;
+    off_p = j ? blk[j - 1].offset : 0;
+  }
   uint8_t* const bad = td_lds + TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // 256 tile flags + the meta blocks
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
   // the block count from fields ts_final leaves alone (it may shrink n_total while later workgroups start)
@@ -4240,8 +4250,10 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     if (fstatus[j] || fb) blk[j].status = 3;  // LCRC_TBLK_BAD_CONTENT
     if (j > 0 && blk[j - 1].offset > blk[j].offset) st->unsorted = 1;
   };
-  const uint64_t j = t * 256 + threadIdx.x;
-  if (threadIdx.x < 256 && j < tail) content(j, bad[threadIdx.x] != 0);
+  if (threadIdx.x < 256 && j < tail) {  // (content() with the values loaded at the start)
+    if (fs_j || bad[threadIdx.x]) blk[j].status = 3;  // LCRC_TBLK_BAD_CONTENT
+    if (j > 0 && off_p > off_j) st->unsorted = 1;
+  }
   TD_STAMP(4);
   if (threadIdx.x == 0 && (last || (n == 0 && t == 0))) {
     for (uint64_t k = tail; k < n; ++k) content(k, bad[256 + (k - tail)] != 0);
@@ -5330,7 +5342,7 @@ hipError_t lcrc_launch_ts_decode(const uint8_t* file, const lcrc_desc_dev* frame
   if (attr != hipSuccess) return attr;
   const uint64_t g = (bound + 255) / 256;
   LCRC_LAUNCH(lcrc_dev::k_ts_decode, dim3((unsigned)(g ? g : 1)), dim3(64 * lcrc_dev::TD_WAVES), lcrc_dev::TD_LDS, s,
-              file, frames, out_off, out, fstatus, st, blk, tab_c, ts_out_cap, tparts, n_out, status_out);
+              file, frames, out_off, out, fstatus, st, blk, tab_c, ts_out_cap, tparts, n_out, status_out, bound);
   return hipGetLastError();
 }
 
