@@ -42,6 +42,18 @@ def test_struct_layouts(lcrc):
     assert ctypes.sizeof(lcrc._WJob) == 40 and lcrc._WJob.n_recs.offset == 32  # lcrc_wjob
 
 
+def test_ctx_options_mirror(lcrc):
+    """The ctypes mirror of lcrc_ctx_options has the header's fields in the header's order (every field a 32-bit
+    integer), so Engine(**options) sets what lcrc_ctx_create_ex reads."""
+    with open(os.path.join(ROOT, "include", "lcrc.h")) as f:
+        src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    body = re.search(r"typedef struct lcrc_ctx_options \{(.*?)\} lcrc_ctx_options;", src, flags=re.S).group(1)
+    fields = re.findall(r"(u?int32_t)\s+(\w+);", body)
+    assert [n for _, n in fields] == [n for n, _ in lcrc._CtxOptions._fields_]
+    import ctypes
+    assert ctypes.sizeof(lcrc._CtxOptions) == 4 * len(fields)
+
+
 @pytest.mark.parametrize("n", [0, 1, 3, 7, 8, 9, 16, 100, 4096, 100003])
 def test_scalar_value(lcrc, orc, n):
     d = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
