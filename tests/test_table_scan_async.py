@@ -596,3 +596,32 @@ def test_async_last_three_at_tile_edges(lcrc, orc, unfused):
             assert _expect_async(lcrc, eng, orc, bytes(g), FILTER, cap=len(blocks) + 4, snappy_index=True) == OK, k
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_async_two_contexts_concurrent(lcrc, orc):
+    """Two contexts scanning on their own streams at once, several rounds back to back (as bench.py's two scanners
+    do): each scan's index workgroups wait only for their own launch's totals, and the totals' words are zeroed
+    for the next scan by the last arrival -- every result equals the oracle's."""
+    f1, b1 = orc.table_build(_kvs(5000, 71), block_size=256, compression=0, filter_name=FILTER, filter_block=b"a" * 50)
+    f2, b2 = orc.table_build(_kvs(7000, 72), block_size=512, compression=1, filter_name=FILTER, filter_block=b"b" * 70)
+    engs = [lcrc.Engine(0, lcrc.MODE_REF), lcrc.Engine(0, lcrc.MODE_REF)]
+    scans = []
+    try:
+        for eng, (f, blocks) in zip(engs, ((f1, b1), (f2, b2))):
+            eng.table_scan_reserve(len(f), len(blocks) + 4, 1 << 22)
+            scans.append((_Scan(lcrc, f, len(blocks) + 4), f))
+        want = [orc.table_scan_expect(f, FILTER)[0] for f in (f1, f2)]
+        for _ in range(6):
+            for eng, (s, _f) in zip(engs, scans):
+                eng.table_scan_async(s.file, s.n, s.blocks, s.cap, s.count, s.status, FILTER)
+            for eng in engs:
+                eng.sync()
+            for (s, _f), w in zip(scans, want):
+                st, code, n, got = s.read()
+                assert st == OK and sorted(_as_tuples(got)) == w
+    finally:
+        for s, _f in scans:
+            s.close()
+        for eng in engs:
+            eng.close()
