@@ -54,8 +54,8 @@ MIXED_QUEUE = 1  # mixed config: steps per lcrc_batch_queue submission (1: one l
 WAL_QUEUE = 1  # wal config: scans per lcrc_wal_scan_queue submission (1: one lcrc_wal_scan_async per step)
 WAL_KERNELS = 4  # lcrc_wal_scan_async: header walk, record emit, window pass, range pass
 TABLE_KERNELS = 4  # lcrc_table_scan_async: window pass with the index walk beside it (k_ts_windows), range pass,
-# finish, decode + chunk checks + close (+ 2 with the context option ts_unfused: the index walk and the handles as
-# launches of their own; + 1 with LCRC_TSCAN_SNAPPY_INDEX: the Snappy-framed index decoded first, k_ts_open2)
+# finish, decode + chunk checks + close (+ 1 with LCRC_TSCAN_SNAPPY_INDEX: the Snappy-framed index decoded first,
+# k_ts_open2)
 
 
 def parse(argv=None):
@@ -671,7 +671,7 @@ def workload_table(m, synth, engs, rank, device, args):
            "lcrc_table_scan_async captured in a HIP graph, replayed" if args.graph else "lcrc_table_scan_async",
            "snappy_index": bool(args.compression and framed[kinds == m.TBLK_INDEX].any())}
     w = Workload(run, int(sum(b[1] + 1 for b in blocks)), cfg, None, sample, lambda: scanned["crc"].copy(),
-                 per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si) + 2 * int(bool(args.engine_opts.get("ts_unfused"))),
+                 per_step_sync=bool(args.table_sync), engines=scanners, kernels_per_step=TABLE_KERNELS + int(si),
                  kernel_events=not (args.table_sync or args.graph))
     w.single = single
     # the compressed scan's decoders are bound by instruction issue (SQ counters: VALU + SALU per element, DESIGN.md
@@ -938,9 +938,8 @@ def main(argv=None):
         "pct_hbm_peak": round(100.0 * (w.nbytes * args.steps * world / elapsed_max / world) / (PEAK_GBS * 1e9), 2),
         "per_gpu": per_gpu,
     }
-    # profiles/ tag (tablez: the compressed table; walop: the one-pass WAL scan; tablezv1: the round-4 index decoder)
-    prof_config = args.config + ("z" if args.compression else "") + \
-        ("op" if args.engine_opts.get("wal_onepass") else "") + ("v1" if args.engine_opts.get("ts_open_v1") else "")
+    # profiles/ tag (tablez: the compressed table)
+    prof_config = args.config + ("z" if args.compression else "")
     if timers and gpu_ms:
         one_stream = len(timers) == 1 and not w.per_step_sync
         launch_s = gpu_ms / 1e3 / cov_launches

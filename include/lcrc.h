@@ -142,14 +142,11 @@ typedef struct lcrc_ctx_options {
   int32_t general;        /* general path: 0 auto, 1 the one-pass k_ranges, 2 window pass + range pass always */
   uint32_t batch_grid_b;  /* lcrc_batch's range-pass workgroups (0: 2 per CU) */
   uint32_t wal_grid_b;    /* the WAL scan's range-pass workgroups (0: every resident one) */
-  uint32_t ts_grid;       /* the table scan's index/emit workgroup cap (0: 4096; beside the window pass: at most
+  uint32_t ts_grid;       /* the table scan's index workgroup cap (0: one per 512 blocks of result capacity, at most
                              the CUs and 256) */
-  uint32_t ts_blocks_div; /* divisor of the table scan's range-pass grid (0: 1, or 2 with ts_unfused) */
-  uint32_t wal_onepass;   /* 1: the WAL scan finishes the records that lie in one 16 KiB region inside its window pass
-                             (k_windows_wal), k_blocks only the others (0: window pass + range pass over all) */
-  uint32_t ts_open_v1;    /* 1: the compressed index decoded by the one-wave k_ts_open (round 4) instead of k_ts_open2 */
-  uint32_t ts_unfused;    /* 1: the table scan's index walk and handles as two launches before the window pass (round
-                             4) instead of beside it in the window pass's launch */
+  uint32_t ts_blocks_div; /* divisor of the table scan's range-pass grid (0: 1) */
+  uint32_t reserved[3];   /* must be 0 (LCRC_EINVAL otherwise): the round-5 measurement variants wal_onepass,
+                             ts_open_v1 and ts_unfused were measured slower and removed */
 } lcrc_ctx_options;
 int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, const lcrc_ctx_options* opt);
 int lcrc_ctx_destroy(lcrc_ctx* ctx);

@@ -89,8 +89,7 @@ class _WJob(ctypes.Structure):
 class _CtxOptions(ctypes.Structure):
     _fields_ = [("size", ctypes.c_uint32), ("general", ctypes.c_int32), ("batch_grid_b", ctypes.c_uint32),
                 ("wal_grid_b", ctypes.c_uint32), ("ts_grid", ctypes.c_uint32), ("ts_blocks_div", ctypes.c_uint32),
-                ("wal_onepass", ctypes.c_uint32), ("ts_open_v1", ctypes.c_uint32),
-                ("ts_unfused", ctypes.c_uint32)]
+                ("reserved", ctypes.c_uint32 * 3)]
 
 
 GENERAL_PATHS = {"auto": 0, "ranges": 1, "blocks": 2}
@@ -409,8 +408,7 @@ class Engine:
     """One device + one CRC mode (``lcrc_ctx``). All batched calls are GPU-only.
 
     Keyword options (``lcrc_ctx_create_ex``, tests and measurement only): ``general`` ("auto" | "ranges" |
-    "blocks"), ``batch_grid_b``, ``wal_grid_b``, ``ts_grid``, ``ts_blocks_div``, ``wal_onepass`` (the WAL scan
-    finishes region-contained records inside its window pass); unset = the library default."""
+    "blocks"), ``batch_grid_b``, ``wal_grid_b``, ``ts_grid``, ``ts_blocks_div``; unset = the library default."""
 
     def __init__(self, device=0, mode=MODE_C, flags=0, **options):
         self.device, self.mode, self.flags = device, mode, flags
@@ -421,8 +419,7 @@ class Engine:
             for k, v in options.items():
                 if k == "general":
                     v = GENERAL_PATHS[v] if isinstance(v, str) else int(v)
-                elif k not in ("batch_grid_b", "wal_grid_b", "ts_grid", "ts_blocks_div", "wal_onepass", "ts_open_v1",
-                               "ts_unfused"):
+                elif k not in ("batch_grid_b", "wal_grid_b", "ts_grid", "ts_blocks_div"):
                     raise TypeError(f"Engine: unknown option {k!r}")
                 setattr(o, k, int(v))
             _check(lib().lcrc_ctx_create_ex(ctypes.byref(ctx), device, mode, flags, ctypes.byref(o)),

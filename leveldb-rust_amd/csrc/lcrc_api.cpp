@@ -38,22 +38,14 @@ hipError_t lcrc_launch_ranges(bool uniform, int grid, const uint8_t* base, uint6
 hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint32_t njobs, const uint32_t* gtab,
                                      uint32_t fin, uint32_t flags, hipStream_t st, hipEvent_t t_start,
                                      hipEvent_t t_stop);
-hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
-                                lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
-                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
-                                const uint64_t* iopen, hipStream_t s);
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uint32_t* tab_c, uint8_t* idec,
                                uint64_t idec_cap, uint64_t* iopen, uint32_t* scratch, hipStream_t s);
 uint64_t lcrc_ts_open_scratch_words();
-hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
-                               const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t vcap, uint64_t bound, uint32_t gcap, const uint8_t* idec, uint64_t* iopen,
-                               hipStream_t s);
-hipError_t lcrc_launch_ts_windows(int grid, const uint8_t* file, uint64_t file_len, const uint32_t* gtab, uint32_t* win,
-                                  const lcrc_tscan_key* key, uint64_t cap, uint64_t vcap, lcrc_tscan_dev* st,
-                                  uint64_t* local_c, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
-                                  const uint64_t* iopen_r, uint64_t* iopen, lcrc_tblk_dev* out, lcrc_desc_dev* descs,
-                                  uint64_t* agg, uint32_t nidx_cap, hipStream_t s);
+hipError_t lcrc_launch_ts_windows(int grid, bool windows, const uint8_t* file, uint64_t file_len, const uint32_t* gtab,
+                                  uint32_t* win, const lcrc_tscan_key* key, uint64_t cap, uint64_t vcap,
+                                  lcrc_tscan_dev* st, uint64_t* local_c, uint32_t* zero, uint64_t nzero,
+                                  const uint8_t* idec, const uint64_t* iopen_r, uint64_t* iopen, lcrc_tblk_dev* out,
+                                  lcrc_desc_dev* descs, uint64_t* agg, uint32_t nidx_cap, hipStream_t s);
 hipError_t lcrc_launch_ts_finish(lcrc_tblk_dev* blk, uint64_t n, const uint32_t* crc, const uint32_t* mismatch,
                                  const uint8_t* file, lcrc_desc_dev* frames, uint64_t* out_off, uint64_t* choff,
                                  uint64_t* part, uint64_t* nchunks, uint8_t* fstatus, lcrc_tscan_dev* st,
@@ -75,12 +67,6 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t m, hipStream_t st);
-hipError_t lcrc_launch_wal_onepass(int grid_a, int grid_b, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
-                                   uint32_t* counts, uint2* slots, uint8_t* stops, uint64_t* local, uint64_t* part,
-                                   uint32_t* rl_cnt, uint4* rl, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
-                                   uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, uint64_t* n_kb,
-                                   uint32_t* win, const uint32_t* gtab, uint32_t init, uint32_t xorout, uint32_t poly,
-                                   uint32_t* crcs, hipStream_t st);
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
                                    uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
                                    hipStream_t st);
@@ -180,8 +166,6 @@ struct lcrc_ctx {
   DevBuf<uint64_t> wal_offsets;
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs;
-  DevBuf<uint32_t> wal_rlcnt;  // (wal_onepass) per 16 KiB region: records the window pass finishes
-  DevBuf<uint4> wal_rl;        // (wal_onepass) their lists, WAL_RMAX slots per region
   // lcrc_batch_multi: this context's shard (the byte span its descriptors cover, the rebased descriptors,
   // CRCs and mismatch words)
   DevBuf<uint8_t> ms_data;
@@ -221,11 +205,9 @@ struct lcrc_ctx {
   DevBuf<lcrc_tscan_dev> ts_state;
   DevBuf<uint8_t> ts_idx;    // table scan: a Snappy-framed index block decoded on the device (k_ts_open)
   DevBuf<uint64_t> ts_open;  // k_ts_open's verdict words (zeroed when allocated)
-  DevBuf<uint64_t> ts_agg;   // k_ts_windows' index workgroups: their entry counts and arrival count (zeroed when
-                             // allocated; the last arrival zeroes them again)
+  DevBuf<uint64_t> ts_agg;   // k_ts_windows' index workgroups: their entry counts, done count and ticket (zeroed when
+                             // allocated; the last ticket zeroes them again)
   DevBuf<uint32_t> ts_open_scr;  // k_ts_open2's per-workgroup source arrays (pointer jumping)
-  bool ts_open_v1 = false;       // lcrc_ctx_options.ts_open_v1: the one-wave k_ts_open instead
-  bool ts_unfused = false;       // lcrc_ctx_options.ts_unfused: k_ts_index + k_ts_emit as launches of their own
   DevBuf<lcrc_tblk_dev> ts_blocks;
   DevBuf<uint64_t> ts_count;
   uint32_t* ts_count_status = nullptr;  // device: the async scan's status words (synchronous wrapper)
@@ -234,12 +216,9 @@ struct lcrc_ctx {
   uint64_t ts_out_cap = 0;  // the decode workspace: ts_decoded_cap + the 16-alignment of its (large) chunks
   // lcrc_ctx_options (lcrc_ctx_create_ex; tests and measurement only -- the library reads no environment variable)
   uint32_t ts_grid = 4096;  // the table scan's index/emit grid cap (tests reach the tile loops with a small one)
-  // k_blocks grid divisor of the table scan (0: auto). With the index walk in separate launches half the range
-  // pass's usual grid co-ran best with the other stream's window pass (raw table on two streams: 3,130-3,158 GiB/s
-  // against 2,806-2,926 with the full grid); with the walk beside the window pass (k_ts_windows) the full grid is
-  // faster both alone (79.6 against 81.4 us) and on two streams (3,521-3,543 against 3,416-3,436 GiB/s)
+  // k_blocks grid divisor of the table scan (0: 1). With the index walk beside the window pass (k_ts_windows) the
+  // full grid is faster both alone (79.6 against 81.4 us) and on two streams (3,521-3,543 against 3,416-3,436 GiB/s)
   int ts_blocks_div = 0;
-  bool wal_onepass = false;  // lcrc_ctx_options.wal_onepass
   uint32_t batch_grid_b = 0;  // lcrc_batch's k_blocks grid (0: 2 per CU)
   uint32_t wal_grid_b = 0;    // the WAL scan's k_blocks grid (0: every resident workgroup)
 };
@@ -355,9 +334,15 @@ int lcrc_ctx_create(lcrc_ctx** out, int device, int mode, uint32_t flags) {
 
 int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, const lcrc_ctx_options* opt) {
   if (!out || (mode != LCRC_MODE_REF && mode != LCRC_MODE_C)) return LCRC_EINVAL;
-  // (a caller built against the round-4 header passes the struct without wal_onepass: accepted, option off)
-  if (opt && (opt->size < offsetof(lcrc_ctx_options, wal_onepass) || opt->general < 0 || opt->general > 2))
+  // (a caller built against the round-4 header passes the struct without the reserved words: accepted)
+  if (opt && (opt->size < offsetof(lcrc_ctx_options, reserved) || opt->general < 0 || opt->general > 2))
     return LCRC_EINVAL;
+  for (size_t k = 0; opt && k < 3; ++k)
+    if (opt->size >= offsetof(lcrc_ctx_options, reserved) + (k + 1) * sizeof(uint32_t) && opt->reserved[k]) {
+      g_last_error = "lcrc_ctx_options.reserved: must be 0 (the round-5 variants wal_onepass, ts_open_v1 and "
+                     "ts_unfused are no longer in the library)";
+      return LCRC_EINVAL;
+    }
   *out = nullptr;
   int ndev = 0;
   int rc = lcrc_device_count(&ndev);
@@ -420,9 +405,6 @@ int lcrc_ctx_create_ex(lcrc_ctx** out, int device, int mode, uint32_t flags, con
     ctx->wal_grid_b = opt->wal_grid_b;
     if (opt->ts_grid) ctx->ts_grid = opt->ts_grid;
     if (opt->ts_blocks_div) ctx->ts_blocks_div = (int)opt->ts_blocks_div;
-    if (opt->size >= offsetof(lcrc_ctx_options, wal_onepass) + sizeof(uint32_t)) ctx->wal_onepass = opt->wal_onepass != 0;
-    if (opt->size >= offsetof(lcrc_ctx_options, ts_open_v1) + sizeof(uint32_t)) ctx->ts_open_v1 = opt->ts_open_v1 != 0;
-    if (opt->size >= offsetof(lcrc_ctx_options, ts_unfused) + sizeof(uint32_t)) ctx->ts_unfused = opt->ts_unfused != 0;
   }
   *out = ctx;
   return LCRC_OK;
@@ -451,8 +433,6 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
   ctx->wal_offsets.release();
   ctx->wal_descs.release();
   ctx->wal_crcs.release();
-  ctx->wal_rlcnt.release();
-  ctx->wal_rl.release();
   ctx->ms_data.release();
   ctx->ms_desc.release();
   ctx->ms_out.release();
@@ -998,19 +978,6 @@ int lcrc_wal_scan_async(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_len, l
   uint64_t* n_total = ctx->wal_offsets.p;
   uint64_t* local = ctx->wal_offsets.p + 1;
   uint64_t* part = ctx->wal_offsets.p + 1 + nblocks;
-  if (max_recs && ctx->wal_onepass) {
-    // the one-pass form: the window pass finishes the records that lie in one 16 KiB region, k_blocks the others
-    // (wal_offsets' last word: their count)
-    const uint64_t nreg = 2 * nblocks;
-    if ((rc = ctx->wal_rlcnt.ensure(nreg + 1)) || (rc = ctx->wal_rl.ensure(nreg * 8 + 1))) return rc;
-    uint64_t* n_kb = ctx->wal_offsets.p + 1 + nblocks + (nblocks + 63) / 64;
-    HIPCHK(lcrc_launch_wal_onepass(ctx->grid_a, ctx->wal_grid_b ? ctx->wal_grid_b : ctx->grid_b / LCRC_WAL_GRID_DIV,
-                                   file, file_len, nblocks, ctx->wal_counts.p, ctx->wal_slots.p, ctx->wal_stops.p, local,
-                                   part, ctx->wal_rlcnt.p, ctx->wal_rl.p, (lcrc_wal_rec_dev*)recs, ctx->wal_descs.p,
-                                   max_recs, n_total, n_recs, n_kb, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout,
-                                   ctx->poly, ctx->wal_crcs.p, st));
-    return LCRC_OK;
-  }
   // One stream: the header walk (k_wal_parse, one lane per 32 KiB block following the 7-byte headers,
   // then k_wal_emit), the window pass over the whole file, then one k_blocks over all records (the log format stores
   // the raw crc: no mask) that also stores each record's crc and verdict.
@@ -1388,7 +1355,8 @@ static uint64_t ts_verify_cap(size_t max_blocks, uint64_t file_len) {
 
 // the device-only scan's workspace (every buffer its launches touch; nothing else: the host-assisted scan and
 // lcrc_snappy_frames size their own)
-constexpr uint32_t TS_AGG_WORDS = 257;  // k_ts_windows: at most 256 index workgroups, then the arrival count
+constexpr uint32_t TS_AGG_WORDS = 258;  // k_ts_windows: at most 256 index workgroups, then the done count, the ticket
+constexpr uint32_t TS_MAX_IDX = 256;
 
 static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap) {
   int rc = set_device(ctx);
@@ -1402,7 +1370,7 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
       (rc = ctx->sn_nch.ensure(nb)) || (rc = ctx->sn_out_off.ensure(nb)) || (rc = ctx->sn_choff.ensure(nb)) ||
       (rc = ctx->sn_status.ensure(nb)) || (rc = ctx->sn_out.ensure(decoded_cap + 16 * (decoded_cap / 4096 + 1) + 16)) ||
       (rc = ctx->win.ensure(window_words(max_file_len))) || (rc = ctx->ts_idx.ensure(decoded_cap)) ||
-      (!ctx->ts_open_v1 && (rc = ctx->ts_open_scr.ensure(lcrc_ts_open_scratch_words()))))
+      (rc = ctx->ts_open_scr.ensure(lcrc_ts_open_scratch_words())))
     return rc;
   if (!ctx->ts_open.p) {
     if ((rc = ctx->ts_open.ensure(4))) return rc;
@@ -1454,31 +1422,22 @@ int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
   lcrc_tblk_dev* blk = (lcrc_tblk_dev*)blocks;
   const uint64_t cap = max_blocks;
   const uint32_t* tab_c = ctx->mode == LCRC_MODE_C ? ctx->d_tab : ctx->d_tab_c;
-  // Six dependent launches (seven with LCRC_TSCAN_SNAPPY_INDEX: a Snappy-framed index block decoded first). The
+  // Four dependent launches (five with LCRC_TSCAN_SNAPPY_INDEX: a Snappy-framed index block decoded first). The
   // footer, the index block header and the metaindex filter entry (optimistic: checksums come with the batch) with
-  // the index block's restart segments: entry counts, scanned per tile
+  // the index block's restart segments walked in ranges, one per index workgroup
   const bool sidx = flags & LCRC_TSCAN_SNAPPY_INDEX;
   if (sidx)
     HIPCHK(lcrc_launch_ts_open(file, file_len, tab_c, ctx->ts_idx.p, ctx->ts_idx.cap, ctx->ts_open.p,
-                               ctx->ts_open_v1 ? nullptr : ctx->ts_open_scr.p, st));
+                               ctx->ts_open_scr.p, st));
   const uint64_t vcap = ts_verify_cap(cap, file_len);
   const uint64_t* nver = &S->n_verify;
-  const bool fused = cap && ctx->general != 1 && !ctx->ts_unfused;
-  if (fused) {
-    // the file's window pass with the index walk and the handles beside it (k_ts_windows: the window values do not
-    // depend on the handles)
-    HIPCHK(lcrc_launch_ts_windows(ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, &key, cap, vcap, S,
-                                  ctx->idx_count.p, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p,
-                                  sidx ? ctx->ts_open.p : nullptr, ctx->ts_open.p, blk, ctx->tbl_descs.p, ctx->ts_agg.p,
-                                  std::min<uint32_t>(ctx->ts_grid, TS_AGG_WORDS - 1), st));
-  } else {
-    HIPCHK(lcrc_launch_ts_index(file, file_len, &key, cap, S, ctx->idx_count.p, ctx->idx_flag.p, ctx->sn_part.p, cap,
-                                ctx->ts_grid, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p,
-                                sidx ? ctx->ts_open.p : nullptr, st));
-    // the handles and the verify descriptors
-    HIPCHK(lcrc_launch_ts_emit(file, file_len, S, ctx->idx_count.p, ctx->sn_part.p, blk, ctx->tbl_descs.p, cap, vcap,
-                               cap, ctx->ts_grid, ctx->ts_idx.p, ctx->ts_open.p, st));
-  }
+  const bool fused = cap && ctx->general != 1;
+  // the index walk and the handles (k_ts_windows' index workgroups), beside the file's window pass when the batch
+  // goes through it (the window values do not depend on the handles)
+  HIPCHK(lcrc_launch_ts_windows(ctx->grid_a, fused, file, file_len, ctx->d_tab, ctx->win.p, &key, cap, vcap, S,
+                                ctx->idx_count.p, ctx->tbl_mm.p, vcap / 32 + 1, ctx->ts_idx.p,
+                                sidx ? ctx->ts_open.p : nullptr, ctx->ts_open.p, blk, ctx->tbl_descs.p, ctx->ts_agg.p,
+                                std::min<uint32_t>(ctx->ts_grid, TS_MAX_IDX), st));
   // ONE batched verify of every block (data, filter, metaindex, index, and the pieces of long ones)
   if (cap) {
     if (ctx->general == 1) {  // options.general = 1: the one-pass kernel
@@ -1486,10 +1445,7 @@ int lcrc_table_scan_async_ex(lcrc_ctx* ctx, const uint8_t* file, uint64_t file_l
                                 ctx->x4096, ctx->poly, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));
     } else {
-      if (!fused)
-        HIPCHK(lcrc_launch_windows(false, ctx->grid_a, file, file_len, ctx->d_tab, ctx->win.p, 0, 0, 0, nullptr,
-                                   nullptr, st));
-      const int div = ctx->ts_blocks_div ? ctx->ts_blocks_div : fused ? 1 : 2;
+      const int div = ctx->ts_blocks_div ? ctx->ts_blocks_div : 1;
       HIPCHK(lcrc_launch_blocks(false, ctx->grid_b / div, file, file_len, ctx->tbl_descs.p, vcap, 0, 0,
                                 nullptr, ctx->win.p, ctx->d_tab, ctx->init, ctx->xorout, ctx->flags & LCRC_FLAG_MASK,
                                 ctx->tbl_crcs.p, ctx->tbl_mm.p, nver, nullptr, st));

@@ -17,7 +17,8 @@
 //     loads and walk, zero-padded by the buffer range check, the padding undone by one GF(2) multiply.
 //   * Snappy framing: k_snappy_size (framing walk), k_snappy_decode_wave (one wave per frame, LDS-staged,
 //     data-parallel element parse), k_snappy_check; table scan: k_idx_parse, k_tbl_finish, k_tbl_content
-//     (host-walked index), and the device-only scan k_ts_index, k_ts_emit, k_ts_finish, k_ts_decode.
+//     (host-walked index), and the device-only scan k_ts_open2 (a framed index), k_ts_windows (the window
+//     pass with Table::open's index walk beside it), k_ts_finish, k_ts_decode.
 //   * k_wal_parse walks the 7-byte headers of every 32 KiB log block (src/db/log.rs:204-279) into
 //     record descriptors for k_blocks.
 #include <hip/hip_runtime.h>
@@ -792,22 +793,6 @@ __global__ void __launch_bounds__(A_THREADS) k_windows_q(const QJobsArg jobs, co
   windows_body<true, true>(src, gtab, fin, flags, L, &wg_ticket);
 }
 
-// ---------------------------------------------------------------------------------------------------
-// k_windows_wal: the one-pass WAL scan's window pass (lcrc_ctx_options.wal_onepass; log.rs:204-279). It is
-// k_windows<false> -- every 256 B window's raw value to `out`, for the records k_blocks still finishes -- that also
-// finishes the records k_wal_emit1 listed for each region (the ones whose covered bytes lie in the region, up to
-// WAL_RMAX), so that those never go through a second pass over the file:
-//  * a record's partial head and tail windows are re-read right after the refill loads of the same region are
-//    issued (the same lines: L2 hits, no second HBM read) and used one iteration later, after that region's walk:
-//    vector loads retire in issue order, so loads issued at the finish would wait behind the next region's
-//    sixteen refills;
-//  * the re-read window is walked masked -- bytes outside the record's [lo, hi) zeroed, the init register injected
-//    into its first bytes (walk(R, M) = walk(0, M ^ LE(R)) for |M| >= 4) -- by four lanes, 64 B each, joined with
-//    Z64 / Z128 from the replicated S1 set; a window masked at hi is walk(0, M || 0^(256 - hi)) = Z_{256-hi}(...);
-//  * the full windows between head and tail are folded from this wave's own window values (its LDS row) with
-//    Z256, and the trailing zero padding is undone by one GF(2) multiply with x^(-8 pad) (an LDS copy of TAB_INV).
-// The stored CRC comes in the list; the record's crc and verdict go to recs[o], as k_blocks stores them.
-// ---------------------------------------------------------------------------------------------------
 // a * b mod P, reflected (bit 31 = x^0): zlib's multmodp recurrence without branches
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
   uint32_t p = 0;
@@ -817,143 +802,6 @@ __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly
     b = (b >> 1) ^ (poly & (0u - (b & 1u)));
   }
   return p;
-}
-
-constexpr uint32_t WW_WAVES = A_THREADS / 64;
-constexpr uint32_t WAL_RMAX = 8;  // records per region finished by k_windows_wal (two boundary windows each: 16)
-
-// bytes [64 q, 64 q + 64) of the boundary window of lane (w4, q): w4 = slot 2k (record k's head window) or 2k + 1
-// (its tail window, when the record ends in another window); its mask [lo, hi) and whether it holds the start
-struct WalBnd {
-  u32x4 d[4];
-  uint32_t lo, hi;
-  bool on, head;
-};
-
-__device__ __forceinline__ void wal_bnd_load(WalBnd& B, const uint4& sl, uint32_t cnt, __amdgpu_buffer_rsrc_t rs,
-                                             uint32_t lane) {
-  const uint32_t w4 = lane >> 2, q = lane & 3, k = w4 >> 1, tail = w4 & 1;
-  const uint32_t se = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * k), (int)sl.y);
-  const uint32_t s = se & 0xFFFFu, e = se >> 16;
-  const uint32_t ws = s >> 8, we = (e - 1) >> 8;
-  B.on = k < cnt && (!tail || we != ws);
-  B.head = !tail;
-  B.lo = tail ? 0u : s & 255u;
-  B.hi = (tail || ws == we) ? ((e - 1) & 255u) + 1u : 256u;
-  const uint32_t off = 256u * (tail ? we : ws) + 64u * q;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) B.d[i] = B.on ? LCRC_REFILL(rs, off + 16 * i) : u32x4{0, 0, 0, 0};
-}
-
-// walk(0, window bytes [lo, hi) ^ injected init, zero elsewhere) of each boundary window, in lane 4 w4 of its group
-__device__ __forceinline__ uint32_t wal_bnd_walk(const void* L, const Rot& R, const WalBnd& B, uint32_t init,
-                                                 uint32_t lane) {
-  const uint32_t q = lane & 3;
-  const int lo = (int)B.lo - (int)(64 * q), hi = (int)B.hi - (int)(64 * q);  // chunk-relative
-  const uint32_t qn = B.hi - B.lo < 4 ? B.hi - B.lo : 4u;
-  const uint32_t rq = !B.head ? 0u : qn == 4 ? init : init & ((1u << (8 * qn)) - 1u);
-  uint32_t w[16];
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    const int kl = min(max(lo - 4 * d, 0), 4), kh = min(max(hi - 4 * d, 0), 4);
-    const uint32_t keep = (uint32_t)((1ull << (8 * kh)) - (1ull << (8 * kl)));
-    const int D = lo - 4 * d;  // where the record's first byte lies relative to this dword
-    const uint32_t inj = (D > -4 && D < 4) ? (uint32_t)((((uint64_t)rq) << 32) >> (32 - 8 * D)) : 0u;
-    w[d] = (B.d[d >> 2][d & 3] & keep) ^ inj;
-  }
-  uint32_t x = w[0];
-#pragma unroll
-  for (int d = 1; d < 16; ++d) x = step4x(L, R, x, w[d]);
-  x = step4x(L, R, x, 0u);
-  // chunks 0..3 of the window: Z64(c0) ^ c1, Z64(c2) ^ c3, then Z128 = Z64 o Z64
-  const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, false);  // row_shl:1
-  if ((q & 1) == 0) x = zrot<SET_S1>(L, R, x) ^ n1;
-  const uint32_t n2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x102, 0xF, 0xF, false);  // row_shl:2
-  if (q == 0) x = zrot<SET_S1>(L, R, zrot<SET_S1>(L, R, x)) ^ n2;
-  return x;
-}
-
-__global__ void __launch_bounds__(A_THREADS) k_windows_wal(const uint8_t* __restrict__ base, uint64_t span,
-                                                          uint64_t nreg, const uint32_t* __restrict__ gtab,
-                                                          uint32_t* __restrict__ out,
-                                                          const uint32_t* __restrict__ rl_cnt,
-                                                          const uint4* __restrict__ rl,
-                                                          lcrc_wal_rec_dev* __restrict__ recs, uint64_t max_recs,
-                                                          uint32_t init, uint32_t xorout, uint32_t poly) {
-  __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
-  __shared__ uint32_t WV[WW_WAVES * 64];  // each wave's window values of its current region
-  __shared__ uint32_t INV[256];           // x^(-8 k) mod P, k < 256
-  __shared__ uint32_t wg_ticket;
-  WinOne src{base, span, nreg, out, 0, nullptr, nullptr};
-  const uint32_t lane = __lane_id();
-  const uint32_t tid = threadIdx.x;
-  const Share share = make_share(nreg);
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t voff_a = lane_voff<KW_LAY>(lane, 0), voff_b = lane_voff<KW_LAY>(lane, 1);
-  uint64_t t = share.region(wv);
-  // the first region's list, before its data (vector loads retire in issue order)
-  uint4 sl = make_uint4(0, 0, 0, 0);
-  if (t != NO_REGION && lane < WAL_RMAX) sl = rl[t * WAL_RMAX + lane];
-  uint32_t cnt = t != NO_REGION ? rl_cnt[t] : 0u;
-  u32x4 va[8], vb[8];
-  uint32_t ht;
-  const __amdgpu_buffer_rsrc_t rs0 = src.first(t, ht);
-  __builtin_amdgcn_sched_barrier(0);
-  load_half<KW_LAY>(va, rs0, voff_a);
-  __builtin_amdgcn_sched_barrier(0);
-  load_half<KW_LAY>(vb, rs0, voff_b);
-  __builtin_amdgcn_sched_barrier(0);
-  build_tables<true>(L, gtab, wv, lane, nullptr);
-  for (uint32_t i = tid; i < 256; i += A_THREADS) INV[i] = gtab[TAB_INV + i];
-  WalBnd B;
-  wal_bnd_load(B, sl, cnt, rs0, lane);  // the first region's boundary windows (the lines just requested)
-  if (tid == 0) wg_ticket = A_THREADS / 64;
-  lds_barrier();
-  const Rot R = make_rot(lane);
-  uint64_t tn = take_region(&wg_ticket, share, lane);
-  while (t != NO_REGION) {
-    const __amdgpu_buffer_rsrc_t rsn = src.rsrc(tn, 0);
-    // the next region's list, before its refills
-    uint4 sln = make_uint4(0, 0, 0, 0);
-    if (tn != NO_REGION && lane < WAL_RMAX) sln = rl[tn * WAL_RMAX + lane];
-    const uint32_t cntn = tn != NO_REGION ? rl_cnt[tn] : 0u;
-    __builtin_amdgcn_sched_barrier(0);
-    const uint32_t x = walk_half<true, KW_LAY, false>(L, R, va, 0u, rsn, voff_a);
-    __builtin_amdgcn_sched_barrier(0);
-    const uint64_t tnn = take_region(&wg_ticket, share, lane);
-    const uint32_t p = walk_half<true, KW_LAY>(L, R, vb, x, rsn, voff_b);
-    const uint32_t wl = window_of_lane<KW_LAY>(lane);
-    out[t * 64 + wl] = p;
-    WV[wv * 64 + wl] = p;
-    // region t's listed records
-    const uint32_t m = wal_bnd_walk(L, R, B, init, lane);
-    const uint32_t mh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(32 * lane), (int)m);       // lane 8 k: head
-    const uint32_t mt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(32 * lane + 16), (int)m);  // lane 8 k + 4: tail
-    if (__builtin_amdgcn_ballot_w64(lane < cnt)) {
-      const uint32_t s = sl.y & 0xFFFFu, e = sl.y >> 16;
-      const uint32_t ws = s >> 8, we = (e - 1) >> 8;
-      const uint32_t nfull = we > ws ? we - ws - 1 : 0u;
-      uint32_t acc = mh;
-      for (uint32_t i = 0; __builtin_amdgcn_ballot_w64(lane < cnt && i < nfull); ++i)
-        if (i < nfull) acc = zlook(L, A_ZT, acc) ^ WV[wv * 64 + ws + 1 + i];
-      if (we != ws) acc = zlook(L, A_ZT, acc) ^ mt;
-      const uint32_t pad = 255u - ((e - 1) & 255u);
-      if (__builtin_amdgcn_ballot_w64(lane < cnt && pad != 0)) acc = pad ? gf_mul(INV[pad], acc, poly) : acc;
-      const uint32_t len = e - s;
-      if (len < 4) acc ^= init >> (8 * len);
-      const uint32_t crc = acc ^ xorout;
-      if (lane < cnt && sl.x < max_recs) {
-        recs[sl.x].crc = crc;
-        recs[sl.x].status = crc != sl.z ? 1 : 0;
-      }
-    }
-    // the next region's boundary windows: the lines its refills just requested
-    sl = sln;
-    cnt = cntn;
-    wal_bnd_load(B, sl, cnt, rsn, lane);
-    t = tn;
-    tn = tnn;
-  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1713,37 +1561,17 @@ __device__ __forceinline__ uint32_t wal_single(uint64_t b, uint32_t at, uint32_t
   return (s >> 8) == ((s + length) >> 8) ? 1u : 0u;  // last covered byte s + length
 }
 
-// The one-pass WAL scan (lcrc_ctx_options.wal_onepass): a record whose covered bytes lie in one 16 KiB region of the
-// file (one half of its 32 KiB log block) is finished by the window pass itself (k_windows_wal), up to WAL_RMAX per
-// region in file order; the others -- records across the middle of their log block, and a region's records past
-// WAL_RMAX -- go to k_blocks. wal_route decides it identically in the parse (counts) and the emit (slots).
-// Two more exclusions, both cases k_windows_wal cannot walk from its boundary windows: a record whose last bytes lie in
-// the file's last partial dword (the buffer range check returns a dword only when it lies wholly inside the file), and
-// a multi-window record with fewer than 4 bytes in its head window (the init register is injected into its first 4).
-__device__ __forceinline__ bool wal_route(uint32_t at, uint32_t length, uint64_t b, uint64_t file_len, uint32_t& n0,
-                                          uint32_t& n1, uint32_t& half) {
-  const uint32_t s = at + 6, e = at + 7 + length;  // covered bytes [s, e), block-relative
-  half = s >= 16384 ? 1u : 0u;
-  const bool single = (s >> 8) == ((e - 1) >> 8);
-  if (b * 32768ull + e > (file_len & ~3ull) || (!single && (s & 255) > 252)) return false;
-  if (e <= 16384 && n0 < WAL_RMAX) return ++n0, true;
-  if (s >= 16384 && n1 < WAL_RMAX) return ++n1, true;
-  return false;
-}
-
-template <bool ONEPASS>
 __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file, uint64_t file_len,
                                                uint64_t nblocks, uint32_t* __restrict__ counts,
                                                uint2* __restrict__ slots, uint8_t* __restrict__ stops,
                                                uint64_t* __restrict__ local, uint64_t* __restrict__ part,
-                                               uint32_t bx, uint32_t* __restrict__ rl_cnt = nullptr) {
+                                               uint32_t bx) {
   const uint64_t b = (uint64_t)bx * 64 + threadIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint8_t* blk = file + b * 32768ull;
   const uint64_t rem = b < nblocks ? file_len - b * 32768ull : 0;
   const uint32_t cap = rem < 32768ull ? (uint32_t)rem : 32768u;
   uint32_t consumed = 0, nrec = 0, nsingle = 0, stop = LCRC_WAL_STOP_TRAILER_DEV;
-  uint32_t n0 = 0, n1 = 0;  // (ONEPASS) records finished by the window pass in each half of the block
   while (cap - consumed >= 7) {
     uint32_t length, type;
     // bytes 4..7 at the header inside the block: ONE dword load per hop (the length and type bytes), instead of
@@ -1765,24 +1593,12 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
       stop = LCRC_WAL_STOP_ZERO_DEV;
       break;
     }
-    uint32_t one, tag;
-    if constexpr (ONEPASS) {  // the high count: records for k_blocks; slot bits: 8 window pass, 9 half
-      uint32_t half;
-      const bool wp = wal_route(consumed, length, b, file_len, n0, n1, half);
-      one = wp ? 0u : 1u;
-      tag = (wp ? 1u << 8 : 0u) | (half << 9);
-    } else {  // the high count: one-window records
-      one = wal_single(b, consumed, length);
-      tag = one << 8;
-    }
+    const uint32_t one = wal_single(b, consumed, length);  // the high count: one-window records
+    const uint32_t tag = one << 8;
     if (nrec < WAL_SLOTS) slots[b * WAL_SLOTS + nrec] = make_uint2(consumed | (length << 16), type | tag);
     ++nrec;
     nsingle += one;
     consumed += 7 + length;
-  }
-  if (ONEPASS && b < nblocks) {
-    rl_cnt[2 * b] = n0;
-    rl_cnt[2 * b + 1] = n1;
   }
   // wave exclusive scan by shuffles of (records | one-window records << 32)
   const uint64_t mine = (uint64_t)nrec | ((uint64_t)nsingle << 32);
@@ -1800,13 +1616,11 @@ __device__ __forceinline__ void wal_parse_body(const uint8_t* __restrict__ file,
   if (lane == 63) part[bx] = inc;
 }
 
-template <bool ONEPASS>
 __global__ void __launch_bounds__(64) k_wal_parse(const uint8_t* __restrict__ file, uint64_t file_len,
                                                   uint64_t nblocks, uint32_t* __restrict__ counts,
                                                   uint2* __restrict__ slots, uint8_t* __restrict__ stops,
-                                                  uint64_t* __restrict__ local, uint64_t* __restrict__ part,
-                                                  uint32_t* __restrict__ rl_cnt) {
-  wal_parse_body<ONEPASS>(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x, rl_cnt);
+                                                  uint64_t* __restrict__ local, uint64_t* __restrict__ part) {
+  wal_parse_body(file, file_len, nblocks, counts, slots, stops, local, part, blockIdx.x);
 }
 
 // several logs in one launch (lcrc_wal_scan_queue): log blockIdx.y, its parse workgroups blockIdx.x
@@ -1832,7 +1646,7 @@ struct WalJobsArg {
 __global__ void __launch_bounds__(64) k_wal_parse_q(const WalJobsArg jobs) {
   const WalJobDev& J = jobs.j[blockIdx.y];
   if ((uint64_t)blockIdx.x * WAL_PARTB >= J.nblocks) return;  // past this log's blocks (workgroup-uniform)
-  wal_parse_body<false>(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
+  wal_parse_body(J.file, J.file_len, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, blockIdx.x);
 }
 
 // record o (file order) and its verify descriptor at position pos of k_blocks' order. The descriptor's
@@ -1867,16 +1681,6 @@ __device__ __forceinline__ void wal_put(lcrc_wal_rec_dev* __restrict__ recs, lcr
 // by each emit workgroup) + local[b]. Descriptors: the one-window records first, then the others, each in file
 // order (both only when every record fits max_recs; else in file order). Workgroup 0 also writes the total
 // record count to n_total (device) and n_out (device or pinned host memory).
-// (ONEPASS) a record the window pass finishes: its slot in its region's list -- {record index, covered bytes
-// [s, e) relative to the region as s | e << 16, the stored CRC (header bytes 0..3)}
-__device__ __forceinline__ void wal_region_slot(const uint8_t* __restrict__ blk, uint4* __restrict__ rl, uint64_t b,
-                                                uint32_t half, uint32_t rank, uint64_t o, uint32_t at,
-                                                uint32_t length) {
-  const uint32_t s = at + 6 - 16384 * half, e = at + 7 + length - 16384 * half;
-  rl[(2 * b + half) * WAL_RMAX + rank] = make_uint4((uint32_t)o, s | (e << 16), load_le32(blk + at), 0u);
-}
-
-template <bool ONEPASS>
 __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, uint64_t nblocks,
                                               const uint32_t* __restrict__ counts,
                                               const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
@@ -1885,8 +1689,7 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
                                               lcrc_wal_rec_dev* __restrict__ recs,
                                               lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
                                               uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
-                                              uint32_t bx, uint4* __restrict__ rl = nullptr,
-                                              uint64_t* __restrict__ n_kb = nullptr, uint64_t file_len = 0) {
+                                              uint32_t bx) {
   const uint64_t g = (uint64_t)bx * blockDim.x + threadIdx.x;
   const uint64_t b = g / WAL_SLOTS;
   const uint32_t i = (uint32_t)(g % WAL_SLOTS);
@@ -1910,53 +1713,8 @@ __device__ __forceinline__ void wal_emit_body(const uint8_t* __restrict__ file, 
   if (bx == 0 && threadIdx.x == 0) {
     *n_total = tot_r;
     if (n_out) *n_out = tot_r;
-    if (ONEPASS) *n_kb = tot_s < max_recs ? tot_s : max_recs;  // the records k_blocks finishes
   }
   if (b >= nblocks || max_recs == 0) return;  // wave-uniform
-  if constexpr (ONEPASS) {
-    // file order as below; the window pass's records to their region's list, the others' descriptors packed in
-    // file order for k_blocks (the high counts are theirs)
-    const uint32_t cnt = counts[b];
-    const uint64_t loc = local[b];
-    const uint64_t first = (uint32_t)before + (uint32_t)loc;
-    const uint64_t first_kb = (before >> 32) + (loc >> 32);
-    uint2 sl = make_uint2(0, 0);
-    if (i < cnt) sl = slots[g];
-    const bool wp = (sl.y >> 8) & 1u;
-    const uint32_t hf = (sl.y >> 9) & 1u;
-    const uint64_t lt = (1ull << i) - 1;
-    const uint64_t kbm = __builtin_amdgcn_ballot_w64(i < cnt && !wp);
-    const uint64_t h0m = __builtin_amdgcn_ballot_w64(i < cnt && wp && hf == 0);
-    const uint64_t h1m = __builtin_amdgcn_ballot_w64(i < cnt && wp && hf == 1);
-    if (i >= cnt) return;
-    const uint8_t* blk = file + b * 32768ull;
-    uint32_t at = sl.x & 0xFFFFu, length = sl.x >> 16;
-    const uint64_t o = first + i;
-    if (wp) {
-      wal_region_slot(blk, rl, b, hf, __builtin_popcountll((hf ? h1m : h0m) & lt), o, at, length);
-      wal_put(recs, descs, o, ~0ull, max_recs, b * 32768ull + at, length, sl.y & 0xFFu, i + 1 == cnt, stops[b]);
-    } else {
-      wal_put(recs, descs, o, o < max_recs ? first_kb + __builtin_popcountll(kbm & lt) : ~0ull, max_recs,
-              b * 32768ull + at, length, sl.y & 0xFFu, i + 1 == cnt, stops[b]);
-    }
-    if (i == WAL_SLOTS - 1 && cnt > WAL_SLOTS) {  // the rest of a block with more records than slots, in order
-      uint32_t n0 = __builtin_popcountll(h0m), n1 = __builtin_popcountll(h1m);
-      uint64_t nk = __builtin_popcountll(kbm);
-      for (uint32_t j = WAL_SLOTS; j < cnt; ++j) {
-        at += 7 + length;
-        uint32_t type, half;
-        wal_header(blk, at, length, type);
-        const uint32_t r0 = n0, r1 = n1;
-        const bool wpj = wal_route(at, length, b, file_len, n0, n1, half);
-        const uint64_t oj = first + j;
-        if (wpj) wal_region_slot(blk, rl, b, half, half ? r1 : r0, oj, at, length);
-        wal_put(recs, descs, oj, wpj || oj >= max_recs ? ~0ull : first_kb + nk, max_recs, b * 32768ull + at, length,
-                type, j + 1 == cnt, stops[b]);
-        nk += wpj ? 0 : 1;
-      }
-    }
-    return;
-  }
   const bool split = tot_r <= max_recs;
   const uint32_t cnt = counts[b];
   const uint64_t loc = local[b];
@@ -1998,29 +1756,15 @@ __global__ void __launch_bounds__(256) k_wal_emit(const uint8_t* __restrict__ fi
                                                   lcrc_wal_rec_dev* __restrict__ recs,
                                                   lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
                                                   uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out) {
-  wal_emit_body<false>(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out,
+  wal_emit_body(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out,
                        blockIdx.x);
-}
-
-// the one-pass scan's emit: region lists for the window pass, packed k_blocks descriptors, their count in n_kb
-__global__ void __launch_bounds__(256) k_wal_emit1(const uint8_t* __restrict__ file, uint64_t file_len, uint64_t nblocks,
-                                                   const uint32_t* __restrict__ counts,
-                                                   const uint2* __restrict__ slots, const uint8_t* __restrict__ stops,
-                                                   const uint64_t* __restrict__ local,
-                                                   const uint64_t* __restrict__ part,
-                                                   lcrc_wal_rec_dev* __restrict__ recs,
-                                                   lcrc_desc_dev* __restrict__ descs, uint64_t max_recs,
-                                                   uint64_t* __restrict__ n_total, uint64_t* __restrict__ n_out,
-                                                   uint4* __restrict__ rl, uint64_t* __restrict__ n_kb) {
-  wal_emit_body<true>(file, nblocks, counts, slots, stops, local, part, recs, descs, max_recs, n_total, n_out,
-                      blockIdx.x, rl, n_kb, file_len);
 }
 
 __global__ void __launch_bounds__(256) k_wal_emit_q(const WalJobsArg jobs) {
   const WalJobDev& J = jobs.j[blockIdx.y];
   // past this log's (block, slot) threads: workgroup 0 always runs (it writes the total)
   if (blockIdx.x && (uint64_t)blockIdx.x * 256 >= J.nblocks * WAL_SLOTS) return;
-  wal_emit_body<false>(J.file, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, J.recs, J.descs, J.max_recs,
+  wal_emit_body(J.file, J.nblocks, J.counts, J.slots, J.stops, J.local, J.part, J.recs, J.descs, J.max_recs,
                        J.n_total, J.n_out, blockIdx.x);
 }
 
@@ -2087,7 +1831,7 @@ static_assert(TR_OUT % 1024 == 0 && TR_ROW % 16 == 0 && TR_IN + 16 <= TR_ROW, "r
 static_assert(TD_WAVES % 2 == 0 && TD_IN + SN_SLACK + TD_OUT <= 2 * TD_WAVE_LDS,
               "the whole-wave decoder's staging is two waves' row areas");
 constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
-static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish and k_ts_index");
+static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish");
 
 // `slow`: the decoded bytes (16-aligned) of the compressed chunks too large for k_ts_decode's LDS staging (TD_IN
 // compressed, TD_OUT decoded), which it decodes lane-serially into the table scan's workspace
@@ -2688,7 +2432,8 @@ __device__ __forceinline__ uint32_t dev_varint(const uint8_t* __restrict__ d, ui
 template <bool PASS2>
 __device__ __forceinline__ uint64_t idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
                                                 uint64_t file_len, uint64_t o0, lcrc_tblk_dev* __restrict__ out,
-                                                lcrc_desc_dev* __restrict__ descs, uint64_t i, bool& bad);
+                                                lcrc_desc_dev* __restrict__ descs, uint64_t i, bool& bad,
+                                                uint64_t ocap = ~0ull);
 
 template <bool PASS2>
 __global__ void __launch_bounds__(256) k_idx_parse(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
@@ -2705,11 +2450,13 @@ __global__ void __launch_bounds__(256) k_idx_parse(const uint8_t* __restrict__ d
   }
 }
 
-// PASS 1: returns the entries of segment i (bad: the host must walk it). PASS 2: writes them from slot o0 on.
+// PASS 1: returns the entries of segment i (bad: the host must walk it). PASS 2: writes them from slot o0 on (the
+// slots below ocap).
 template <bool PASS2>
 __device__ __forceinline__ uint64_t idx_segment(const uint8_t* __restrict__ d, uint32_t len, uint32_t nres,
                                                 uint64_t file_len, uint64_t o0, lcrc_tblk_dev* __restrict__ out,
-                                                lcrc_desc_dev* __restrict__ descs, uint64_t i, bool& bad) {
+                                                lcrc_desc_dev* __restrict__ descs, uint64_t i, bool& bad,
+                                                uint64_t ocap) {
   const uint32_t restarts = len - (1 + nres) * 4;
   auto rst = [&](uint32_t k) { return load_le32(d + restarts + 4 * k); };
   const uint32_t start = rst((uint32_t)i);
@@ -2758,8 +2505,10 @@ __device__ __forceinline__ uint64_t idx_segment(const uint8_t* __restrict__ d, u
         b.status = 2;  // LCRC_TBLK_TRUNCATED
         b.type = 0xFF;
       }
-      out[o] = b;
-      descs[o] = dd;
+      if (o < ocap) {  // (k_ts_windows: slots past the result capacity are never written)
+        out[o] = b;
+        descs[o] = dd;
+      }
     }
     ++n;
     off = (uint32_t)(p + non_shared + vlen);
@@ -2823,7 +2572,7 @@ enum { TS_OK = 0, TS_CORRUPT = 1, TS_HOST = 2, TS_CAPACITY = 3 };
 enum { TSM_SHORT = 1, TSM_MAGIC = 2, TSM_VARINT = 3, TSM_CHECKSUM = 4, TSM_TYPE = 5, TSM_SMALL = 6, TSM_CONTENTS = 7 };
 
 // footer, index block header and (meta) the metaindex filter entry, by one thread; key: 256 B of LDS
-// idec / iopen: k_ts_open's decoded index and its verdict (nullptr when the scan has no LCRC_TSCAN_SNAPPY_INDEX)
+// idec / iopen: k_ts_open2's decoded index and its verdict (nullptr when the scan has no LCRC_TSCAN_SNAPPY_INDEX)
 // pre (k_ts_windows, nullable): every value this walk loads, loaded beforehand by the workgroup in parallel rounds
 // (a chain of dependent loads costs ~5 us a link under the window stream), each under the condition its use here has
 struct TsPre {
@@ -2866,7 +2615,7 @@ __device__ __forceinline__ void ts_open_state(const uint8_t* __restrict__ file, 
   const uint8_t* ic = file + s.idx_off;  // the index block's contents
   uint64_t clen = s.idx_size;
   if (itype == 1) {
-    // a Snappy-framed index block: its contents are what k_ts_open decoded, when it decoded them all; otherwise the
+    // a Snappy-framed index block: its contents are what k_ts_open2 decoded, when it decoded them all; otherwise the
     // host path decodes it (and gives the reference's message) -- after the workspace grows, when that was the reason
     const uint64_t o0 = iopen ? (pre ? pre->io[0] : iopen[0]) : 0;
     const uint64_t o1 = o0 ? (pre ? pre->io[1] : iopen[1]) : 0, o2 = o0 ? (pre ? pre->io[2] : iopen[2]) : 0;
@@ -2989,82 +2738,11 @@ __device__ __forceinline__ void wg_scan2(uint64_t va, uint64_t vb, uint64_t* sa,
   eb = pb + ib - vb;
 }
 
-// sums of part[2 w] and part[2 w + 1] over w in [lo, hi), by a 256-thread workgroup (every thread gets them)
-__device__ __forceinline__ void wg_sum_parts(const uint64_t* __restrict__ part, uint64_t lo, uint64_t hi, uint64_t* sa,
-                                             uint64_t* sb, uint64_t& ra, uint64_t& rb) {
-  unsigned long long xa = 0, xb = 0;
-  for (uint64_t w = lo + threadIdx.x; w < hi; w += 256) {
-    xa += part[2 * w];
-    xb += part[2 * w + 1];
-  }
-  for (int d = 1; d < 64; d <<= 1) {
-    xa += __shfl_xor(xa, d, 64);
-    xb += __shfl_xor(xb, d, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    sa[threadIdx.x >> 6] = xa;
-    sb[threadIdx.x >> 6] = xb;
-  }
-  __syncthreads();
-  ra = sa[0] + sa[1] + sa[2] + sa[3];
-  rb = sb[0] + sb[1] + sb[2] + sb[3];
-  __syncthreads();
-}
-
-// The table scan's first launch: the footer and the index block header (thread 0 of every workgroup, so that
-// no launch waits on them; workgroup 0 also walks the metaindex and records the state), then pass 1 over the
-// restart segments in 256-segment tiles: entry counts and fallback flags, scanned within the tile (local[i]),
-// the tile totals in part[2 t], part[2 t + 1]. k_ts_emit adds the totals of the tiles before.
-__global__ void __launch_bounds__(256) k_ts_index(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                  const lcrc_tscan_key fkey, uint64_t seg_cap,
-                                                  lcrc_tscan_dev* __restrict__ st, uint64_t* __restrict__ local_c,
-                                                  uint64_t* __restrict__ local_f, uint64_t* __restrict__ part,
-                                                  uint32_t* __restrict__ zero, uint64_t nzero,
-                                                  const uint8_t* __restrict__ idec, const uint64_t* __restrict__ iopen) {
-  __shared__ uint8_t key[256];
-  __shared__ uint64_t hdr[3], sa[4], sb[4];
-  // the batch's mismatch bitmap starts at zero (no memset launch)
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (uint64_t)gridDim.x * blockDim.x)
-    zero[i] = 0;
-  if (threadIdx.x == 0) {
-    lcrc_tscan_dev s;
-    ts_open_state(file, file_len, fkey, seg_cap, key, blockIdx.x == 0, idec, iopen, s);
-    if (blockIdx.x == 0) *st = s;
-    hdr[0] = s.nres;  // 0 unless the index block can be walked (a later metaindex verdict changes nothing here)
-    hdr[1] = s.idx_dec ? ~0ull : s.idx_off;
-    hdr[2] = s.idx_clen;
-  }
-  __syncthreads();
-  const uint64_t nres = hdr[0];
-  const uint8_t* d = hdr[1] == ~0ull ? idec : file + hdr[1];
-  const uint32_t len = (uint32_t)hdr[2];
-  for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
-    const uint64_t i = t0 + threadIdx.x;
-    uint64_t c = 0, f = 0;
-    if (i < nres) {
-      bool bad;
-      const uint64_t n = idx_segment<false>(d, len, (uint32_t)nres, file_len, 0, nullptr, nullptr, i, bad);
-      c = bad ? 0 : n;
-      f = bad ? 1 : 0;
-    }
-    uint64_t ec, ef, tc, tf;
-    wg_scan2(c, f, sa, sb, ec, ef, tc, tf);
-    if (i < nres) {
-      local_c[i] = ec;
-      local_f[i] = ef;
-    }
-    if (threadIdx.x == 0) {
-      part[2 * (t0 / 256)] = tc;
-      part[2 * (t0 / 256) + 1] = tf;
-    }
-  }
-}
-
 // After pass 1, from the totals (nd: the data blocks the index names, nflag: segments the device walk cannot vouch
 // for): the capacity check and the fallback flags (decided alike by every workgroup; `lead` records them), then
 // pass 2 writes the handles (seg(d, len, nres): this workgroup's segments at their slots) and, in workgroup 0
 // (wg0), threads 0..2 append the filter, metaindex and index blocks with their descriptors. s: the state
-// ts_open_state left (k_ts_emit: from st; k_ts_windows: the workgroup's own).
+// ts_open_state left (the last index ticket's own).
 template <class Seg>
 __device__ void ts_emit_body(const lcrc_tscan_dev& s, lcrc_tscan_dev* __restrict__ st, bool lead, bool wg0,
                              uint64_t nd, uint64_t nflag, const uint8_t* __restrict__ file, uint64_t file_len,
@@ -3173,45 +2851,26 @@ __device__ void ts_emit_body(const lcrc_tscan_dev& s, lcrc_tscan_dev* __restrict
   }
 }
 
-// after k_ts_index: the totals of its tiles, then ts_emit_body with the tiles dealt over the workgroups (slot = the
-// tiles before + the segment's place in its tile)
-__global__ void __launch_bounds__(256) k_ts_emit(const uint8_t* __restrict__ file, uint64_t file_len,
-                                                 lcrc_tscan_dev* __restrict__ st, const uint64_t* __restrict__ local_c,
-                                                 const uint64_t* __restrict__ part, lcrc_tblk_dev* __restrict__ out,
-                                                 lcrc_desc_dev* __restrict__ descs, uint64_t cap, uint64_t vcap,
-                                                 const uint8_t* __restrict__ idec, uint64_t* __restrict__ iopen) {
-  __shared__ uint64_t sa[4], sb[4];
-  const lcrc_tscan_dev s = *st;  // as k_ts_index left it (the fields read below are not written here)
-  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-  if (lead) iopen[2] = 0;  // k_ts_open's failure mark, read by k_ts_index: clear for the next scan
-  uint64_t nd = 0, nflag = 0;
-  if (s.status == TS_OK) wg_sum_parts(part, 0, (s.nres + 255) / 256, sa, sb, nd, nflag);
-  ts_emit_body(s, st, lead, blockIdx.x == 0, nd, nflag, file, file_len, out, descs, cap, vcap, idec,
-               [&](const uint8_t* d, uint32_t len, uint64_t nres) {
-                 for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < nres; t0 += (uint64_t)gridDim.x * 256) {
-                   uint64_t base, bf;
-                   wg_sum_parts(part, 0, t0 / 256, sa, sb, base, bf);
-                   const uint64_t i = t0 + threadIdx.x;
-                   bool bad;
-                   if (i < nres)
-                     idx_segment<true>(d, len, (uint32_t)nres, file_len, base + local_c[i], out, descs, i, bad);
-                 }
-               });
-}
-
-// The table scan's first launch when the batch goes through the window pass (lcrc_table_scan_async_ex): the file's
-// window pass (k_windows<false>: its values do not depend on the index) in workgroups [0, nwg), and k_ts_index +
-// k_ts_emit in the nidx workgroups after them, which run beside the window stream instead of before it (two
-// dependent launches less). Index workgroup j walks a contiguous range of the restart segments; the ranges' entry
-// counts meet through agg[j] (a ready bit, a fallback bit, the count), published once and read by every index
-// workgroup (all of them are resident: they follow the window workgroups in dispatch order and wait on nothing
-// but each other, and nidx <= the CUs); the last one to have read them zeroes agg and the arrival count for the
-// next scan. Each index workgroup computes the footer state itself (the metaindex walk included), so that none
-// reads another's. The totals travel inside the atomic words themselves, so the atomics are relaxed: an
-// acquire/release at agent scope would write back / invalidate the XCD's L2 on every poll, under the window stream.
-// (The reset cannot overtake a reader: each workgroup's arrival depends on the values it loaded.)
+// The table scan's first launch (lcrc_table_scan_async_ex): the file's window pass (k_windows<false>: its values do
+// not depend on the index) in workgroups [0, nwg), and Table::open's index walk with the handles in the nidx
+// workgroups after them, which run beside the window stream instead of before it (nwg = 0: the index walk alone).
+// Progress without co-residency (several scans may share the chip, one per stream): an index workgroup first takes a
+// TICKET j from agg[TSA_TICKET_AT] and walks the j-th contiguous range of the restart segments; the ranges' entry
+// counts meet through agg[j] (a ready bit, a fallback bit, the count), which ticket j publishes before it waits on
+// anything. Ticket j then waits only on the words of tickets below j (decoupled look-back, without the shortcut:
+// at most 256 words, one polling thread each). A lower ticket was taken by a workgroup that has started, so it is
+// resident or done, and it publishes without waiting: every wait ends whatever else occupies the CUs. Each ticket
+// writes its handles at its offset (slots bounded by the capacity, since only the last ticket knows the total) and
+// counts itself in agg[TSA_DONE_AT]; the last ticket (nidx - 1) waits for that count -- its lower tickets again --,
+// then alone writes the state, the filter / metaindex / index entries after the data blocks, and when a range is
+// bad the index block's entry at slot 0 (the one slot another range may have written: that range releases its
+// stores before counting itself, the last ticket acquires), and zeroes the words for the next scan. Each index
+// workgroup computes the footer state itself (the metaindex walk included), so that none reads another's. The
+// totals travel inside the atomic words themselves, so the polls are relaxed: an acquire/release at agent scope
+// writes back / invalidates the XCD's L2, under the window stream, and is paid once, by the two workgroups above.
 constexpr uint64_t TSA_READY = 1ull << 63, TSA_BAD = 1ull << 62, TSA_COUNT = (1ull << 62) - 1;
-static_assert(A_THREADS >= 256, "a thread per index workgroup's total (at most 256)");
+constexpr uint32_t TSA_MAX = 256, TSA_DONE_AT = TSA_MAX, TSA_TICKET_AT = TSA_MAX + 1;  // agg: 258 words
+static_assert(A_THREADS >= TSA_MAX, "a thread per lower ticket's word");
 struct TsIdxArgs {
   const uint8_t* file;
   uint64_t file_len;
@@ -3220,7 +2879,7 @@ struct TsIdxArgs {
   uint64_t* local_c;
   uint32_t* zero;  // the batch's mismatch bitmap (nzero words)
   const uint8_t* idec;
-  const uint64_t* iopen_r;  // k_ts_open's verdict (nullptr: no Snappy-framed index)
+  const uint64_t* iopen_r;  // k_ts_open2's verdict (nullptr: no Snappy-framed index)
   uint64_t* iopen;          // its failure mark is cleared once every workgroup has read it
   lcrc_tblk_dev* out;
   lcrc_desc_dev* descs;
@@ -3266,7 +2925,7 @@ __device__ __forceinline__ void wg_copy_bytes(uint8_t* dst1, const uint8_t* __re
 #define TSI_STAMP(k)
 #endif
 // Index workgroup j of k_ts_windows. Under the window stream a load takes ~5 us, so every value the walk needs is
-// loaded in four parallel rounds instead of chains: (1) the footer and k_ts_open's verdict words; (2) the metaindex
+// loaded in four parallel rounds instead of chains: (1) the footer and k_ts_open2's verdict words; (2) the metaindex
 // block, the index block's type byte and its restart count (raw and decoded: the type picks); (3) the workgroup's
 // slice of the restart array; (4) the bytes of its segments. Its restart segments [lo, hi) are then a block of their
 // own in LDS (stage): the bytes [s0, E) -- s0 = the first segment's start (0 in workgroup 0, so that segment 0 must
@@ -3275,8 +2934,12 @@ __device__ __forceinline__ void wg_copy_bytes(uint8_t* dst1, const uint8_t* __re
 // exact once the offsets are non-decreasing, within the restart array and rst(0) = 0; a violation is a segment the
 // whole-block walk finds bad too (start > end, or end past the restarts), so it only raises the fallback bit. A
 // range too long for the LDS is walked in place.
-__device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint32_t j, uint32_t nidx,
-                            uint32_t* L) {
+__device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint32_t nidx, uint32_t* L,
+                            uint32_t* ticket) {
+  if (threadIdx.x == 0)
+    *ticket = __hip_atomic_fetch_add((uint32_t*)(a.agg + TSA_TICKET_AT), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t j = *ticket;  // this workgroup's range (the order in which the index workgroups started)
   TSI_STAMP(0);
 #ifndef LCRC_TSI_PRIO
 #define LCRC_TSI_PRIO 3
@@ -3421,51 +3084,67 @@ __device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint
   else
     pass1(d, len, nres, 0, false);
   TSI_STAMP(4);
+  // publish this range's count (never waiting on anything first), then look back at the ranges BEFORE it only: one
+  // thread per lower ticket polls that ticket's word (one load round trip per poll, all in flight together)
   if (tid == 0)
     __hip_atomic_store(a.agg + j, TSA_READY | (nbad ? TSA_BAD : 0) | run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // every workgroup's word polled by a thread of its own (one load round trip per poll, all in flight together),
-  // then summed over the workgroup
   uint64_t v = 0;
-  if (tid < nidx) {
+  if (tid < j) {
     do {
       v = __hip_atomic_load(a.agg + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } while (!(v & TSA_READY));
   }
   const uint64_t cnt = v & TSA_COUNT;
-  uint64_t e1, e2, total, before;
-  wg_scan2<NWAVE>(cnt, tid < j ? cnt : 0, sa, sb, e1, e2, total, before);
-  const int anyb = __syncthreads_or((v & TSA_BAD) != 0);
-  if (tid == 0) {
-    tot[0] = before;
-    tot[1] = total;
-    tot[2] = anyb ? 1 : 0;
-    // every workgroup has published and read the totals once all nidx arrived here: the last one resets them
-    uint32_t* arrived = (uint32_t*)(a.agg + nidx);
-    if (__hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nidx - 1) {
-      for (uint32_t k = 0; k < nidx; ++k) __hip_atomic_store(a.agg + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(arrived, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t e1, e2, before, unused;
+  wg_scan2<NWAVE>(cnt, 0, sa, sb, e1, e2, before, unused);
+  const bool badb = __syncthreads_or((v & TSA_BAD) != 0) != 0;  // a range before this one the walk cannot vouch for
+  TSI_STAMP(5);
+  // this range's handles at their slots, unless a range up to this one is bad (the scan is then the index block's
+  // checksum alone). Whether the whole index fits the result is known to the last ticket only: every slot is bounded
+  // by the capacity instead, and the last ticket reports TS_CAPACITY (nothing the caller reads) when it does not fit
+  const bool write = s.status == TS_OK && nres && !badb && !nbad;
+  if (write) {
+    bool bad;
+    if (staged) {
+      for (uint64_t i = lo + tid; i < hi; i += NT)
+        idx_segment<true>(stage + voff, (uint32_t)(bytes + 4 * (m + 1)), (uint32_t)m, file_len, before + loc[i - lo],
+                          a.out, a.descs, i - lo, bad, a.cap);
+    } else {
+      for (uint64_t i = lo + tid; i < hi; i += NT)
+        idx_segment<true>(d, len, (uint32_t)nres, file_len, before + a.local_c[i], a.out, a.descs, i, bad, a.cap);
     }
   }
   __syncthreads();
-  TSI_STAMP(5);
-  const uint64_t base = tot[0], nd = tot[1], nflag = tot[2];
-  const bool lead = j == 0 && tid == 0;
-  if (lead) {
-    *a.st = s;
-    a.iopen[2] = 0;  // k_ts_open's failure mark (every workgroup read it before publishing): clear for the next scan
+  uint32_t* const done = (uint32_t*)(a.agg + TSA_DONE_AT);
+  const bool last = j == nidx - 1;
+  if (!last) {
+    if (tid == 0) {
+      // slot 0 is the one the last ticket may overwrite (the index block alone): a range that wrote it makes its
+      // stores visible across the XCDs' L2s before it counts itself done
+      if (write && before == 0 && run) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    TSI_STAMP(6);
+    return;
   }
-  ts_emit_body(s, a.st, lead, j == 0, nd, nflag, a.file, a.file_len, a.out, a.descs, a.cap, a.vcap, a.idec,
-               [&](const uint8_t*, uint32_t, uint64_t) {
-                 bool bad;
-                 if (staged) {
-                   for (uint64_t i = lo + tid; i < hi; i += NT)
-                     idx_segment<true>(stage + voff, (uint32_t)(bytes + 4 * (m + 1)), (uint32_t)m, file_len,
-                                       base + loc[i - lo], a.out, a.descs, i - lo, bad);
-                 } else {
-                   for (uint64_t i = lo + tid; i < hi; i += NT)
-                     idx_segment<true>(d, len, (uint32_t)nres, file_len, base + a.local_c[i], a.out, a.descs, i, bad);
-                 }
-               });
+  // the last ticket: every other range has published, read what it needed and written its handles once `done`
+  // counts them all. It alone writes the state, the tail entries (the filter, metaindex and index blocks after the
+  // data blocks) and, when a range is bad, the index block's entry at slot 0; then it resets the words for the next
+  // scan (nobody reads them any more)
+  if (tid == 0) {
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nidx - 1) __builtin_amdgcn_s_sleep(2);
+    if (nres && (badb || nbad)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *a.st = s;
+    a.iopen[2] = 0;  // k_ts_open2's failure mark (every workgroup read it before publishing): clear for the next scan
+  }
+  __syncthreads();
+  ts_emit_body(s, a.st, tid == 0, true, before + run, (badb || nbad) ? 1 : 0, a.file, a.file_len, a.out, a.descs,
+               a.cap, a.vcap, a.idec, [&](const uint8_t*, uint32_t, uint64_t) {});
+  if (tid < nidx) __hip_atomic_store(a.agg + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) {
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((uint32_t*)(a.agg + TSA_TICKET_AT), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   TSI_STAMP(6);
 }
 
@@ -3476,7 +3155,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ts_windows(const uint8_t* __restr
   __shared__ __attribute__((aligned(16))) uint32_t L[A_LDS_BYTES / 4];
   __shared__ uint32_t wg_ticket;
   if (blockIdx.x >= nwg) {
-    ts_index_wg(ia, fkey, blockIdx.x - nwg, gridDim.x - nwg, L);
+    ts_index_wg(ia, fkey, gridDim.x - nwg, L, &wg_ticket);
     return;
   }
   WinOne src{base, span, nreg, out, 0, nullptr, nullptr};
@@ -3543,7 +3222,7 @@ __device__ void ts_finish_tile(uint64_t t, lcrc_tblk_dev* __restrict__ blk, uint
         b.status = c != load_le32(file + b.offset + b.size + 1);
       }
       if (b.status == 0 && b.type > 1) b.status = 4;  // LCRC_TBLK_BAD_TYPE
-      if (b.status == 0 && b.type == 1 && !(k == 2 && st->idx_dec)) flen = (uint32_t)b.size;  // (k_ts_open decoded
+      if (b.status == 0 && b.type == 1 && !(k == 2 && st->idx_dec)) flen = (uint32_t)b.size;  // (k_ts_open2 decoded
       // and checked a Snappy-framed index already)
     }
     lcrc_desc_dev f;
@@ -4263,282 +3942,19 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   TD_STAMP(5);
 }
 
-#ifndef LCRC_TO_TWO_PHASE  // k_ts_open's index chunks through the two-phase decoder (0: the wave decoder)
-#define LCRC_TO_TWO_PHASE 1
-#endif
-// Two-phase decode of one chunk (k_ts_open's index chunks: tens of short elements per window, each key a copy of the
-// last): phase 1 walks the element chain as the wave decoder does (64 candidate starts per window, the chain by
-// v_readlane, the same validation) but only RECORDS the elements -- ea[k] = out position | (length - 1) << 16, eb[k] =
-// literal input position | 1 << 31 or copy offset -- and marks each start in a bitmap over the output. Phase 2 writes
-// the output 64 bytes at a time, one byte per lane: the lane's element is the previous block's last element plus the
-// starts at or below it in this block (a popcount of the bitmap word), its source a literal's input byte or an
-// earlier output byte; a source inside the same 64 bytes (not yet written) is chased by pointer jumping
-// (ds_bpermute, at most six rounds: every source lies before its byte). No batch selection and no element-by-element
-// round trips. Returns 1 decoded, 0 malformed, 2 more elements than ecap (the caller decodes with the wave decoder).
-__device__ uint32_t snappy_two_phase(const uint8_t* in_g, uint32_t q, uint32_t qe, uint8_t* o_g, uint32_t ulen,
-                                     uint32_t* ea_g, uint32_t* eb_g, uint32_t ecap, uint32_t* bm_g, uint32_t lane) {
-  typedef __attribute__((address_space(3))) uint32_t lds_u32;
-  const lds_u8* const in = (const lds_u8*)in_g;
-  lds_u8* const o = (lds_u8*)o_g;
-  lds_u32* const ea = (lds_u32*)ea_g;
-  lds_u32* const eb = (lds_u32*)eb_g;
-  lds_u32* const bm = (lds_u32*)bm_g;
-  const uint32_t nbw = ((ulen + 63) >> 6) * 2;  // bitmap words, whole 64-bit blocks
-  for (uint32_t k = lane; k < nbw; k += 64) bm[k] = 0;
-  uint32_t w0 = 0, ne = 0;
-  for (uint32_t base = q; base < qe;) {
-    const uint32_t i = base + lane;  // candidate start (reads stay inside the staging's slack)
-    const uint32_t t = in[i], b1 = in[i + 1], b2 = in[i + 2], b3 = in[i + 3], b4 = in[i + 4];
-    const uint32_t typ = t & 3;
-    const uint32_t room = qe > i ? qe - i : 0;
-    uint32_t hdr, outlen, a;
-    bool good;
-    if (typ == 0) {
-      const uint32_t L = t >> 2;
-      const uint32_t nb = L >= 60 ? L - 59 : 0;
-      const uint32_t ext = b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
-      const uint32_t lm1 = nb ? (nb == 4 ? ext : ext & ((1u << (8 * nb)) - 1)) : L;
-      hdr = 1 + nb;
-      outlen = lm1 + 1;
-      a = i + hdr;
-      good = room >= hdr && lm1 < room - hdr && (nb == 0 || room >= 5);  // (as snappy_wave_decode)
-    } else {
-      hdr = typ == 1 ? 2 : typ == 2 ? 3 : 5;
-      outlen = typ == 1 ? 4 + ((t >> 2) & 7) : 1 + (t >> 2);
-      a = typ == 1 ? ((t >> 5) << 8) | b1 : typ == 2 ? b1 | (b2 << 8) : b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
-      good = room >= hdr;
-    }
-    const uint32_t size = typ == 0 ? hdr + outlen : hdr;
-    const uint32_t nxt = good ? lane + size : 0x7FFFFFFFu;
-    const uint32_t lim = qe - base < 64 ? qe - base : 64;
-    uint64_t mask = 0;
-    uint32_t cur = 0;
-    while (cur < lim) {
-      mask |= 1ull << cur;
-      cur = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)cur);
-    }
-    const bool sel = (mask >> lane) & 1;
-    const uint32_t v = sel ? outlen : 0u;
-    const uint32_t incl = wave_incl_scan(v, lane);
-    const uint32_t w = w0 + incl - v;
-    const bool bad = sel && (!good || w > ulen || outlen > ulen - w || (typ != 0 && (a == 0 || a > w)));
-    if (__builtin_amdgcn_ballot_w64(bad)) return 0;
-    const uint32_t cnt = (uint32_t)__builtin_popcountll(mask);
-    if (ne + cnt > ecap) return 2;
-    if (sel) {
-      const uint32_t k = ne + (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1));
-      ea[k] = w | ((outlen - 1) << 16);  // (w < ulen <= 65536, outlen <= 65536)
-      eb[k] = typ == 0 ? (a | 0x80000000u) : a;
-      __hip_atomic_fetch_or(&bm[w >> 5], 1u << (w & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    ne += cnt;
-    w0 += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    base += cur;
-  }
-  if (w0 != ulen) return 0;
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-#ifdef LCRC_PROBE_CLOCK
-  {
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0 && blockIdx.x < 1024) lcrc_dbg_stamp[(3072 + blockIdx.x) * 8 + 4] = t_;  // (k_windows: below 3072)
-  }
-#endif
-  int32_t eprev = -1;  // the element covering the byte before this block
-  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-  for (uint32_t x0 = 0; x0 < ulen; x0 += 64) {
-    const uint64_t m = ((uint64_t)bm[(x0 >> 5) + 1] << 32) | bm[x0 >> 5];
-    const uint32_t x = x0 + lane;
-    const bool valid = x < ulen;
-    const int32_t e = eprev + (int32_t)__builtin_popcountll(m & le);
-    const uint32_t A = valid ? ea[e] : 0u, B = valid ? eb[e] : 0x80000000u;
-    const uint32_t ew = A & 0xFFFFu, elen = (A >> 16) + 1;
-    const uint32_t off = x - ew;
-    uint32_t src, fin, ptr = 64;
-    if (B >> 31) {
-      src = (B & 0x7FFFFFFFu) + off;
-      fin = 1;
-    } else {
-      const uint32_t per = B < elen ? B : 0u;  // (a copy is at most 64 bytes long: off < 64)
-      src = per ? ew - B + small_mod(off, per) : x - B;
-      fin = 0;
-      if (valid && src >= x0) ptr = src - x0;  // written in this block: chase it
-    }
-    while (__builtin_amdgcn_ballot_w64(ptr < 64)) {
-      const int p4 = (int)(ptr < 64 ? ptr : lane) * 4;
-      const uint32_t ns = (uint32_t)__builtin_amdgcn_ds_bpermute(p4, (int)src);
-      const uint32_t nf = (uint32_t)__builtin_amdgcn_ds_bpermute(p4, (int)fin);
-      const uint32_t np = (uint32_t)__builtin_amdgcn_ds_bpermute(p4, (int)ptr);
-      if (ptr < 64) {
-        src = ns;
-        fin = nf;
-        ptr = np;
-      }
-    }
-    const uint32_t byte = valid ? (fin ? in[src] : o[src]) : 0u;
-    if (valid) o[x] = (uint8_t)byte;
-    eprev += (int32_t)__builtin_popcountll(m);
-  }
-  return 1;
-}
-
-// ---------------------------------------------------------------------------------------------------
-// k_ts_open (lcrc_table_scan_async_ex with LCRC_TSCAN_SNAPPY_INDEX): the table scan's first launch when the table was
-// written with compression -- its index block is then usually a Snappy frame (table.rs:430, write_block keeps the
-// frame when it saves 12.5%) -- decodes that frame on the device, as Table::open's read_block_from_file does on the
-// host (format.rs:194-206), so that the index walk reads the decoded contents instead of handing the table to the host.
-// One wave per workgroup, the frame's data chunks dealt round-robin over the workgroups. A chunk is decoded in LDS (its
-// whole output: a copy may reach back anywhere in it), its masked CRC-32C computed there (td_chunk_crc), and copied out
-// to the decoded-index workspace; a chunk whose compressed bytes exceed the staging is decoded lane-serially in the
-// workspace and checksummed there. iopen[0]: 1 framed | 2 decoded (framing good, total within the workspace) | 4 over
-// the workspace; iopen[1]: the decoded length; iopen[2]: set by a chunk that does not decode or check (k_ts_emit
-// clears it). The index block's own checksum comes with the batch, as for a raw index; every verdict on the footer
-// and the handle is ts_open_state's.
-// ---------------------------------------------------------------------------------------------------
-#ifdef LCRC_PROBE_CLOCK  // diagnostic build: k_ts_open's per-workgroup phase stamps (s_memrealtime, 100 MHz)
-#define TO_STAMP(i)                                                                              \
-  do {                                                                                           \
-    __builtin_amdgcn_s_waitcnt(0);                                                               \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                              \
-    if (__lane_id() == 0 && blockIdx.x < 1024) lcrc_dbg_stamp[(3072 + blockIdx.x) * 8 + (i)] = t_; \
-  } while (0)
-#else
-#define TO_STAMP(i) \
-  do {              \
-  } while (0)
-#endif
 constexpr uint32_t TO_IN = 32768 + 16;  // compressed bytes staged (+ the dword alignment)
 constexpr uint32_t TO_OUT = 65536;      // a whole chunk's output, V = 0^pad || M a multiple of 1 KiB
-constexpr uint32_t TO_BM = 8192 + 16;   // the two-phase decode's element-start bitmap (+ one word past the end)
-constexpr uint32_t TO_ECAP = 7000;      // its element records (ea, eb); the area then holds the CRC tables
-constexpr uint32_t TO_E = 8 * TO_ECAP;
-static_assert(TO_E >= TD_TAB_WORDS * 4 && TO_E % 16 == 0, "the element area holds the CRC tables afterwards");
-constexpr uint32_t TO_LDS = TO_IN + SN_SLACK + TO_OUT + TO_BM + TO_E;
-static_assert(TO_LDS <= 163840 && (TO_IN + SN_SLACK) % 16 == 0, "k_ts_open's LDS");
-
-__global__ void __launch_bounds__(64) k_ts_open(const uint8_t* __restrict__ file, uint64_t file_len,
-                                               const uint32_t* __restrict__ tab_c, uint8_t* __restrict__ idec,
-                                               uint64_t idec_cap, uint64_t* __restrict__ iopen) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t to_lds[];
-  uint8_t* const lin = to_lds;
-  uint8_t* const lout = lin + TO_IN + SN_SLACK;
-  uint32_t* const bm = (uint32_t*)(lout + TO_OUT);
-  uint32_t* const T = (uint32_t*)(lout + TO_OUT + TO_BM);  // the CRC tables, or the two-phase element records
-  uint32_t* const ea = T;
-  uint32_t* const eb = T + TO_ECAP;
-  const uint32_t lane = __lane_id();
-  TO_STAMP(0);
-  // the footer's index handle, checked as ts_open_state checks it (all lanes alike)
-  uint64_t io = 0, is = 0;
-  bool framed = false;
-  if (file_len >= 48) {
-    const uint8_t* f = file + file_len - 48;
-    const uint64_t magic = (uint64_t)load_le32(f + 40) | ((uint64_t)load_le32(f + 44) << 32);
-    uint64_t mo, ms;
-    uint32_t p = magic == 0xdb4775248b80fb57ull ? dev_varint<64>(f, 0, 48, &mo) : ~0u;
-    if (p != ~0u) p = dev_varint<64>(f, p, 48, &ms);
-    if (p != ~0u) p = dev_varint<64>(f, p, 48, &io);
-    if (p != ~0u) p = dev_varint<64>(f, p, 48, &is);
-    framed = p != ~0u && io <= file_len && is + 5 <= file_len - io && is + 1 <= 0x7FFFFFFFull && file[io + is] == 1;
-  }
-  const uint8_t* const p = file + io;
-  const uint32_t len = (uint32_t)is;
-  uint64_t total = 0, chunks = 0, padded;
-  uint32_t mi, mo;
-  const bool ok = framed && snappy_frame_size(p, len, total, chunks, mi, mo, padded);
-  const bool fits = total <= idec_cap;
-  if (blockIdx.x == 0 && lane == 0) {
-    iopen[1] = ok ? total : 0;
-    iopen[0] = (framed ? 1u : 0u) | (ok && fits ? 2u : 0u) | (ok && !fits ? 4u : 0u);
-  }
-  TO_STAMP(1);
-  if (!ok || !fits || blockIdx.x >= chunks) return;  // (uniform)
-  bool tables = false;  // T holds the CRC tables (the two-phase decode borrows the area)
-  auto load_tables = [&]() {
-    if (!tables) stage_to_lds(tab_c, (lds_u8*)(uint8_t*)T, TD_TAB_WORDS, lane, 64);
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    tables = true;
-  };
-  bool good = true;
-  uint64_t o = 0, k = 0;
-  for (uint32_t at = 0; at < len;) {  // the framing is good (snappy_frame_size): headers and lengths in bounds
-    const uint32_t type = ld_u8(p + at);
-    const uint32_t cl = ld_u8(p + at + 1) | (ld_u8(p + at + 2) << 8) | (ld_u8(p + at + 3) << 16);
-    const uint32_t body = at + 4;
-    at = body + cl;
-    if (type > 1) continue;  // stream identifier, skippable chunks
-    uint32_t ulen = cl - 4, q = body + 4;
-    if (type == 0) {  // preamble = uncompressed length (valid: snappy_frame_size)
-      uint32_t used = 0;
-      snappy_preamble([&](uint32_t i) { return ld_u8(p + q + i); }, at - q, ulen, used);
-      q += used;
-    }
-    const uint64_t oc = o;
-    o += ulen;
-    if (k++ % gridDim.x != blockIdx.x) continue;
-    const uint32_t want = ld_u8(p + body) | (ld_u8(p + body + 1) << 8) | (ld_u8(p + body + 2) << 16) |
-                          ((uint32_t)ld_u8(p + body + 3) << 24);
-    uint32_t crc;
-    bool cok = true;
-    if (type == 1) {  // uncompressed: checksummed where it lies, copied out
-      load_tables();
-      crc = td_chunk_crc<false>(T, p + q, ulen, lane);
-      for (uint32_t x = lane; x < ulen; x += 64) idec[oc + x] = p[q + x];
-    } else if (at - q + 4 <= TO_IN) {
-      TO_STAMP(2);
-      const uint32_t pad = ((ulen + 1023) & ~1023u) - ulen;
-      for (uint32_t x = 16 * lane; x < pad; x += 1024) *(u32x4*)(lout + x) = u32x4{0, 0, 0, 0};
-      const uint8_t* zs = p + q;
-      const uint32_t d = (uint32_t)((uintptr_t)zs & 3);
-      const uint32_t* za = (const uint32_t*)(zs - d);
-      const uint32_t ndw = (d + (at - q) + 3) >> 2;
-      stage_to_lds(za, (lds_u8*)lin, ndw, lane, 64);
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      TO_STAMP(3);
-#if LCRC_TO_TWO_PHASE
-      tables = false;
-      const uint32_t r = snappy_two_phase(lin, d, d + (at - q), lout + pad, ulen, ea, eb, TO_ECAP, bm, lane);
-      cok = r == 2 ? snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane) : r == 1;
-#else
-      cok = snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane);
-#endif
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      TO_STAMP(5);
-      load_tables();
-      crc = cok ? td_chunk_crc<true>(T, lout, ulen, lane) : 0u;
-      TO_STAMP(6);
-      if (cok) {
-        const uint8_t* src = lout + pad;
-        uint32_t x0 = 0;
-        if (((oc | pad) & 15) == 0) {  // whole 16 B pieces, then the tail byte by byte
-          x0 = ulen & ~15u;
-          for (uint32_t x = 16 * lane; x < x0; x += 1024) *(u32x4*)(idec + oc + x) = *(const u32x4*)(src + x);
-        }
-        for (uint32_t x = x0 + lane; x < ulen; x += 64) idec[oc + x] = src[x];
-      }
-    } else {  // too large for the staging: lane-serial in the workspace, checksummed there
-      uint64_t oo = oc;
-      if (lane == 0) cok = sn_serial_decode(p + q, p + at, idec, oo, oc + ulen);
-      cok = bcast(cok ? 1u : 0u) != 0;
-      __threadfence_block();
-      load_tables();
-      crc = cok ? td_chunk_crc<false>(T, idec + oc, ulen, lane) : 0u;
-    }
-    good = good && cok && mask32c(crc) == want;
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();  // the staging is reused by the next chunk
-  }
-  if (!good && lane == 0) iopen[2] = 1;  // (every writer stores the same 1)
-  TO_STAMP(7);
-}
-
-
+constexpr uint32_t TO_BM = 8192 + 16;   // the element-start bitmap (+ one word past the end)
 // ---------------------------------------------------------------------------------------------------
-// k_ts_open2: k_ts_open with a 16-wave workgroup per index chunk (one wave per 64 KiB chunk left 29 CUs
-// decoding the bench table's index for 0.73 ms). The chunk's two-phase decode is made data-parallel end to end:
+// k_ts_open2 (lcrc_table_scan_async_ex with LCRC_TSCAN_SNAPPY_INDEX): the table scan's first launch when the table was
+// written with compression -- its index block is then usually a Snappy frame (table.rs:430, write_block keeps the
+// frame when it saves 12.5%) -- decodes that frame on the device, as Table::open's read_block_from_file does on the
+// host (format.rs:194-206), so that the index walk reads the decoded contents instead of handing the table to the
+// host. iopen[0]: 1 framed | 2 decoded (framing good, total within the workspace) | 4 over the workspace; iopen[1]:
+// the decoded length; iopen[2]: set by a chunk that does not decode or check (the index walk's last ticket clears
+// it). The index block's own checksum comes with the batch, as for a raw index; every verdict on the footer and the
+// handle is ts_open_state's. A 16-wave workgroup per 64 KiB index chunk (round 4's one wave per chunk left 29 CUs
+// decoding the bench table's index for 0.73 ms); the chunk's decode is data-parallel end to end:
 //  A. every parse window (64 candidate element starts) gets, for each candidate, the element that would start there
 //     and -- by pointer jumping inside the window, five ds_bpermute rounds (elements are >= 2 bytes) -- the first
 //     start at or past the window's end reached from it (its exit; a malformed element on the way: none);
@@ -4958,7 +4374,7 @@ __global__ void __launch_bounds__(T2_THREADS) k_ts_open2(const uint8_t* __restri
   lds_u32* const ctl = (lds_u32*)(t2_lds + T2_O_CTL);
   uint16_t* const S = (uint16_t*)(scratch + (uint64_t)blockIdx.x * 65536);
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  // the footer's index handle, by wave 0 (as k_ts_open)
+  // the footer's index handle, by wave 0
   if (tid < 64) {
     uint64_t io = 0, is = 0;
     bool framed = false;
@@ -5262,27 +4678,10 @@ hipError_t lcrc_launch_windows_queue(int grid, const lcrc_qjob_host* jobs, uint3
 // ---- asynchronous table scan (lcrc_table_scan_async) ----
 // grid: a bound on the restart segments (the workgroups past the device count only zero their share)
 // gcap: the most workgroups (the rest of the tiles grid-stride)
-hipError_t lcrc_launch_ts_index(const uint8_t* file, uint64_t file_len, const lcrc_tscan_key* key, uint64_t cap,
-                                lcrc_tscan_dev* st, uint64_t* local_c, uint64_t* local_f, uint64_t* part,
-                                uint64_t bound, uint32_t gcap, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
-                                const uint64_t* iopen, hipStream_t s) {
-  const uint64_t g = bound / 256 + 1;
-  LCRC_LAUNCH(lcrc_dev::k_ts_index, dim3((unsigned)(g < gcap ? g : gcap)), dim3(256), 0, s, file, file_len, *key, cap,
-              st, local_c, local_f, part, zero, nzero, idec, iopen);
-  return hipGetLastError();
-}
-// a Snappy-framed index block decoded into idec (k_ts_open); 64 one-wave workgroups
-// scratch: T2_GRID x 65,536 words (k_ts_open2's pointer-jumping sources); nullptr: the one-wave k_ts_open
+// a Snappy-framed index block decoded into idec (k_ts_open2); scratch: T2_GRID x 65,536 words (its pointer-jumping
+// sources)
 hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uint32_t* tab_c, uint8_t* idec,
                                uint64_t idec_cap, uint64_t* iopen, uint32_t* scratch, hipStream_t s) {
-  if (!scratch) {
-    static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_open,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::TO_LDS);
-    if (attr != hipSuccess) return attr;
-    LCRC_LAUNCH(lcrc_dev::k_ts_open, dim3(64), dim3(64), lcrc_dev::TO_LDS, s, file, file_len, tab_c, idec, idec_cap,
-                iopen);
-    return hipGetLastError();
-  }
   static const hipError_t attr2 = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_open2,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::T2_LDS);
   if (attr2 != hipSuccess) return attr2;
@@ -5291,30 +4690,23 @@ hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uin
   return hipGetLastError();
 }
 uint64_t lcrc_ts_open_scratch_words() { return (uint64_t)lcrc_dev::T2_GRID * 65536; }
-hipError_t lcrc_launch_ts_emit(const uint8_t* file, uint64_t file_len, lcrc_tscan_dev* st, const uint64_t* local_c,
-                               const uint64_t* part, lcrc_tblk_dev* out, lcrc_desc_dev* descs, uint64_t cap,
-                               uint64_t vcap, uint64_t bound, uint32_t gcap, const uint8_t* idec, uint64_t* iopen,
-                               hipStream_t s) {
-  const uint64_t g = bound / 256 + 1;
-  LCRC_LAUNCH(lcrc_dev::k_ts_emit, dim3((unsigned)(g < gcap ? g : gcap)), dim3(256), 0, s, file, file_len, st,
-              local_c, part, out, descs, cap, vcap, idec, iopen);
-  return hipGetLastError();
-}
-// the file's window pass with k_ts_index + k_ts_emit beside it (k_ts_windows): `grid` = CUs; nidx_cap: the index
-// workgroups' cap (lcrc_ctx_options.ts_grid; never more than the CUs, so that they are all resident); agg: nidx_cap +
-// 1 words, zero
-hipError_t lcrc_launch_ts_windows(int grid, const uint8_t* file, uint64_t file_len, const uint32_t* gtab, uint32_t* win,
-                                  const lcrc_tscan_key* key, uint64_t cap, uint64_t vcap, lcrc_tscan_dev* st,
-                                  uint64_t* local_c, uint32_t* zero, uint64_t nzero, const uint8_t* idec,
-                                  const uint64_t* iopen_r, uint64_t* iopen, lcrc_tblk_dev* out, lcrc_desc_dev* descs,
-                                  uint64_t* agg, uint32_t nidx_cap, hipStream_t s) {
+// the table scan's index walk and handles (k_ts_windows' index workgroups), with the file's window pass beside them
+// when `windows` (grid = CUs; without it the index workgroups alone: the one-pass general path, or no result
+// capacity). nidx_cap: the index workgroups' cap (lcrc_ctx_options.ts_grid); agg: TSA_MAX + 2 words, zero
+hipError_t lcrc_launch_ts_windows(int grid, bool windows, const uint8_t* file, uint64_t file_len, const uint32_t* gtab,
+                                  uint32_t* win, const lcrc_tscan_key* key, uint64_t cap, uint64_t vcap,
+                                  lcrc_tscan_dev* st, uint64_t* local_c, uint32_t* zero, uint64_t nzero,
+                                  const uint8_t* idec, const uint64_t* iopen_r, uint64_t* iopen, lcrc_tblk_dev* out,
+                                  lcrc_desc_dev* descs, uint64_t* agg, uint32_t nidx_cap, hipStream_t s) {
   const uint64_t nreg = (file_len + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
   const uint64_t need = (nreg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
   const uint64_t gw = (uint64_t)grid * lcrc_dev::A_WG_PER_CU;
-  const uint32_t nwg = (uint32_t)(need < gw ? need : gw);
+  const uint32_t nwg = windows ? (uint32_t)(need < gw ? need : gw) : 0u;
+  // one index workgroup per 512 restart segments (a segment names at least one block), at most one per CU
   uint64_t nidx = cap / lcrc_dev::A_THREADS + 1;
   if (nidx > nidx_cap) nidx = nidx_cap;
   if (nidx > (uint64_t)grid) nidx = (uint64_t)grid;
+  if (nidx > lcrc_dev::TSA_MAX) nidx = lcrc_dev::TSA_MAX;
   if (nidx == 0) nidx = 1;
   lcrc_dev::TsIdxArgs ia{file, file_len, cap, cap, vcap, nzero, st, local_c, zero, idec, iopen_r, iopen, out, descs, agg};
   LCRC_LAUNCH(lcrc_dev::k_ts_windows, dim3((unsigned)(nwg + nidx)), dim3(lcrc_dev::A_THREADS), 0, s, file, file_len,
@@ -5400,41 +4792,13 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  uint64_t* n_out, hipStream_t st) {
   const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
   if (nparts)
-    LCRC_LAUNCH(lcrc_dev::k_wal_parse<false>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks,
-                counts, slots, stops, local, part, nullptr);
+    LCRC_LAUNCH(lcrc_dev::k_wal_parse, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks,
+                counts, slots, stops, local, part);
   const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
   const uint64_t g = (nt + 255) / 256;
   LCRC_LAUNCH(lcrc_dev::k_wal_emit, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, nblocks, counts, slots,
                      stops, local, part, recs, descs, max_recs, n_total, n_out);
   return hipGetLastError();
-}
-
-// the one-pass WAL scan (lcrc_ctx_options.wal_onepass): header walk, emit (region lists + k_blocks descriptors), the
-// window pass that finishes the listed records, k_blocks over the rest (their count on the device, n_kb)
-hipError_t lcrc_launch_wal_onepass(int grid_a, int grid_b, const uint8_t* file, uint64_t file_len, uint64_t nblocks,
-                                   uint32_t* counts, uint2* slots, uint8_t* stops, uint64_t* local, uint64_t* part,
-                                   uint32_t* rl_cnt, uint4* rl, lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs,
-                                   uint64_t max_recs, uint64_t* n_total, uint64_t* n_out, uint64_t* n_kb,
-                                   uint32_t* win, const uint32_t* gtab, uint32_t init, uint32_t xorout, uint32_t poly,
-                                   uint32_t* crcs, hipStream_t st) {
-  const uint64_t nparts = (nblocks + lcrc_dev::WAL_PARTB - 1) / lcrc_dev::WAL_PARTB;
-  if (nparts)
-    LCRC_LAUNCH(lcrc_dev::k_wal_parse<true>, dim3((unsigned)nparts), dim3(64), 0, st, file, file_len, nblocks, counts,
-                slots, stops, local, part, rl_cnt);
-  const uint64_t nt = nblocks * lcrc_dev::WAL_SLOTS;
-  const uint64_t g = (nt + 255) / 256;
-  LCRC_LAUNCH(lcrc_dev::k_wal_emit1, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, file, file_len, nblocks, counts, slots,
-              stops, local, part, recs, descs, max_recs, n_total, n_out, rl, n_kb);
-  if (max_recs == 0) return hipGetLastError();
-  const uint64_t nreg = (file_len + lcrc_dev::REGION - 1) / lcrc_dev::REGION;
-  if (nreg) {
-    const uint64_t need = (nreg + lcrc_dev::A_THREADS / 64 - 1) / (lcrc_dev::A_THREADS / 64);
-    const int ga = (int)(need < (uint64_t)grid_a ? need : (uint64_t)grid_a);
-    LCRC_LAUNCH(lcrc_dev::k_windows_wal, dim3(ga), dim3(lcrc_dev::A_THREADS), 0, st, file, file_len, nreg, gtab, win,
-                rl_cnt, rl, recs, max_recs, init, xorout, poly);
-  }
-  return lcrc_launch_blocks(false, grid_b, file, file_len, descs, max_recs, 0, 0, nullptr, win, gtab, init, xorout, 0,
-                            crcs, nullptr, n_kb, recs, st);
 }
 
 // several logs' header walks and record emits, two launches (lcrc_wal_scan_queue); m <= MAX_WJOBS

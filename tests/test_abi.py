@@ -48,10 +48,10 @@ def test_ctx_options_mirror(lcrc):
     with open(os.path.join(ROOT, "include", "lcrc.h")) as f:
         src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
     body = re.search(r"typedef struct lcrc_ctx_options \{(.*?)\} lcrc_ctx_options;", src, flags=re.S).group(1)
-    fields = re.findall(r"(u?int32_t)\s+(\w+);", body)
-    assert [n for _, n in fields] == [n for n, _ in lcrc._CtxOptions._fields_]
+    fields = re.findall(r"(u?int32_t)\s+(\w+)(?:\[(\d+)\])?;", body)
+    assert [n for _, n, _c in fields] == [n for n, _ in lcrc._CtxOptions._fields_]
     import ctypes
-    assert ctypes.sizeof(lcrc._CtxOptions) == 4 * len(fields)
+    assert ctypes.sizeof(lcrc._CtxOptions) == 4 * sum(int(c or 1) for _, _n, c in fields)
 
 
 @pytest.mark.parametrize("n", [0, 1, 3, 7, 8, 9, 16, 100, 4096, 100003])

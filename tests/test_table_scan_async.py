@@ -285,14 +285,14 @@ def test_async_long_meta_blocks(lcrc, orc, mode, masked):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("unfused", [0, 1])
+@pytest.mark.parametrize("general", ["auto", "ranges"])
 @pytest.mark.parametrize("grid", [1, 3])
-def test_async_tile_loops(lcrc, orc, grid, unfused):
-    """The index walk with fewer workgroups than tiles (the context option ts_grid caps their grid). Separate
-    launches (ts_unfused, k_ts_index / k_ts_emit): a workgroup scans several 256-segment tiles and emit adds the
-    totals of every tile before each one. Beside the window pass (k_ts_windows): a workgroup walks a range of
-    several 512-segment chunks, and the ranges' counts meet through the per-workgroup totals."""
-    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_grid=grid, ts_unfused=unfused)
+def test_async_tile_loops(lcrc, orc, grid, general):
+    """The index walk with fewer workgroups than 512-segment chunks (the context option ts_grid caps their grid): a
+    workgroup walks a range of several chunks, and the ranges' counts meet through the per-ticket words. Beside the
+    window pass (k_ts_windows, the default) and alone (general="ranges": the one-pass range kernel verifies, so the
+    launch holds only the index workgroups)."""
+    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_grid=grid, general=general)
     try:
         f, blocks = orc.table_build(_kvs(6000, 41), block_size=256, compression=1, index_restart_interval=1,
                                     filter_name=FILTER, filter_block=b"z" * 100)
@@ -473,12 +473,10 @@ def test_async_snappy_index_graph_replay(lcrc, orc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("v1", [0, 1])
-def test_async_snappy_index_decoders_agree(lcrc, orc, v1):
-    """The compressed index through k_ts_open2 (16 waves per chunk, the default) and the round-4 one-wave k_ts_open
-    (context option ts_open_v1): a multi-chunk index, clean and with a chunk that does not decode, the oracle's
-    result either way."""
-    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_open_v1=v1)
+def test_async_snappy_index_multi_chunk(lcrc, orc):
+    """The compressed index through k_ts_open2 (16 waves per 64 KiB chunk): a multi-chunk index, clean and with a
+    chunk that does not decode, the oracle's result either way."""
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
     try:
         f, blocks = orc.table_build(_seq_kvs(40000), block_size=128, compression=1)
         off, size, _ = _index_block(f, blocks)
@@ -509,8 +507,8 @@ def test_async_index_ranges(lcrc, orc, grid, skew):
     """The index walk beside the window pass (k_ts_windows): each index workgroup stages its range of restart
     segments in LDS with the range's offsets rebased (a range too long for the LDS is walked in place: one workgroup,
     grid 1, over this ~120 KB index). Restart arrays and entries corrupted at range boundaries and inside ranges, the
-    index block re-sealed so that the walk must judge them: the verdict, count and blocks equal those of the separate
-    k_ts_index / k_ts_emit launches (ts_unfused), and the synchronous scan gives the oracle's answer. The skewed
+    index block re-sealed so that the walk must judge them: the verdict, count and blocks equal those of the index
+    workgroups launched alone (general="ranges"), and the synchronous scan gives the oracle's answer. The skewed
     table's ranges lie far from where even entries would put them (the walk's speculative load of a range's bytes
     misses, and a second round loads them)."""
     kvs = _skewed_kvs(16000, 17) if skew else _kvs(16000, 17)
@@ -521,7 +519,7 @@ def test_async_index_ranges(lcrc, orc, grid, skew):
     ra = off + size - 4 * (1 + nres)
     cap = len(blocks) + 4
     opts = {"ts_grid": grid} if grid else {}
-    fused, unfused = lcrc.Engine(0, lcrc.MODE_REF, **opts), lcrc.Engine(0, lcrc.MODE_REF, ts_unfused=1, **opts)
+    fused, unfused = lcrc.Engine(0, lcrc.MODE_REF, **opts), lcrc.Engine(0, lcrc.MODE_REF, general="ranges", **opts)
 
     def rst(g, k):
         return int.from_bytes(g[ra + 4 * k:ra + 4 * k + 4], "little")
@@ -577,12 +575,11 @@ def test_async_index_ranges(lcrc, orc, grid, skew):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("unfused", [0, 1])
-def test_async_last_three_at_tile_edges(lcrc, orc, unfused):
+def test_async_last_three_at_tile_edges(lcrc, orc):
     """The last three blocks (filter as a Snappy frame, metaindex, Snappy-framed index) at every position across a
     256-block tile edge: k_ts_decode's last workgroup finishes, decodes and judges them -- fused, also the finish of a
     tile that holds only some of them -- and the workspace offsets of their frames follow the tiles before."""
-    eng = lcrc.Engine(0, lcrc.MODE_REF, ts_unfused=unfused)
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
     try:
         for k in (1, 2, 252, 253, 254, 255, 256, 257, 509, 510, 511, 512, 513):
             f, blocks = orc.table_build(_seq_kvs(k), block_size=1, compression=1, filter_name=FILTER,
@@ -601,8 +598,8 @@ def test_async_last_three_at_tile_edges(lcrc, orc, unfused):
 @pytest.mark.gpu
 def test_async_two_contexts_concurrent(lcrc, orc):
     """Two contexts scanning on their own streams at once, several rounds back to back (as bench.py's two scanners
-    do): each scan's index workgroups wait only for their own launch's totals, and the totals' words are zeroed
-    for the next scan by the last arrival -- every result equals the oracle's."""
+    do): each scan's index workgroups wait only for their own launch's words, and the words are zeroed for the next
+    scan by the last ticket -- every result equals the oracle's."""
     f1, b1 = orc.table_build(_kvs(5000, 71), block_size=256, compression=0, filter_name=FILTER, filter_block=b"a" * 50)
     f2, b2 = orc.table_build(_kvs(7000, 72), block_size=512, compression=1, filter_name=FILTER, filter_block=b"b" * 70)
     engs = [lcrc.Engine(0, lcrc.MODE_REF), lcrc.Engine(0, lcrc.MODE_REF)]
@@ -622,6 +619,64 @@ def test_async_two_contexts_concurrent(lcrc, orc):
                 assert st == OK and sorted(_as_tuples(got)) == w
     finally:
         for s, _f in scans:
+            s.close()
+        for eng in engs:
+            eng.close()
+
+
+@pytest.mark.gpu
+def test_async_four_contexts_full_index_grid(lcrc, orc):
+    """Four contexts on four streams, each scanning a table of more than 131,072 blocks (so 256 index workgroups per
+    launch, the cap) three times, all enqueued before any synchronisation: 4 x (256 index + the window workgroups)
+    is more than the 512 workgroups the CUs hold at once, so the index workgroups of one launch are not all resident
+    together. The ticketed look-back (each index workgroup waits only on tickets taken before its own) must still end
+    every launch, and every result equals the oracle's (table.rs:39-146, format.rs:146-171). One table has a
+    corrupt index entry, so its last ticket writes the index block alone at slot 0 over the handles lower tickets
+    wrote there."""
+    tables = []
+    for k in range(4):
+        f, blocks = orc.table_build(_seq_kvs(131_200 + 500 * k, vlen=4 + 3 * k, seed=40 + k), block_size=1,
+                                    compression=0, filter_name=FILTER if k % 2 else None, filter_block=b"q" * 64)
+        assert sum(1 for b in blocks if b[2] == 0) > 131_072
+        tables.append((f, blocks, FILTER if k % 2 else None))
+    # table 3: an index entry inside the last range made unreadable and the index block's trailer NOT re-sealed: the
+    # device walk cannot vouch for that segment, so the scan verifies the index block alone -- the last ticket's entry
+    # at slot 0, over the data handle ticket 0 wrote there -- and must report the reference's checksum message (a
+    # data handle left at slot 0 would verify clean and say LCRC_TSCAN_HOST instead)
+    f, blocks, filt = tables[3]
+    off, size, _ = _index_block(f, blocks)
+    nres = int.from_bytes(f[off + size - 4:off + size], "little")
+    ra = off + size - 4 * (1 + nres)
+    g = bytearray(f)
+    e = int.from_bytes(g[ra + 4 * (nres - 10):ra + 4 * (nres - 9)], "little")
+    g[off + e + 1] = 0xFF  # the entry's non_shared varint
+    tables[3] = (bytes(g), blocks, filt)
+    want = [orc.table_scan_expect(f, filt) for f, _b, filt in tables]
+    assert want[3][1] == "block checksum mismatch" and all(w[1] is None for w in want[:3])
+    engs = [lcrc.Engine(0, lcrc.MODE_REF) for _ in range(4)]
+    scans = []
+    try:
+        for eng, (f, blocks, _filt) in zip(engs, tables):
+            cap = len(blocks) + 4
+            assert cap // 512 + 1 >= 256  # the index grid is at its cap
+            eng.table_scan_reserve(len(f), cap, 1 << 20)
+            scans.append(_Scan(lcrc, f, cap))
+        for _ in range(3):
+            for s in scans:
+                s.blocks.zero()
+                s.count.zero()
+            for eng, s, (_f, _b, filt) in zip(engs, scans, tables):
+                eng.table_scan_async(s.file, s.n, s.blocks, s.cap, s.count, s.status, filt)
+            for eng in engs:
+                eng.sync()
+            for k, (s, (w, werr)) in enumerate(zip(scans, want)):
+                st, code, n, got = s.read()
+                if werr is None:
+                    assert st == OK and sorted(_as_tuples(got)) == w, k
+                else:
+                    assert st == CORRUPT and lcrc.lib().lcrc_table_scan_message(code).decode() == werr, k
+    finally:
+        for s in scans:
             s.close()
         for eng in engs:
             eng.close()
