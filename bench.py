@@ -746,11 +746,21 @@ def workload_snappy(m, synth, engs, rank, device, args):
 # evidence: committed profiles, CPU baseline
 # ---------------------------------------------------------------------------------------------------
 def load_traffic(config, mode):
+    """The committed PMC traffic of this config (tools/summarize_profile.py): HBM bytes read + written per STEP over
+    every kernel of the step (the contract's `traffic`), and the read / write split with the streaming kernel's own
+    figure beside it."""
     path = os.path.join(ROOT, "profiles", f"traffic_{config}_{mode}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        t = json.load(f)
+    rd, wr = t.get("step_hbm_read_bytes"), t.get("step_hbm_write_bytes")
+    if rd is None or wr is None:
+        return {"traffic": t.get("hbm_bytes_per_launch")}
+    return {"traffic": rd + wr, "detail": {
+        "step_read_bytes": round(rd), "step_write_bytes": round(wr), "stream_kernel": t.get("kernel"),
+        "stream_kernel_read_bytes": round(t.get("hbm_read_bytes_per_launch", 0)),
+        "stream_kernel_write_bytes": round(t.get("hbm_write_bytes_per_launch", 0)), "source": t.get("source")}}
 
 
 def load_profile(config, mode, streams=2):
@@ -945,9 +955,13 @@ def main(argv=None):
         launch_s = gpu_ms / 1e3 / cov_launches
         bytes_per_launch = w.nbytes * cov_steps / cov_launches
         achieved = bytes_per_launch / launch_s / 1e9
+        tr = load_traffic(prof_config, args.mode) or {}
+        if tr.get("detail"):
+            tr["detail"]["step_read_x"] = round(tr["detail"]["step_read_bytes"] / bytes_per_launch, 4)
+            tr["detail"]["step_write_x"] = round(tr["detail"]["step_write_bytes"] / bytes_per_launch, 4)
         result["roofline"] = {
             "bound": w.bound, "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / PEAK_GBS, 4), "traffic": load_traffic(prof_config, args.mode),
+            "frac": round(achieved / PEAK_GBS, 4), "traffic": tr.get("traffic"), "traffic_detail": tr.get("detail"),
             "bytes_per_launch": int(bytes_per_launch), "launches": cov_launches, "steps_timed_on_gpu": cov_steps,
             "launch_us": round(launch_s * 1e6, 2),
             "timing": timing_text(w, timers, one_stream),

@@ -67,6 +67,7 @@ hipError_t lcrc_launch_wal_parse(const uint8_t* file, uint64_t file_len, uint64_
                                  lcrc_wal_rec_dev* recs, lcrc_desc_dev* descs, uint64_t max_recs, uint64_t* n_total,
                                  uint64_t* n_out, hipStream_t st);
 hipError_t lcrc_launch_wal_parse_queue(const lcrc_wjob_dev_host* jobs, uint32_t m, hipStream_t st);
+
 hipError_t lcrc_launch_snappy_size(const uint8_t* base, const lcrc_desc_dev* frames, uint64_t n, uint64_t* size,
                                    uint64_t* nchunks, uint8_t* status, uint32_t* maxes, const uint64_t* n_dev,
                                    hipStream_t st);
@@ -160,12 +161,12 @@ struct lcrc_ctx {
   DevBuf<uint8_t> chunk[2];   // host-resident pipeline staging
   DevBuf<uint32_t> hexp[2];   // expected values per chunk
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
-  DevBuf<uint32_t> wal_counts;
-  DevBuf<uint2> wal_slots;
-  DevBuf<uint8_t> wal_stops;
   DevBuf<uint64_t> wal_offsets;
   DevBuf<lcrc_desc_dev> wal_descs;
   DevBuf<uint32_t> wal_crcs;
+  DevBuf<uint32_t> wal_counts;
+  DevBuf<uint2> wal_slots;
+  DevBuf<uint8_t> wal_stops;
   // lcrc_batch_multi: this context's shard (the byte span its descriptors cover, the rebased descriptors,
   // CRCs and mismatch words)
   DevBuf<uint8_t> ms_data;
@@ -293,6 +294,14 @@ int set_device(lcrc_ctx* ctx) {
 }
 
 hipStream_t pick_stream(lcrc_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+// A newly allocated word array the kernels expect zero (tickets, look-back words), zeroed and FINISHED before any
+// later launch on any stream: hipMemset goes to the null stream, which the contexts' non-blocking streams do not wait
+// for, and a freshly allocated buffer may hold a freed one's bytes
+hipError_t zero_now(lcrc_ctx* ctx, void* p, size_t bytes) {
+  hipError_t e = hipMemsetAsync(p, 0, bytes, ctx->stream);
+  return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
+}
 
 }  // namespace
 
@@ -427,12 +436,12 @@ int lcrc_ctx_destroy(lcrc_ctx* ctx) {
     if (ctx->ev_copied[i]) (void)hipEventDestroy(ctx->ev_copied[i]);
     if (ctx->ev_done[i]) (void)hipEventDestroy(ctx->ev_done[i]);
   }
-  ctx->wal_counts.release();
-  ctx->wal_slots.release();
-  ctx->wal_stops.release();
   ctx->wal_offsets.release();
   ctx->wal_descs.release();
   ctx->wal_crcs.release();
+  ctx->wal_counts.release();
+  ctx->wal_slots.release();
+  ctx->wal_stops.release();
   ctx->ms_data.release();
   ctx->ms_desc.release();
   ctx->ms_out.release();
@@ -1355,7 +1364,7 @@ static uint64_t ts_verify_cap(size_t max_blocks, uint64_t file_len) {
 
 // the device-only scan's workspace (every buffer its launches touch; nothing else: the host-assisted scan and
 // lcrc_snappy_frames size their own)
-constexpr uint32_t TS_AGG_WORDS = 258;  // k_ts_windows: at most 256 index workgroups, then the done count, the ticket
+constexpr uint32_t TS_AGG_WORDS = 257;  // k_ts_windows: at most 256 index workgroups' words, then the ticket counter
 constexpr uint32_t TS_MAX_IDX = 256;
 
 static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, uint64_t decoded_cap) {
@@ -1374,11 +1383,11 @@ static int ts_reserve(lcrc_ctx* ctx, uint64_t max_file_len, size_t max_blocks, u
     return rc;
   if (!ctx->ts_open.p) {
     if ((rc = ctx->ts_open.ensure(4))) return rc;
-    HIPCHK(hipMemset(ctx->ts_open.p, 0, 4 * sizeof(uint64_t)));
+    HIPCHK(zero_now(ctx, ctx->ts_open.p, 4 * sizeof(uint64_t)));
   }
   if (!ctx->ts_agg.p) {
     if ((rc = ctx->ts_agg.ensure(TS_AGG_WORDS))) return rc;
-    HIPCHK(hipMemset(ctx->ts_agg.p, 0, TS_AGG_WORDS * sizeof(uint64_t)));
+    HIPCHK(zero_now(ctx, ctx->ts_agg.p, TS_AGG_WORDS * sizeof(uint64_t)));
   }
   if (ctx->mode != LCRC_MODE_C && !ctx->d_tab_c && (rc = upload_tables(LCRC_MODE_C, &ctx->d_tab_c))) return rc;
   ctx->ts_decoded_cap = decoded_cap;
@@ -1721,7 +1730,10 @@ int lcrc_memcpy_d2h(void* dst, const void* src, size_t bytes) {
   return LCRC_OK;
 }
 int lcrc_memset_d(void* dst, int value, size_t bytes) {
-  HIPCHK(hipMemset(dst, value, bytes));
+  // finished when this returns (a fill left queued on the null stream is not ordered before the contexts'
+  // non-blocking streams)
+  HIPCHK(hipMemsetAsync(dst, value, bytes, nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));
   return LCRC_OK;
 }
 int lcrc_device_sync(void) {

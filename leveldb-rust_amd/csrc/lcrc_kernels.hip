@@ -1530,6 +1530,7 @@ __global__ void __launch_bounds__(A_THREADS) k_ranges(const uint8_t* __restrict_
 // LogReader::read_physical_record (src/db/log.rs:204-279) does, minus the checksum (k_blocks computes it,
 // in parallel over all records, and stores it with the verdict in the record); k_wal_emit writes the
 // records and their descriptors at their file-order positions. Nothing returns to the host in between.
+// (Several logs, lcrc_wal_scan_queue: k_wal_parse_q walks every log's blocks in one launch, k_wal_emit_q emits.)
 // ---------------------------------------------------------------------------------------------------
 constexpr uint32_t WAL_SLOTS = 64;  // records per block kept by the parse (a block with more is re-walked)
 
@@ -1547,10 +1548,8 @@ __device__ __forceinline__ void wal_header(const uint8_t* __restrict__ blk, uint
 // one lane per block: record count, stop reason and the first WAL_SLOTS records as (offset | length << 16,
 // type), and the wave's exclusive scan of the counts: local[b] (u32) and part[wave] (the total). One wave
 // per workgroup, so the waves spread over the CUs instead of sharing one CU's address units four apiece.
-//
 // The walk is one dependent memory round trip per record, so the block with the most records sets the
-// kernel's time. (Staging a window of the block in LDS per lane and following the chain there measured slower
-// alone and beside a window pass)
+// kernel's time.
 constexpr uint32_t WAL_PARTB = 64;  // blocks per parse workgroup (= per part total)
 
 // The WAL scan orders its record descriptors for k_blocks with the records whose covered bytes
@@ -2861,15 +2860,15 @@ __device__ void ts_emit_body(const lcrc_tscan_dev& s, lcrc_tscan_dev* __restrict
 // at most 256 words, one polling thread each). A lower ticket was taken by a workgroup that has started, so it is
 // resident or done, and it publishes without waiting: every wait ends whatever else occupies the CUs. Each ticket
 // writes its handles at its offset (slots bounded by the capacity, since only the last ticket knows the total) and
-// counts itself in agg[TSA_DONE_AT]; the last ticket (nidx - 1) waits for that count -- its lower tickets again --,
-// then alone writes the state, the filter / metaindex / index entries after the data blocks, and when a range is
+// then sets the done bit of its word; the last ticket (nidx - 1) waits for every done bit -- its lower tickets
+// again --, then alone writes the state, the filter / metaindex / index entries after the data blocks, and when a range is
 // bad the index block's entry at slot 0 (the one slot another range may have written: that range releases its
 // stores before counting itself, the last ticket acquires), and zeroes the words for the next scan. Each index
 // workgroup computes the footer state itself (the metaindex walk included), so that none reads another's. The
 // totals travel inside the atomic words themselves, so the polls are relaxed: an acquire/release at agent scope
 // writes back / invalidates the XCD's L2, under the window stream, and is paid once, by the two workgroups above.
-constexpr uint64_t TSA_READY = 1ull << 63, TSA_BAD = 1ull << 62, TSA_COUNT = (1ull << 62) - 1;
-constexpr uint32_t TSA_MAX = 256, TSA_DONE_AT = TSA_MAX, TSA_TICKET_AT = TSA_MAX + 1;  // agg: 258 words
+constexpr uint64_t TSA_READY = 1ull << 63, TSA_BAD = 1ull << 62, TSA_DONE = 1ull << 61, TSA_COUNT = TSA_DONE - 1;
+constexpr uint32_t TSA_MAX = 256, TSA_TICKET_AT = TSA_MAX;  // agg: 257 words
 static_assert(A_THREADS >= TSA_MAX, "a thread per lower ticket's word");
 struct TsIdxArgs {
   const uint8_t* file;
@@ -2940,6 +2939,7 @@ __device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint
     *ticket = __hip_atomic_fetch_add((uint32_t*)(a.agg + TSA_TICKET_AT), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const uint32_t j = *ticket;  // this workgroup's range (the order in which the index workgroups started)
+  if (j >= nidx) return;       // (never: the counter is zero at every launch; no store past the words if it were not)
   TSI_STAMP(0);
 #ifndef LCRC_TSI_PRIO
 #define LCRC_TSI_PRIO 3
@@ -3115,24 +3115,27 @@ __device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint
     }
   }
   __syncthreads();
-  uint32_t* const done = (uint32_t*)(a.agg + TSA_DONE_AT);
   const bool last = j == nidx - 1;
   if (!last) {
     if (tid == 0) {
       // slot 0 is the one the last ticket may overwrite (the index block alone): a range that wrote it makes its
-      // stores visible across the XCDs' L2s before it counts itself done
+      // stores visible across the XCDs' L2s before it marks itself done
       if (write && before == 0 && run) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // done: on its own word, so that the last ticket's reset of that word is ordered after both of its stores
+      __hip_atomic_fetch_or(a.agg + j, TSA_DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     TSI_STAMP(6);
     return;
   }
-  // the last ticket: every other range has published, read what it needed and written its handles once `done`
-  // counts them all. It alone writes the state, the tail entries (the filter, metaindex and index blocks after the
-  // data blocks) and, when a range is bad, the index block's entry at slot 0; then it resets the words for the next
-  // scan (nobody reads them any more)
+  // the last ticket: every other range has published, read what it needed and written its handles once its word
+  // says done. It alone writes the state, the tail entries (the filter, metaindex and index blocks after the data
+  // blocks) and, when a range is bad, the index block's entry at slot 0; then it resets the words for the next scan
+  // (nobody reads them any more)
+  if (tid < j)
+    while (!(__hip_atomic_load(a.agg + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TSA_DONE))
+      __builtin_amdgcn_s_sleep(2);
+  __syncthreads();
   if (tid == 0) {
-    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nidx - 1) __builtin_amdgcn_s_sleep(2);
     if (nres && (badb || nbad)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     *a.st = s;
     a.iopen[2] = 0;  // k_ts_open2's failure mark (every workgroup read it before publishing): clear for the next scan
@@ -3141,10 +3144,8 @@ __device__ void ts_index_wg(const TsIdxArgs& a, const lcrc_tscan_key& fkey, uint
   ts_emit_body(s, a.st, tid == 0, true, before + run, (badb || nbad) ? 1 : 0, a.file, a.file_len, a.out, a.descs,
                a.cap, a.vcap, a.idec, [&](const uint8_t*, uint32_t, uint64_t) {});
   if (tid < nidx) __hip_atomic_store(a.agg + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid == 0) {
-    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((uint32_t*)(a.agg + TSA_TICKET_AT), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  // (every ticket was taken before this one's: the count is nidx)
+  if (tid == 0) __hip_atomic_store((uint32_t*)(a.agg + TSA_TICKET_AT), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   TSI_STAMP(6);
 }
 
@@ -4692,7 +4693,7 @@ hipError_t lcrc_launch_ts_open(const uint8_t* file, uint64_t file_len, const uin
 uint64_t lcrc_ts_open_scratch_words() { return (uint64_t)lcrc_dev::T2_GRID * 65536; }
 // the table scan's index walk and handles (k_ts_windows' index workgroups), with the file's window pass beside them
 // when `windows` (grid = CUs; without it the index workgroups alone: the one-pass general path, or no result
-// capacity). nidx_cap: the index workgroups' cap (lcrc_ctx_options.ts_grid); agg: TSA_MAX + 2 words, zero
+// capacity). nidx_cap: the index workgroups' cap (lcrc_ctx_options.ts_grid); agg: TSA_MAX + 1 words, zero
 hipError_t lcrc_launch_ts_windows(int grid, bool windows, const uint8_t* file, uint64_t file_len, const uint32_t* gtab,
                                   uint32_t* win, const lcrc_tscan_key* key, uint64_t cap, uint64_t vcap,
                                   lcrc_tscan_dev* st, uint64_t* local_c, uint32_t* zero, uint64_t nzero,

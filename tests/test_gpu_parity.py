@@ -866,6 +866,84 @@ def test_wal_config3_full_size(lcrc, orc, synth, engines):
     assert (got_s["status"] == 0).all()
 
 
+def test_wal_capacity_below_count_after_larger_scan(lcrc, orc, synth):
+    """lcrc_wal_scan_async with max_recs below the record count, on a context that has just scanned a larger log with
+    the full capacity (so its descriptor and record buffers hold that scan's entries): every record below max_recs --
+    including a corrupted one -- has the oracle's header, crc and verdict (log.rs:204-279), the count is the full one,
+    and nothing past max_recs is written. Capacities inside the first walk ticket (32 blocks), at a ticket edge and
+    inside a later ticket."""
+    big = _wal_file(lcrc, synth, 24 << 20, 0x5EED0031)
+    data = _wal_file(lcrc, synth, 12 << 20, 0x5EED0032)
+    want = _wal_expect(orc, data)
+    k_bad = len(want) // 3
+    h, n, _ = want[k_bad]
+    data[h + 6 + n // 2] ^= 0x08
+    eng = lcrc.Engine(0, lcrc.MODE_REF)
+    try:
+        _wal_check_scan(lcrc, orc, eng, big, 0)
+        dev = lcrc.DeviceBuffer.from_host(np.frombuffer(bytes(data), np.uint8))
+        hh = np.array([x[0] for x in want], np.uint64)
+        ln = np.array([x[1] for x in want], np.uint64)
+        crc, _ = orc.crc_ranges_mt(bytes(data), hh + 6, ln + 1, 8, orc.ALGO_PCLMUL_REF)
+        a = np.frombuffer(bytes(data), np.uint8)
+        stored = np.array([int.from_bytes(bytes(a[int(x):int(x) + 4]), "little") for x in hh], np.uint32)
+        edge = sum(1 for x in want if x[0] < 32 * 32768)  # the records of ticket 0's 32 blocks
+        for cap in (5, edge, edge + 1, k_bad + 10, len(want) - 1):
+            rd = lcrc.DeviceBuffer((cap + 64) * lcrc.WAL_REC_DTYPE.itemsize)
+            rd.upload(np.full((cap + 64) * lcrc.WAL_REC_DTYPE.itemsize, 0xEE, np.uint8))
+            cnt = lcrc.DeviceBuffer(8)
+            eng.wal_scan_async(dev, len(data), rd, cap, cnt)
+            eng.sync()
+            assert int(cnt.download(np.uint64, 1)[0]) == len(want), cap
+            raw = rd.download(np.uint8, (cap + 64) * lcrc.WAL_REC_DTYPE.itemsize)
+            assert (raw[cap * lcrc.WAL_REC_DTYPE.itemsize:] == 0xEE).all(), cap
+            got = raw[:cap * lcrc.WAL_REC_DTYPE.itemsize].view(lcrc.WAL_REC_DTYPE)
+            assert np.array_equal(got["header"], hh[:cap]), cap
+            assert np.array_equal(got["crc"], crc[:cap]), cap
+            assert np.array_equal(got["status"], (stored[:cap] != crc[:cap]).astype(np.uint8)), cap
+            assert (cap <= k_bad) or got["status"][k_bad] == 1
+    finally:
+        eng.close()
+
+
+def test_wal_four_contexts_concurrent(lcrc, orc, synth):
+    """Four contexts scanning four different logs on their own streams at once, three rounds enqueued back to back:
+    each launch's walk workgroups take tickets from their own context's counter and look back only at their own
+    launch's words, which the last ticket zeroes for the next scan -- every record, crc and verdict equals the
+    oracle's walk (log.rs:204-279) every round."""
+    logs = [_wal_file(lcrc, synth, (8 + 6 * k) << 20, 0x5EED0040 + k) for k in range(4)]
+    exp = []
+    for data in logs:
+        want = _wal_expect(orc, data)
+        hh = np.array([x[0] for x in want], np.uint64)
+        ln = np.array([x[1] for x in want], np.uint64)
+        crc, _ = orc.crc_ranges_mt(bytes(data), hh + 6, ln + 1, 8, orc.ALGO_PCLMUL_REF)
+        exp.append((hh, ln, crc))
+    engs = [lcrc.Engine(0, lcrc.MODE_REF) for _ in logs]
+    bufs = []
+    try:
+        for eng, data in zip(engs, logs):
+            cap = len(data) // 7 + 1
+            eng.reserve(len(data))
+            bufs.append((lcrc.DeviceBuffer.from_host(np.frombuffer(bytes(data), np.uint8)),
+                         lcrc.DeviceBuffer(cap * lcrc.WAL_REC_DTYPE.itemsize), lcrc.DeviceBuffer(8), cap))
+        for _ in range(3):
+            for eng, data, (dev, rd, cnt, cap) in zip(engs, logs, bufs):
+                rd.zero()
+                eng.wal_scan_async(dev, len(data), rd, cap, cnt)
+            for eng in engs:
+                eng.sync()
+            for (dev, rd, cnt, cap), (hh, ln, crc) in zip(bufs, exp):
+                n = int(cnt.download(np.uint64, 1)[0])
+                assert n == len(hh)
+                got = rd.download(lcrc.WAL_REC_DTYPE, n)
+                assert np.array_equal(got["header"], hh) and np.array_equal(got["length"], ln.astype(np.uint32))
+                assert np.array_equal(got["crc"], crc) and (got["status"] == 0).all()
+    finally:
+        for eng in engs:
+            eng.close()
+
+
 def test_wal_just_past_64_parts_with_corruption(lcrc, orc, synth, engines):
     """A log of 4,161 blocks (65 header-walk parts, the last block partial) with corrupted payload bytes, a
     corrupted length field and a zeroed header: every record, crc and verdict against the oracle's walk."""

@@ -16,8 +16,6 @@ cat gpurun_out/bench_fixed.json
 for c in ${CONFIGS:-mixed wal table tablez}; do
   case "$c" in
     tablez) BC="--config table --compression 1" ;;
-    tablezv1) BC="--config table --compression 1 --engine-opt ts_open_v1=1" ;;
-    walop) BC="--config wal --engine-opt wal_onepass=1" ;;
     *) BC="--config $c" ;;
   esac
   timeout -k 10 300 python -u bench.py $BC > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || { tail -20 gpurun_out/bench_$c.err; exit 1; }

@@ -24,8 +24,6 @@ for c in $CONFIGS; do
   python3 -c "import json;s=json.load(open('profiles/${R}_${c}_c_summary.json'));print('$c profile:', s.get('kernel'), s.get('avg_us'), s.get('trace_launch_us'), 'agreement (profiled run)', s.get('agreement_profiled_run'))"
   case "$c" in
     tablez) BC="--config table --compression 1" ;;
-    tablezv1) BC="--config table --compression 1 --engine-opt ts_open_v1=1" ;;
-    walop) BC="--config wal --engine-opt wal_onepass=1" ;;
     *) BC="--config $c" ;;
   esac
   timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 $BC --extra-out "$OUT/bench_${c}_full.json" > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }

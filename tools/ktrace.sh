@@ -10,8 +10,6 @@ mkdir -p $O
 for c in "$@"; do
   case "$c" in
     tablez) BC="--config table --compression 1" ;;
-    tablezv1) BC="--config table --compression 1 --engine-opt ts_open_v1=1" ;;
-    walop) BC="--config wal --engine-opt wal_onepass=1" ;;
     *) BC="--config $c" ;;
   esac
   rm -rf $O/prof_$c

@@ -16,11 +16,9 @@ rm -rf "$OUT"
 mkdir -p "$OUT" profiles
 # the driver's command (bench.py --gpus 1 --steps 20 --warmup 5) for this config, without the CPU leg
 # tablez: the Snappy-compressed table (bench.py --config table --compression 1)
-# walop: the one-pass WAL scan (context option wal_onepass); tablezv1: the compressed table with the round-4 index decoder
+
 case "$CONFIG" in
   tablez) BCONF="--config table --compression 1" ;;
-  tablezv1) BCONF="--config table --compression 1 --engine-opt ts_open_v1=1" ;;
-  walop) BCONF="--config wal --engine-opt wal_onepass=1" ;;
   *) BCONF="--config $CONFIG" ;;
 esac
 BENCH="bench.py --gpus 1 $BCONF --mode $MODE --steps 20 --warmup 5 --no-cpu-baseline $EXTRA"

@@ -39,8 +39,8 @@ def stream_kernel(kernels):
     """(name, stats) of the step's byte-streaming kernel: the k_windows* launch, or the table scan's k_ts_windows (its
     window pass with the index walk beside it): every algorithmic byte passes through it once; a config without one
     (the Snappy frames) falls back to the kernel with the most time."""
-    win = [kv for kv in kernels.items() if kv[0].split("::")[-1].split("<")[0] in ("k_windows", "k_windows_wal",
-                                                                                   "k_windows_q", "k_ts_windows")]
+    win = [kv for kv in kernels.items() if kv[0].split("::")[-1].split("<")[0] in ("k_windows", "k_windows_q",
+                                                                                   "k_ts_windows")]
     if win:
         return max(win, key=lambda kv: kv[1]["total_ns"])
     return max(kernels.items(), key=lambda kv: kv[1]["total_ns"])
@@ -173,8 +173,20 @@ def main(outdir, rnd, config, mode, committed=None, unprofiled=None):
         t = traffic[hot]
         calls = {k: v["calls"] for k, v in summary["kernels"].items()}
         per_step = calls.get(dom) or 1
-        step_rd = sum(v["hbm_read_bytes_per_launch"] * calls.get(k, 1) / per_step for k, v in traffic.items())
-        step_wr = sum(v["hbm_write_bytes_per_launch"] * calls.get(k, 1) / per_step for k, v in traffic.items())
+        # every kernel's bytes per step: a kernel's average per launch x its launches per streaming-kernel launch
+        # (kernels named in the trace; the one-off launches of the set-up, e.g. the WAL bench's seal, are not steps)
+        stepk = {k: v for k, v in traffic.items() if k in calls and calls[k] >= per_step}
+        step_rd = sum(v["hbm_read_bytes_per_launch"] * calls[k] / per_step for k, v in stepk.items())
+        step_wr = sum(v["hbm_write_bytes_per_launch"] * calls[k] / per_step for k, v in stepk.items())
+        bpl = summary.get("bytes_per_launch")
+        summary["step_traffic"] = {
+            "read_bytes": step_rd, "write_bytes": step_wr, "kernels": sorted(stepk),
+            "read_x": round(step_rd / bpl, 4) if bpl else None, "write_x": round(step_wr / bpl, 4) if bpl else None,
+            "stream_kernel": hot, "stream_kernel_read_x": round(t["hbm_read_bytes_per_launch"] / bpl, 4) if bpl else None,
+            "note": "HBM bytes per step over every kernel of the step (FETCH_SIZE x1024 x2, WRITE_SIZE x1024), and "
+                    "their ratio to the algorithmic bytes of one step (bytes_per_launch)"}
+        with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
+            json.dump(summary, f, indent=1)
         with open(os.path.join(prof, f"traffic_{config}_{mode}.json"), "w") as f:
             json.dump({"kernel": hot, "hbm_bytes_per_launch": t["hbm_read_bytes_per_launch"] + t["hbm_write_bytes_per_launch"],
                        "hbm_read_bytes_per_launch": t["hbm_read_bytes_per_launch"],
