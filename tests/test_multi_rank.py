@@ -60,9 +60,10 @@ def test_bench_spawns_ranks(orc, synth, world):
     _check(orc, synth, _line(r.stdout), world, 3)
 
 
-def test_bench_under_torchrun(orc, synth):
-    """The driver's form: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N."""
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_under_torchrun(orc, synth, world):
+    """The driver's form: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N -- with N = 8 the
+    driver's SCALE run (configs[4]: 8 independent shards, no collective) rehearsed on gloo ranks."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(world), "--engine", "host", "--blocks", str(NBLK), "--steps", "2", "--warmup", "1"]

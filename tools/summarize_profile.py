@@ -174,8 +174,9 @@ def main(outdir, rnd, config, mode, committed=None, unprofiled=None):
         calls = {k: v["calls"] for k, v in summary["kernels"].items()}
         per_step = calls.get(dom) or 1
         # every kernel's bytes per step: a kernel's average per launch x its launches per streaming-kernel launch
-        # (kernels named in the trace; the one-off launches of the set-up, e.g. the WAL bench's seal, are not steps)
-        stepk = {k: v for k, v in traffic.items() if k in calls and calls[k] >= per_step}
+        # (kernels named in the trace with at least half as many launches; the one-off launches of the set-up, e.g.
+        # the WAL bench's seal, are not steps)
+        stepk = {k: v for k, v in traffic.items() if k in calls and 2 * calls[k] >= per_step}
         step_rd = sum(v["hbm_read_bytes_per_launch"] * calls[k] / per_step for k, v in stepk.items())
         step_wr = sum(v["hbm_write_bytes_per_launch"] * calls[k] / per_step for k, v in stepk.items())
         bpl = summary.get("bytes_per_launch")
