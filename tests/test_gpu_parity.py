@@ -365,6 +365,24 @@ def test_graph_replay_general_path_and_wal(lcrc, orc):
     eng.close()
 
 
+def test_ctx_options_reserved_refused(lcrc):
+    """lcrc_ctx_options.reserved[3] held the round-5 measurement variants (wal_onepass, ts_open_v1, ts_unfused),
+    removed in round 6: a non-zero word is refused with LCRC_EINVAL and a message; zero words create a context."""
+    import ctypes
+    for k in range(3):
+        o = lcrc._CtxOptions()
+        o.size = ctypes.sizeof(lcrc._CtxOptions)
+        o.reserved[k] = 1
+        ctx = ctypes.c_void_p()
+        assert lcrc.lib().lcrc_ctx_create_ex(ctypes.byref(ctx), 0, lcrc.MODE_C, 0, ctypes.byref(o)) == lcrc.EINVAL
+        assert not ctx.value and b"reserved" in lcrc.lib().lcrc_last_error()
+    o = lcrc._CtxOptions()
+    o.size = ctypes.sizeof(lcrc._CtxOptions)
+    ctx = ctypes.c_void_p()
+    assert lcrc.lib().lcrc_ctx_create_ex(ctypes.byref(ctx), 0, lcrc.MODE_C, 0, ctypes.byref(o)) == 0 and ctx.value
+    assert lcrc.lib().lcrc_ctx_destroy(ctx) == 0
+
+
 @pytest.mark.parametrize("path", ["ranges", "blocks"])
 def test_general_path_variants(lcrc, orc, path):
     """Both general-path kernels, forced through the context option `general` (lcrc_ctx_create_ex): k_ranges (one
