@@ -1811,25 +1811,39 @@ constexpr uint32_t SN_SLACK = 128;
 constexpr uint32_t SN_MAX = 16384;
 // k_ts_decode (the whole-table scan's decode): TD_WAVES waves per 256-block tile. Each wave decodes four frames at once,
 // one per 16-lane row. A row (TR_ROW bytes of LDS) decodes IN PLACE: the frame is staged at the row's end and the
-// chunk decoded from the row's start, the output growing towards the unread input (round 5: 5,136 B a row instead of
-// 7,856 with separate input and output areas -- six waves a CU instead of four, so two SIMDs hold two waves and hide
-// each other's LDS and dependency latency). A frame of over TR_IN bytes (the register staging), a chunk of over TR_OUT,
-// or one whose output would reach its own unread input goes through the whole-wave decoder afterwards, in the LDS of
-// two waves' rows (TD_IN + TD_OUT); a chunk too large for that, lane-serially to the workspace.
-constexpr uint32_t TD_WAVES = 6;
+// chunk decoded from the row's start, the output growing towards the unread input. Round 6: the chunk CRC masks the
+// bytes past the chunk's end instead of zero-filling the row to whole 1 KiB passes, so a row holds the chunk itself
+// (4,192 B against 5,136: a db_bench-style 4 KiB block decodes to ~4,125 B and needs at most 4,132 B of row with its
+// frame staged behind the output), and only the row path's CRC tables stay in LDS (24 KiB: T0..T3, Z64..Z1024; the
+// whole-wave decoder reads Z16 / Z32 from the table image in global memory): eight waves a CU, two per SIMD, where
+// round 5 fitted six. A frame of over TR_IN bytes (the register staging), a chunk of over TR_OUT, or one whose output
+// would reach its own unread input goes through the whole-wave decoder afterwards, in the LDS of two waves' rows
+// (TD_IN + TD_OUT); a chunk too large for that, lane-serially to the workspace.
+#ifndef LCRC_TD_WAVES
+#define LCRC_TD_WAVES 8  // (measurement builds: 6 with LCRC_TD_ROW 5136 is round 5's occupancy)
+#endif
+#ifndef LCRC_TD_ROW
+#define LCRC_TD_ROW 4192
+#endif
+constexpr uint32_t TD_WAVES = LCRC_TD_WAVES;
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
+// k_ts_decode's LDS table image (words): T0..T3, then Z64, Z128, Z256, Z512, Z1024
+constexpr uint32_t TDL_Z64 = 1024, TDL_Z128 = 2048, TDL_Z256 = 3072, TDL_Z512 = 4096, TDL_Z1024 = 5120;
+constexpr uint32_t TDL_WORDS = 6144;
+static_assert(TAB_SLICE == 0 && TAB_ZPIECE + 2 * 1024 + 5 * 1024 == TD_TAB_WORDS && TAB_ZWIN == TAB_ZPIECE + 4 * 1024,
+              "k_ts_decode's image: the slice tables, then the table image's Z64..Z1024 in order");
 // a row's frame (+ the slack of its element-header reads): frames up to 2,701 B (db_bench-style 4 KiB blocks: <= 2,298)
 constexpr uint32_t TR_IN = 2704 + 16;
-constexpr uint32_t TR_OUT = 5120;        // a row's decoded chunk, walked by the CRC in whole 1 KiB passes
-constexpr uint32_t TR_ROW = TR_OUT + 16;  // + 16 B of slack: header reads past the input, the dump dword
+constexpr uint32_t TR_ROW = LCRC_TD_ROW;  // the row's decoded chunk + 16 B of slack (header reads past the input,
+constexpr uint32_t TR_OUT = TR_ROW - 16;  // the dump dword)
 constexpr uint32_t TD_WAVE_LDS = 4 * TR_ROW;
 constexpr uint32_t TD_IN = 12288 + 16;   // the whole-wave decoder's staging: compressed bytes (+ 4 for the tail dword)
 constexpr uint32_t TD_OUT = 16384;       // decoded bytes (a multiple of 1 KiB: V fits as is)
 static_assert(TD_OUT % 1024 == 0, "the chunk CRC reads V in whole 1 KiB passes");
-static_assert(TR_OUT % 1024 == 0 && TR_ROW % 16 == 0 && TR_IN + 16 <= TR_ROW, "row staging");
+static_assert(TR_ROW % 16 == 0 && TR_IN + 16 <= TR_ROW && TR_OUT >= 4096, "row staging");
 static_assert(TD_WAVES % 2 == 0 && TD_IN + SN_SLACK + TD_OUT <= 2 * TD_WAVE_LDS,
               "the whole-wave decoder's staging is two waves' row areas");
-constexpr uint32_t TD_LDS = TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
+constexpr uint32_t TD_LDS = TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
 static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish");
 
 // `slow`: the decoded bytes (16-aligned) of the compressed chunks too large for k_ts_decode's LDS staging (TD_IN
@@ -3371,8 +3385,9 @@ __global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, u
 //
 // Chunk CRC (td_chunk_crc): the chunk M is read as V = 0^pad || M, |V| = 1024 np (leading zeros walked from register
 // 0 stay 0, so walk(0, V) = walk(0, M)); per 1 KiB pass each lane walks 16 B (slice-by-4), the 16-lane rows join with
-// Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- a 32 KiB table copy in LDS. The init register
-// is injected into the first min(4, |M|) bytes: walk(R, M) = walk(0, M ^ LE(R)) ^ (R >> 8 |M|) for |M| < 4.
+// Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- T0..T3 and Z64..Z1024 from k_ts_decode's LDS
+// image (TDL_*), Z16 / Z32 (used by this path only) from the table image in global memory. The init register is
+// injected into the first min(4, |M|) bytes: walk(R, M) = walk(0, M ^ LE(R)) ^ (R >> 8 |M|) for |M| < 4.
 // ---------------------------------------------------------------------------------------------------
 
 // the piece of pass k of lane `lane`: V[1024 k + 16 lane, +16), init injected into V[pad, pad + q)
@@ -3390,7 +3405,8 @@ __device__ __forceinline__ u32x4 td_inject(u32x4 w, uint32_t x0, uint32_t pad, u
 }
 
 template <bool FROM_LDS>
-__device__ uint32_t td_chunk_crc(const uint32_t* T, const uint8_t* src, uint32_t len, uint32_t lane) {
+__device__ uint32_t td_chunk_crc(const uint32_t* T, const uint32_t* __restrict__ G, const uint8_t* src, uint32_t len,
+                                 uint32_t lane) {
   const uint32_t np = (len + 1023) >> 10, pad = (np << 10) - len, q = len < 4 ? len : 4u;
   const uint32_t g = lane & 15;
   uint32_t acc = 0;
@@ -3416,21 +3432,22 @@ __device__ uint32_t td_chunk_crc(const uint32_t* T, const uint8_t* src, uint32_t
 #pragma unroll
     for (int m = 0; m < 4; ++m) {  // row tree: 16 pieces of 16 B -> one 256 B value in lane 0 of the row
       const uint32_t pn = row_down(cv, m);
-      if ((g & ((2u << m) - 1)) == 0) cv = zl(T, TAB_ZPIECE + m * 1024, cv) ^ pn;
+      if ((g & ((2u << m) - 1)) == 0)
+        cv = (m < 2 ? zl(G, TAB_ZPIECE + m * 1024, cv) : zl(T, m == 2 ? TDL_Z64 : TDL_Z128, cv)) ^ pn;
     }
     const uint32_t r0 = __builtin_amdgcn_readlane(cv, 0), r1 = __builtin_amdgcn_readlane(cv, 16);
     const uint32_t r2 = __builtin_amdgcn_readlane(cv, 32), r3 = __builtin_amdgcn_readlane(cv, 48);
-    const uint32_t a = zl(T, TAB_ZWIN, r0) ^ r1, b = zl(T, TAB_ZWIN, r2) ^ r3;
-    const uint32_t pass = zl(T, TAB_ZWIN + 1024, a) ^ b;
-    acc = k ? zl(T, TAB_ZWIN + 2048, acc) ^ pass : pass;
+    const uint32_t a = zl(T, TDL_Z256, r0) ^ r1, b = zl(T, TDL_Z256, r2) ^ r3;
+    const uint32_t pass = zl(T, TDL_Z512, a) ^ b;
+    acc = k ? zl(T, TDL_Z1024, acc) ^ pass : pass;
   }
   if (len < 4) acc ^= len ? 0xFFFFFFFFu >> (8 * len) : 0xFFFFFFFFu;
   return __builtin_amdgcn_readfirstlane(acc ^ 0xFFFFFFFFu);  // raw CRC-32C (xorout)
 }
 
 // frame f decoded chunk by chunk, every chunk's masked CRC-32C checked: true when the frame is good (format.rs:194-206)
-__device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint32_t* T, uint8_t* lin, uint8_t* lout,
-                         uint8_t* __restrict__ out, uint64_t o, uint32_t lane) {
+__device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint32_t* T, const uint32_t* __restrict__ G,
+                         uint8_t* lin, uint8_t* lout, uint8_t* __restrict__ out, uint64_t o, uint32_t lane) {
   sn_reader rd;
   rd.init(p, len, lane);
   const uint32_t end = rd.lim;
@@ -3448,7 +3465,7 @@ __device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint
     const uint32_t want = rd.le(body, 4);
     uint32_t crc;
     if (type == 1) {  // uncompressed: checksummed where it lies
-      crc = td_chunk_crc<false>(T, rd.a + body + 4, cl - 4, lane);
+      crc = td_chunk_crc<false>(T, G, rd.a + body + 4, cl - 4, lane);
     } else {
       uint32_t ulen = 0, q = body + 4, used = 0;  // preamble = uncompressed length (valid: k_ts_finish)
       snappy_preamble([&](uint32_t i) { return rd.byte(q + i); }, at - q, ulen, used);
@@ -3467,13 +3484,13 @@ __device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint
         ok = snappy_wave_decode(lin, d, d + (at - q), lout + pad, ulen, lane);
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
-        crc = ok ? td_chunk_crc<true>(T, lout, ulen, lane) : 0u;
+        crc = ok ? td_chunk_crc<true>(T, G, lout, ulen, lane) : 0u;
       } else {  // too large for the staging: lane-serial into this frame's workspace, checksummed there
         uint64_t oo = o;
         if (lane == 0) ok = sn_serial_decode(rd.a + q, rd.a + at, out, oo, o + ulen);
         ok = bcast(ok ? 1u : 0u) != 0;
         __threadfence_block();
-        crc = ok ? td_chunk_crc<false>(T, out + o, ulen, lane) : 0u;
+        crc = ok ? td_chunk_crc<false>(T, G, out + o, ulen, lane) : 0u;
         o += (ulen + 15) & ~15u;
       }
     }
@@ -3604,11 +3621,12 @@ __device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uin
   return res ? res : w == ulen ? 0u : 1u;
 }
 
-// The CRC-32C of M = V[0, len) per row, V = o[0, 1024 np) with V[len, 1024 np) zero (z = 1024 np - len bytes, undone
-// at the end by one GF(2) multiply with invz = x^(-8z)) and the init register already XORed into the first min(4, len)
-// bytes of M by the caller (the decoded bytes are not kept): per 1 KiB pass each lane walks 64 B (slice-by-4), the row
-// tree joins the lanes with Z64, Z128, Z256, Z512, and the passes chain with Z1024 -- a quarter of the passes (and of
-// their tree and broadcast) of 16 B per lane.
+// The CRC-32C of M = V[0, len) per row, walked as M || 0^z to whole 1 KiB passes (z = 1024 np - len, undone at the end
+// by one GF(2) multiply with invz = x^(-8z)), the init register already XORed into the first min(4, len) bytes of M by
+// the caller (the decoded bytes are not kept): per 1 KiB pass each lane walks 64 B (slice-by-4), the row tree joins
+// the lanes with Z64, Z128, Z256, Z512, and the passes chain with Z1024 -- a quarter of the passes (and of their tree
+// and broadcast) of 16 B per lane. The zeros are not in the row (round 6): a chunk's last pass masks the bytes at and
+// past len as it reads them (16 B reads end at most at len rounded up to 16, inside the row), so the row holds M only.
 __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, uint32_t len, bool active,
                                                   uint32_t g, uint32_t lane, uint32_t invz) {
   const uint32_t np = active ? (len + 1023) >> 10 : 0u;
@@ -3616,36 +3634,54 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
   for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
     const bool on = k < np;
     uint32_t cv = 0;
+    if (__builtin_amdgcn_ballot_w64(on && 1024 * (k + 1) > len)) {  // some row's last, partial pass
 #pragma unroll
-    for (int sp = 0; sp < 4; ++sp) {
-      const uint32_t x0 = 1024 * k + 64 * g + 16 * sp;
-      const u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
-      cv = step4(T, cv, w.x);
-      cv = step4(T, cv, w.y);
-      cv = step4(T, cv, w.z);
-      cv = step4(T, cv, w.w);
+      for (int sp = 0; sp < 4; ++sp) {
+        const uint32_t x0 = 1024 * k + 64 * g + 16 * sp;
+        u32x4 w = *(lds_cu32x4*)(V + (on && x0 < len ? x0 : 0u));
+        const int rem = (int)len - (int)x0;  // bytes of M from x0 on
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int rd = rem - 4 * d;
+          w[d] &= rd >= 4 ? ~0u : rd <= 0 ? 0u : (1u << (8 * rd)) - 1u;
+        }
+        cv = step4(T, cv, w.x);
+        cv = step4(T, cv, w.y);
+        cv = step4(T, cv, w.z);
+        cv = step4(T, cv, w.w);
+      }
+    } else {
+#pragma unroll
+      for (int sp = 0; sp < 4; ++sp) {
+        const uint32_t x0 = 1024 * k + 64 * g + 16 * sp;
+        const u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
+        cv = step4(T, cv, w.x);
+        cv = step4(T, cv, w.y);
+        cv = step4(T, cv, w.z);
+        cv = step4(T, cv, w.w);
+      }
     }
     // row tree over 64 B pieces: level m joins lane g with g + 2^m, shifting the left part by 64 * 2^m bytes
     {
       const uint32_t pn = row_down(cv, 0);
-      if ((g & 1) == 0) cv = zl(T, TAB_ZPIECE + 2 * 1024, cv) ^ pn;
+      if ((g & 1) == 0) cv = zl(T, TDL_Z64, cv) ^ pn;
     }
     {
       const uint32_t pn = row_down(cv, 1);
-      if ((g & 3) == 0) cv = zl(T, TAB_ZPIECE + 3 * 1024, cv) ^ pn;
+      if ((g & 3) == 0) cv = zl(T, TDL_Z128, cv) ^ pn;
     }
     {
       const uint32_t pn = row_down(cv, 2);
-      if ((g & 7) == 0) cv = zl(T, TAB_ZWIN, cv) ^ pn;
+      if ((g & 7) == 0) cv = zl(T, TDL_Z256, cv) ^ pn;
     }
     {
       const uint32_t pn = row_down(cv, 3);
-      if ((g & 15) == 0) cv = zl(T, TAB_ZWIN + 1024, cv) ^ pn;
+      if ((g & 15) == 0) cv = zl(T, TDL_Z512, cv) ^ pn;
     }
     const uint32_t pass = row_bcast0(cv, lane);
-    if (on) acc = k ? zl(T, TAB_ZWIN + 2048, acc) ^ pass : pass;
+    if (on) acc = k ? zl(T, TDL_Z1024, acc) ^ pass : pass;
   }
-  // M sits at V's start and zeros follow it to the pass end: walk(M || 0^z) = Z_z(walk(M)), undone by x^(-8z)
+  // walk(M || 0^z) = Z_z(walk(M)), undone by x^(-8z)
   if (__builtin_amdgcn_ballot_w64(active && (len & 1023) != 0)) acc = (len & 1023) ? gf_mul(invz, acc, 0x82F63B78u) : acc;
   if (len < 4) acc ^= len ? 0xFFFFFFFFu >> (8 * len) : 0xFFFFFFFFu;
   return acc ^ 0xFFFFFFFFu;
@@ -3686,8 +3722,8 @@ __device__ __forceinline__ void row_stage_store(const RowStage& s, lds_u8* dst, 
 
 // One frame per row (`elig` rows only), staged by the caller at B[ib + d, ib + d + len) (row_stage_load / _store), its
 // chunks walked there, each data chunk decoded in place (or, uncompressed, copied forward) to B[0, ulen) and
-// checksummed. Returns 0 good, 1 bad, 2 deferred to the whole-wave decoder (a chunk over TR_OUT, an in-place decode
-// that would reach unread input, or a chunk's CRC zeros that would reach a later chunk's input).
+// checksummed. Returns 0 good, 1 bad, 2 deferred to the whole-wave decoder (a chunk over TR_OUT, or an in-place decode
+// that would reach unread input).
 __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool elig, const uint32_t* T, lds_u8* B,
                                               uint32_t ib, uint32_t g, uint32_t lane, const uint32_t* __restrict__ inv) {
   lds_u8* const in = B + ib;
@@ -3718,9 +3754,7 @@ __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool eli
         snappy_preamble([&](uint32_t i) { return (uint32_t)in[q + i]; }, next - q, ulen, used);
         q += used;
       }
-      const uint32_t vend = (ulen + 1023) & ~1023u;
-      // too large for the row, or the CRC's zeros after M would overwrite a later chunk's input: the whole wave
-      if (ulen > TR_OUT || (next < end && vend > ib + next)) {
+      if (ulen > TR_OUT) {  // too large for the row: the whole wave
         res = 2;
         have = false;
       }
@@ -3737,10 +3771,7 @@ __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool eli
       res = 2;  // given up in place: the whole wave decodes the frame from the file
       have = false;
     }
-    // V[ulen, 1024 np) zeroed (input bytes already consumed), then the init register injected into M's first bytes
-    const uint32_t u4 = (ulen + 3) & ~3u;
-    for (uint32_t x = ulen + g; x < (have ? u4 : 0u); x += 16) B[x] = 0;
-    for (uint32_t x = u4 + 4 * g; x < (have ? ulen + z : 0u); x += 64) *(__attribute__((address_space(3))) uint32_t*)(B + x) = 0;
+    // the init register injected into M's first bytes (the CRC masks the bytes past M: nothing is zeroed)
     if (have && g < (ulen < 4 ? ulen : 4u)) B[g] ^= 0xFFu;
     const uint32_t crc = row_chunk_crc(T, B, ulen, have, g, lane, invz);
     if (have) {
@@ -3771,7 +3802,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     off_j = blk[j].offset;
     off_p = j ? blk[j - 1].offset : 0;
   }
-  uint8_t* const bad = td_lds + TD_TAB_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // 256 tile flags + the meta blocks
+  uint8_t* const bad = td_lds + TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // 256 tile flags + the meta blocks
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
   // the block count from fields ts_final leaves alone (it may shrink n_total while later workgroups start)
   const bool live = st->status == TS_OK && !st->idx_only;
@@ -3825,26 +3856,36 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   TD_STAMP(3);
   const bool dec = !over && chunks;
   for (uint32_t i = threadIdx.x; i < 256 + 16; i += blockDim.x) bad[i] = 0;
-  if (dec)
-    for (uint32_t i = threadIdx.x; i < TD_TAB_WORDS / 4; i += blockDim.x) ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i];
+  if (dec)  // the LDS image (TDL_*): the table image's T0..T3, then its Z64..Z1024
+    for (uint32_t i = threadIdx.x; i < TDL_WORDS / 4; i += blockDim.x)
+      ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i < 256 ? i : i + (TAB_ZPIECE + 2 * 1024 - TDL_Z64) / 4];
   __syncthreads();
   if (dec) {
     // this tile's frames (the meta blocks excluded): four per wave at a time, one per row, over a static share of
-    // the tile's 64 groups of four -- waves 2 and 3 take 12, the others 10: the hardware puts a workgroup's waves on
-    // the SIMDs in order, so waves 0/4 and 1/5 share a SIMD (issue rate ~1.6x one wave's, measured with rows of
-    // fewer frames) and 2 and 3 have one each. A frame the row cannot decode (bad[] = 2) then through the whole wave,
-    // in two waves' row areas; then the last workgroup's wave 0 the meta blocks.
+    // the tile's 64 groups of four -- eight each with eight waves, two a SIMD (round 5's six waves: waves 2 and 3 took
+    // 12, the others 10: the hardware puts a workgroup's waves on the SIMDs in order, so waves 0/4 and 1/5 shared a
+    // SIMD and 2 and 3 had one each). A frame the row cannot decode (bad[] = 2) then through the whole wave, in two
+    // waves' row areas; then the last workgroup's wave 0 the meta blocks.
     const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
     const uint32_t r = lane >> 4, g = lane & 15;
 #ifndef LCRC_TD_SPLIT
+#if LCRC_TD_WAVES == 8
+#define LCRC_TD_SPLIT 8, 8, 8, 8, 8, 8, 8, 8
+#else
 #define LCRC_TD_SPLIT 10, 10, 12, 12, 10, 10  // (a probe build may try another share)
 #endif
+#endif
     constexpr uint32_t gsplit[TD_WAVES] = {LCRC_TD_SPLIT};
+    static_assert([] {
+      uint32_t sum = 0;
+      for (uint32_t i = 0; i < TD_WAVES; ++i) sum += gsplit[i];
+      return sum == 64;
+    }(), "the waves' shares cover the tile's 64 groups of four frames");
     uint32_t gbeg = 0;
 #pragma unroll
     for (uint32_t i = 0; i < TD_WAVES; ++i) gbeg += i < wv ? gsplit[i] : 0u;
     const uint32_t gcnt = gsplit[wv];
-    lds_u8* const rb = (lds_u8*)(td_lds + TD_TAB_WORDS * 4 + wv * TD_WAVE_LDS + r * TR_ROW);
+    lds_u8* const rb = (lds_u8*)(td_lds + TDL_WORDS * 4 + wv * TD_WAVE_LDS + r * TR_ROW);
     const uint32_t* const inv = tab_c + TAB_INV;
     // the wave's frames lo + 4 (gbeg + k) + r (k < gcnt): their descriptors loaded at once, lane 4 k + r holding frame
     // k's of row r; each group's frames staged through registers one group ahead (RowStage)
@@ -3897,12 +3938,12 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   __syncthreads();  // every row done: the whole-wave decoder takes two waves' row areas
   if (dec) {
     const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
-    uint8_t* const lin = td_lds + TD_TAB_WORDS * 4 + (wv & ~1u) * TD_WAVE_LDS;
+    uint8_t* const lin = td_lds + TDL_WORDS * 4 + (wv & ~1u) * TD_WAVE_LDS;
     uint8_t* const lout = lin + TD_IN + SN_SLACK;
     if ((wv & 1) == 0)
       for (uint64_t f = lo + wv / 2; f < hi; f += TD_WAVES / 2)
         if (bad[f - lo] == 2) {
-          const bool ok = td_frame(file + frames[f].offset, frames[f].length, T, lin, lout, out, out_off[f] + before, lane);
+          const bool ok = td_frame(file + frames[f].offset, frames[f].length, T, tab_c, lin, lout, out, out_off[f] + before, lane);
           __builtin_amdgcn_s_waitcnt(0);
           __builtin_amdgcn_wave_barrier();
           if (lane == 0) bad[f - lo] = ok ? 0 : 1;
@@ -3919,7 +3960,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
           base_o = xb;
         }
         if (frames[f].length && !fstatus[f] &&
-            !td_frame(file + frames[f].offset, frames[f].length, T, lin, lout, out, out_off[f] + base_o, lane) &&
+            !td_frame(file + frames[f].offset, frames[f].length, T, tab_c, lin, lout, out, out_off[f] + base_o, lane) &&
             lane == 0)
           bad[256 + (f - tail)] = 1;
       }
