@@ -1809,40 +1809,51 @@ constexpr uint32_t SN_MAX_CHUNK = 76490;
 // bytes, each at most SN_MAX (k_snappy_decode_wave sizes them from the batch's largest chunk)
 constexpr uint32_t SN_SLACK = 128;
 constexpr uint32_t SN_MAX = 16384;
-// k_ts_decode (the whole-table scan's decode): TD_WAVES waves per 256-block tile. Each wave decodes four frames at once,
-// one per 16-lane row. A row (TR_ROW bytes of LDS) decodes IN PLACE: the frame is staged at the row's end and the
-// chunk decoded from the row's start, the output growing towards the unread input. Round 6: the chunk CRC masks the
-// bytes past the chunk's end instead of zero-filling the row to whole 1 KiB passes, so a row holds the chunk itself
-// (4,192 B against 5,136: a db_bench-style 4 KiB block decodes to ~4,125 B and needs at most 4,132 B of row with its
-// frame staged behind the output), and only the row path's CRC tables stay in LDS (24 KiB: T0..T3, Z64..Z1024; the
-// whole-wave decoder reads Z16 / Z32 from the table image in global memory): eight waves a CU, two per SIMD, where
-// round 5 fitted six. A frame of over TR_IN bytes (the register staging), a chunk of over TR_OUT, or one whose output
-// would reach its own unread input goes through the whole-wave decoder afterwards, in the LDS of two waves' rows
-// (TD_IN + TD_OUT); a chunk too large for that, lane-serially to the workspace.
-#ifndef LCRC_TD_WAVES
-#define LCRC_TD_WAVES 8  // (measurement builds: 6 with LCRC_TD_ROW 5136 is round 5's occupancy)
+// k_ts_decode (the whole-table scan's decode): TD_WAVES waves per 256-block tile. Each wave decodes 64 / TD_RL frames
+// at once, one per TD_RL-lane row. A row (TR_ROW bytes of LDS) decodes IN PLACE: the frame is staged at the row's end
+// and the chunk decoded from the row's start, the output growing towards the unread input. Round 6: the chunk CRC
+// masks the bytes past the chunk's end instead of zero-filling the row to whole 1 KiB passes, so a row holds the chunk
+// itself (a db_bench-style 4 KiB block decodes to ~4,125 B and needs at most 4,132 B of row with its frame staged
+// behind the output), and only the row path's CRC tables stay in LDS; and rows are 8 lanes, not 16: a Snappy element
+// of the bench's blocks is 39 B on average (41 literals of ~50 B and 65 copies a 4 KiB block), so a 16-lane row moved
+// it with half its lanes idle while the element loop's ~110 instructions served four frames. With eight frames a wave
+// the loop's instructions per frame halve; LDS (32 rows a CU) then holds four waves, one a SIMD. A frame of over TR_IN
+// bytes (the register staging), a chunk of over TR_OUT, or one whose output would reach its own unread input goes
+// through the whole-wave decoder afterwards, in its wave's row area (TD_IN + TD_OUT); a chunk too large for that,
+// lane-serially to the workspace.
+#ifndef LCRC_TD_RL
+#define LCRC_TD_RL 8  // lanes a row (measurement builds: 16, with eight waves of four rows)
 #endif
-#ifndef LCRC_TD_ROW
-#define LCRC_TD_ROW 4192
-#endif
-constexpr uint32_t TD_WAVES = LCRC_TD_WAVES;
+constexpr uint32_t TD_RL = LCRC_TD_RL;
+static_assert(TD_RL == 8 || TD_RL == 16, "rows of 8 or 16 lanes");
+constexpr uint32_t TD_RPW = 64 / TD_RL;     // rows (frames in flight) a wave
+constexpr uint32_t TD_PASS = 8 * TD_RL;     // bytes a row moves per pass (8 a lane)
+constexpr uint32_t TD_WAVES = 32 / TD_RPW;  // 32 rows a workgroup (one a CU: the LDS)
 constexpr uint32_t TD_TAB_WORDS = TAB_ZWIN + 3 * 1024;  // T0..T3, Z16..Z128, Z256, Z512, Z1024 (at their TAB_* offsets)
-// k_ts_decode's LDS table image (words): T0..T3, then Z64, Z128, Z256, Z512, Z1024
-constexpr uint32_t TDL_Z64 = 1024, TDL_Z128 = 2048, TDL_Z256 = 3072, TDL_Z512 = 4096, TDL_Z1024 = 5120;
-constexpr uint32_t TDL_WORDS = 6144;
-static_assert(TAB_SLICE == 0 && TAB_ZPIECE + 2 * 1024 + 5 * 1024 == TD_TAB_WORDS && TAB_ZWIN == TAB_ZPIECE + 4 * 1024,
-              "k_ts_decode's image: the slice tables, then the table image's Z64..Z1024 in order");
+// k_ts_decode's LDS table image (words): T0..T3, then the table image's Z_(1024 / TD_RL) .. Z1024 (the row tree's
+// joins of lane pieces of 1024 / TD_RL bytes, Z1024 chaining the passes); the shorter shifts stay in global memory
+constexpr uint32_t TDL_ZSRC = TD_RL == 16 ? TAB_ZPIECE + 2 * 1024 : TAB_ZPIECE + 3 * 1024;  // Z64 or Z128
+constexpr uint32_t TDL_Z64 = 1024;  // (TD_RL = 16 only)
+constexpr uint32_t TDL_Z128 = 1024 + (TAB_ZPIECE + 3 * 1024 - TDL_ZSRC), TDL_Z256 = TDL_Z128 + 1024;
+constexpr uint32_t TDL_Z512 = TDL_Z256 + 1024, TDL_Z1024 = TDL_Z512 + 1024, TDL_WORDS = TDL_Z1024 + 1024;
+static_assert(TAB_SLICE == 0 && TAB_ZWIN == TAB_ZPIECE + 4 * 1024 && TD_TAB_WORDS == TAB_ZWIN + 3 * 1024,
+              "k_ts_decode's image: the slice tables, then the table image's Z64 or Z128 .. Z1024 in order");
 // a row's frame (+ the slack of its element-header reads): frames up to 2,701 B (db_bench-style 4 KiB blocks: <= 2,298)
 constexpr uint32_t TR_IN = 2704 + 16;
+#ifndef LCRC_TD_ROW
+#define LCRC_TD_ROW (LCRC_TD_RL == 8 ? 4320 : 4192)
+#endif
 constexpr uint32_t TR_ROW = LCRC_TD_ROW;  // the row's decoded chunk + 16 B of slack (header reads past the input,
 constexpr uint32_t TR_OUT = TR_ROW - 16;  // the dump dword)
-constexpr uint32_t TD_WAVE_LDS = 4 * TR_ROW;
+constexpr uint32_t TD_WAVE_LDS = TD_RPW * TR_ROW;
 constexpr uint32_t TD_IN = 12288 + 16;   // the whole-wave decoder's staging: compressed bytes (+ 4 for the tail dword)
 constexpr uint32_t TD_OUT = 16384;       // decoded bytes (a multiple of 1 KiB: V fits as is)
 static_assert(TD_OUT % 1024 == 0, "the chunk CRC reads V in whole 1 KiB passes");
 static_assert(TR_ROW % 16 == 0 && TR_IN + 16 <= TR_ROW && TR_OUT >= 4096, "row staging");
-static_assert(TD_WAVES % 2 == 0 && TD_IN + SN_SLACK + TD_OUT <= 2 * TD_WAVE_LDS,
-              "the whole-wave decoder's staging is two waves' row areas");
+// the whole-wave decoder's staging: one wave's row area, or two (TD_WW waves then share one decoder)
+constexpr uint32_t TD_WW = TD_IN + SN_SLACK + TD_OUT <= TD_WAVE_LDS ? 1 : 2;
+static_assert(TD_WAVES % TD_WW == 0 && TD_IN + SN_SLACK + TD_OUT <= TD_WW * TD_WAVE_LDS,
+              "the whole-wave decoder's staging is one or two waves' row areas");
 constexpr uint32_t TD_LDS = TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
 static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish");
 
@@ -3385,8 +3396,8 @@ __global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, u
 //
 // Chunk CRC (td_chunk_crc): the chunk M is read as V = 0^pad || M, |V| = 1024 np (leading zeros walked from register
 // 0 stay 0, so walk(0, V) = walk(0, M)); per 1 KiB pass each lane walks 16 B (slice-by-4), the 16-lane rows join with
-// Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- T0..T3 and Z64..Z1024 from k_ts_decode's LDS
-// image (TDL_*), Z16 / Z32 (used by this path only) from the table image in global memory. The init register is
+// Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- T0..T3 and Z64 or Z128 .. Z1024 from
+// k_ts_decode's LDS image (TDL_*), the shorter shifts (used by this path only) from the table image in global memory. The init register is
 // injected into the first min(4, |M|) bytes: walk(R, M) = walk(0, M ^ LE(R)) ^ (R >> 8 |M|) for |M| < 4.
 // ---------------------------------------------------------------------------------------------------
 
@@ -3433,7 +3444,8 @@ __device__ uint32_t td_chunk_crc(const uint32_t* T, const uint32_t* __restrict__
     for (int m = 0; m < 4; ++m) {  // row tree: 16 pieces of 16 B -> one 256 B value in lane 0 of the row
       const uint32_t pn = row_down(cv, m);
       if ((g & ((2u << m) - 1)) == 0)
-        cv = (m < 2 ? zl(G, TAB_ZPIECE + m * 1024, cv) : zl(T, m == 2 ? TDL_Z64 : TDL_Z128, cv)) ^ pn;
+        cv = (m == 3 ? zl(T, TDL_Z128, cv) : m == 2 && TD_RL == 16 ? zl(T, TDL_Z64, cv)
+                                                                  : zl(G, TAB_ZPIECE + m * 1024, cv)) ^ pn;
     }
     const uint32_t r0 = __builtin_amdgcn_readlane(cv, 0), r1 = __builtin_amdgcn_readlane(cv, 16);
     const uint32_t r2 = __builtin_amdgcn_readlane(cv, 32), r3 = __builtin_amdgcn_readlane(cv, 48);
@@ -3499,7 +3511,7 @@ __device__ bool td_frame(const uint8_t* __restrict__ p, uint32_t len, const uint
   return ok;
 }
 
-// ---- four frames per wave: one per 16-lane row (lane g = lane & 15 of row lane >> 4) ----
+// ---- 64 / TD_RL frames per wave: one per TD_RL-lane row (lane g = lane % TD_RL of row lane / TD_RL) ----
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 
@@ -3508,28 +3520,45 @@ typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 __device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
 
 // An element's bytes moved within a row's staging: m bytes to D from S = Sl (a literal, the input) or D - off (a copy,
-// earlier output); the pass layout and the repeat as row_snappy_decode describes.
-__device__ __forceinline__ void row_move(lds_u8* B, uint32_t D, uint32_t Sl, uint32_t m, uint32_t off, bool lit,
-                                         uint32_t gmask, uint32_t g, uint32_t dump) {
+// earlier output); the pass layout and the repeat as row_snappy_decode describes. Two halves: the loads of pass 0
+// (row_move_load, issued as soon as the element's header is decoded) and the rest (row_move_store, once the element is
+// validated: m = 0 for an element that is not moved).
+struct RowMoveLd {
+  uint32_t S, old, d0, d1, d2;
+};
+__device__ __forceinline__ RowMoveLd row_move_load(const lds_u8* B, uint32_t D, uint32_t Sl, uint32_t off, bool lit,
+                                                   uint32_t g) {
+  RowMoveLd l;
+  l.S = sel(lit, Sl, D - min(off, D));  // (an offset past the output is refused later: clamped, the reads stay in the row)
+  const uint32_t Da = D & ~3u, sh = D & 3u;
+  l.old = *(lds_cu32*)(B + Da);
+  const uint32_t A = (l.S + 8 * g - sh) & ~3u;
+  l.d0 = *(lds_cu32*)(B + A);
+  l.d1 = *(lds_cu32*)(B + A + 4);
+  l.d2 = *(lds_cu32*)(B + A + 8);
+  return l;
+}
+__device__ __forceinline__ void row_move_store(lds_u8* B, const RowMoveLd& l, uint32_t D, uint32_t m, uint32_t off,
+                                               bool lit, uint32_t gmask, uint32_t g, uint32_t dump) {
   typedef __attribute__((address_space(3))) uint32_t lds_w32;
-  const uint32_t S = sel(lit, Sl, D - off);
+  const uint32_t S = l.S;
   const bool pat = !lit & (off < m) & (off < 128);
   const uint32_t mm = sel(pat, 0u, m), Da = D & ~3u, sh = D & 3u;
-  const uint32_t old = *(lds_cu32*)(B + Da);
   // pass 0 (every row; a row with nothing to move -- finished, inactive, or a repeat, which goes bytewise below --
   // writes nothing: its first lane's merged dword would carry garbage past D into bytes the row's uncompressed-chunk
   // copy has written)
   const int r0 = (int)(8 * g) - (int)sh;  // element-relative offset of the lane's first dword
-  const uint32_t sa = S + (uint32_t)r0, A = sa & ~3u, al = sa & 3u;
-  const uint32_t d0 = *(lds_cu32*)(B + A), d1 = *(lds_cu32*)(B + A + 4), d2 = *(lds_cu32*)(B + A + 8);
+  const uint32_t al = (S + (uint32_t)r0) & 3u;
   const uint32_t keep = ((1u << (8 * sh)) - 1) & gmask;  // (sh = 0: nothing kept)
-  const uint32_t v0 = (__builtin_amdgcn_alignbyte(d1, d0, al) & ~keep) | (old & keep);
-  const uint32_t v1 = __builtin_amdgcn_alignbyte(d2, d1, al);
+  const uint32_t v0 = (__builtin_amdgcn_alignbyte(l.d1, l.d0, al) & ~keep) | (l.old & keep);
+  const uint32_t v1 = __builtin_amdgcn_alignbyte(l.d2, l.d1, al);
   const uint32_t a0 = Da + 8 * g;
   *(lds_w32*)(B + sel((mm != 0) & (r0 < (int)mm), a0, dump)) = v0;
   *(lds_w32*)(B + sel(r0 + 4 < (int)mm, a0 + 4, dump)) = v1;
-  if (__builtin_amdgcn_ballot_w64(sh + mm > 128)) {  // literals longer than a pass (copies: at most 64 B)
-    for (uint32_t b = 128; __builtin_amdgcn_ballot_w64(b < sh + mm); b += 128) {
+  // elements longer than a pass: literals (and with 8-lane rows copies of over 61 B; a copy that is not a repeat
+  // reads only output written before it)
+  if (__builtin_amdgcn_ballot_w64(sh + mm > TD_PASS)) {
+    for (uint32_t b = TD_PASS; __builtin_amdgcn_ballot_w64(b < sh + mm); b += TD_PASS) {
       const int r = (int)(b + 8 * g) - (int)sh;
       const uint32_t sb = S + (uint32_t)r, Ab = sb & ~3u, ab = sb & 3u;
       const uint32_t e0 = *(lds_cu32*)(B + Ab), e1 = *(lds_cu32*)(B + Ab + 4), e2 = *(lds_cu32*)(B + Ab + 8);
@@ -3537,16 +3566,17 @@ __device__ __forceinline__ void row_move(lds_u8* B, uint32_t D, uint32_t Sl, uin
       *(lds_w32*)(B + sel(r + 4 < (int)mm, Da + b + 8 * g + 4, dump)) = __builtin_amdgcn_alignbyte(e2, e1, ab);
     }
   }
-  if (__builtin_amdgcn_ballot_w64(pat)) {  // (pat: a copy, m <= 64)
-    uint32_t v[4];
+  if (__builtin_amdgcn_ballot_w64(pat)) {  // (pat: a copy, m <= 64: 64 / TD_RL bytes a lane)
+    constexpr int PB = 64 / TD_RL;
+    uint32_t v[PB];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t j = 4 * g + k;
+    for (int k = 0; k < PB; ++k) {
+      const uint32_t j = PB * g + k;
       v[k] = pat ? B[S + small_mod(j, off)] : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t j = 4 * g + k;
+    for (int k = 0; k < PB; ++k) {
+      const uint32_t j = PB * g + k;
       B[pat && j < m ? D + j : dump] = (uint8_t)v[k];
     }
   }
@@ -3556,7 +3586,7 @@ __device__ __forceinline__ void row_move(lds_u8* B, uint32_t D, uint32_t Sl, uin
 // its base). Every row walks its own chain -- one element per iteration, its header two dwords of the row's staging
 // read one element ahead (its position is known once the previous header is decoded; the input is never written) --
 // and decodes the header without branches (selects only: the round-4 decoder's divergent if/else cost more SALU exec
-// juggling than VALU work). An element is moved in destination-aligned dwords, 8 B per lane and 128 B per row pass:
+// juggling than VALU work). An element is moved in destination-aligned dwords, 8 B per lane and TD_PASS per row pass:
 // each lane reads the three aligned dwords holding its 8 source bytes and funnel-shifts them (v_alignbyte); the row's
 // first dword keeps the bytes before the element from the dword already there; the bytes a row's last dword writes
 // past the element are overwritten by the next element's (in order: a wave's LDS operations execute in issue order),
@@ -3600,20 +3630,26 @@ __device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uin
     const uint32_t off = sel(c1, o1, sel(c2, o2, ext));
     const uint32_t hdr = sel(lit, 1 + nb, (0x5320u >> (4 * typ)) & 0xFu);  // 1 + nb | 2 | 3 | 5
     const uint32_t n = sel(lit, lm1 + 1, sel(c1, 4 + (L & 7), L + 1));
+    const uint32_t qn0 = q + hdr + sel(lit, n, 0u);
+    // the next header and the element's pass-0 source read before the element's verdict is known (a row whose element
+    // fails stops: what it read is never used), so their LDS round trip runs beside the validation; min: qn0 <= qe,
+    // the 8 bytes from qe & ~3 lie in the row's input staging and its slack
+    const uint32_t qh = q + hdr;
+    fetch(min(qn0, qe));
+    const RowMoveLd ld = row_move_load(B, OB + w, qh, off, lit, g);
+    __builtin_amdgcn_sched_barrier(0);  // (the scheduler would otherwise sink the loads below the validation)
     const bool good = (room >= hdr) & (!lit | ((lm1 < room - hdr) & ((nb == 0) | (room >= 5))));
     // (w <= ulen holds; off - 1 >= w: a copy's offset 0 or past the output)
     const bool bad = live & (!good | (n > ulen - w) | (!lit & (off - 1u >= w)));
     // in place (output and input in one row area, the output from its start): every dword this element writes lies
     // before the input not yet read -- from the next element on (its header is read before these writes), and for a
     // literal longer than a pass, before its own bytes' later passes. Else the row gives the frame up (spill)
-    const uint32_t qn0 = q + hdr + sel(lit, n, 0u);
-    const bool sp = live & !bad & ((((OB + w + n + 3) & ~3u) > qn0) | (lit & (OB + w + 8 > q + hdr)));
+    const bool sp = live & !bad & ((((OB + w + n + 3) & ~3u) > qn0) | (lit & (OB + w + 8 > qh)));
     res = sel(bad, 1u, sel(sp, 2u, res));
     const bool ex = live & !bad & !sp;
     const uint32_t m = sel(ex, n, 0u);
     const uint32_t qn = sel(ex, qn0, q);
-    fetch(qn);  // (qn <= qe: the 8 bytes from qe & ~3 lie in the row's input staging and its slack)
-    row_move(B, OB + w, q + hdr, m, off, lit, gmask, g, dump);
+    row_move_store(B, ld, OB + w, m, off, lit, gmask, g, dump);
     q = qn;
     w += m;
     livef = sel(ex & (qn < qe), 1u, 0u);
@@ -3621,14 +3657,23 @@ __device__ __forceinline__ uint32_t row_snappy_decode(lds_u8* B, uint32_t q, uin
   return res ? res : w == ulen ? 0u : 1u;
 }
 
+// every lane of a k_ts_decode row <- the row's first lane (8-lane rows: ds_swizzle in bit-mask mode, source lane
+// = lane & 0x18 within each 32)
+__device__ __forceinline__ uint32_t td_row_bcast0(uint32_t v, uint32_t lane) {
+  if constexpr (TD_RL == 16) return row_bcast0(v, lane);
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18);
+}
+
 // The CRC-32C of M = V[0, len) per row, walked as M || 0^z to whole 1 KiB passes (z = 1024 np - len, undone at the end
 // by one GF(2) multiply with invz = x^(-8z)), the init register already XORed into the first min(4, len) bytes of M by
-// the caller (the decoded bytes are not kept): per 1 KiB pass each lane walks 64 B (slice-by-4), the row tree joins
-// the lanes with Z64, Z128, Z256, Z512, and the passes chain with Z1024 -- a quarter of the passes (and of their tree
-// and broadcast) of 16 B per lane. The zeros are not in the row (round 6): a chunk's last pass masks the bytes at and
-// past len as it reads them (16 B reads end at most at len rounded up to 16, inside the row), so the row holds M only.
+// the caller (the decoded bytes are not kept): per 1 KiB pass each lane walks 1024 / TD_RL B (slice-by-4), the row tree joins
+// the lanes with Z64, Z128, Z256, Z512 (8-lane rows: 128 B a lane, Z128 .. Z512), and the passes chain with Z1024 -- a
+// quarter of the passes (and of their tree and broadcast) of 16 B per lane. The zeros are not in the row (round 6): a
+// chunk's last pass masks the bytes at and past len as it reads them (16 B reads end at most at len rounded up to 16,
+// inside the row), so the row holds M only.
 __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, uint32_t len, bool active,
                                                   uint32_t g, uint32_t lane, uint32_t invz) {
+  constexpr uint32_t LB = 1024 / TD_RL, SP = LB / 16;  // bytes a lane walks per pass, in 16 B pieces
   const uint32_t np = active ? (len + 1023) >> 10 : 0u;
   uint32_t acc = 0;
   for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
@@ -3636,8 +3681,8 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
     uint32_t cv = 0;
     if (__builtin_amdgcn_ballot_w64(on && 1024 * (k + 1) > len)) {  // some row's last, partial pass
 #pragma unroll
-      for (int sp = 0; sp < 4; ++sp) {
-        const uint32_t x0 = 1024 * k + 64 * g + 16 * sp;
+      for (uint32_t sp = 0; sp < SP; ++sp) {
+        const uint32_t x0 = 1024 * k + LB * g + 16 * sp;
         u32x4 w = *(lds_cu32x4*)(V + (on && x0 < len ? x0 : 0u));
         const int rem = (int)len - (int)x0;  // bytes of M from x0 on
 #pragma unroll
@@ -3652,8 +3697,8 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
       }
     } else {
 #pragma unroll
-      for (int sp = 0; sp < 4; ++sp) {
-        const uint32_t x0 = 1024 * k + 64 * g + 16 * sp;
+      for (uint32_t sp = 0; sp < SP; ++sp) {
+        const uint32_t x0 = 1024 * k + LB * g + 16 * sp;
         const u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
         cv = step4(T, cv, w.x);
         cv = step4(T, cv, w.y);
@@ -3661,24 +3706,16 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
         cv = step4(T, cv, w.w);
       }
     }
-    // row tree over 64 B pieces: level m joins lane g with g + 2^m, shifting the left part by 64 * 2^m bytes
-    {
-      const uint32_t pn = row_down(cv, 0);
-      if ((g & 1) == 0) cv = zl(T, TDL_Z64, cv) ^ pn;
+    // row tree over LB-byte pieces: level m joins lane g with g + 2^m, shifting the left part by LB * 2^m bytes
+    // (Z64 .. Z512 for 16 lanes, Z128 .. Z512 for 8)
+#pragma unroll
+    for (int m = 0; (1u << m) < TD_RL; ++m) {
+      const uint32_t pn = row_down(cv, m);
+      const int zt = TD_RL == 16 ? (m == 0 ? TDL_Z64 : m == 1 ? TDL_Z128 : m == 2 ? TDL_Z256 : TDL_Z512)
+                                 : (m == 0 ? TDL_Z128 : m == 1 ? TDL_Z256 : TDL_Z512);
+      if ((g & ((2u << m) - 1)) == 0) cv = zl(T, zt, cv) ^ pn;
     }
-    {
-      const uint32_t pn = row_down(cv, 1);
-      if ((g & 3) == 0) cv = zl(T, TDL_Z128, cv) ^ pn;
-    }
-    {
-      const uint32_t pn = row_down(cv, 2);
-      if ((g & 7) == 0) cv = zl(T, TDL_Z256, cv) ^ pn;
-    }
-    {
-      const uint32_t pn = row_down(cv, 3);
-      if ((g & 15) == 0) cv = zl(T, TDL_Z512, cv) ^ pn;
-    }
-    const uint32_t pass = row_bcast0(cv, lane);
+    const uint32_t pass = td_row_bcast0(cv, lane);
     if (on) acc = k ? zl(T, TDL_Z1024, acc) ^ pass : pass;
   }
   // walk(M || 0^z) = Z_z(walk(M)), undone by x^(-8z)
@@ -3688,10 +3725,10 @@ __device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u
 }
 
 // A row's frame staging through registers: the next group's frames are loaded (row_stage_load, 16 B units, lane g of
-// the row taking units g, g + 16, ...) while this group decodes, and stored to the row's input area when its turn
+// the row taking units g, g + TD_RL, ...) while this group decodes, and stored to the row's input area when its turn
 // comes (row_stage_store) -- the global-memory latency of the staging off the decode's path
-constexpr int TR_UNITS = 11;  // 16 lanes x 11 x 16 B >= the row's input staging
-static_assert(16 * TR_UNITS * 16 >= TR_IN, "row staging units");
+constexpr int TR_UNITS = (TR_IN + 16 * TD_RL - 1) / (16 * TD_RL);  // TD_RL lanes x TR_UNITS x 16 B >= the row's input
+static_assert(TD_RL * TR_UNITS * 16 >= TR_IN, "row staging units");
 struct RowStage {
   u32x4 t[TR_UNITS];
   uint32_t tail;
@@ -3700,7 +3737,7 @@ __device__ __forceinline__ void row_stage_load(RowStage& s, const uint32_t* za, 
   const uint32_t units = ndw >> 2;
 #pragma unroll
   for (int i = 0; i < TR_UNITS; ++i) {
-    const uint32_t u = g + 16 * i;
+    const uint32_t u = g + TD_RL * i;
     if (u < units) s.t[i] = *(const u32x4_ua*)(za + 4 * u);
   }
   // (unconditional: a select or an exec-masked load into the register would make the compiler wait for every load
@@ -3714,7 +3751,7 @@ __device__ __forceinline__ void row_stage_store(const RowStage& s, lds_u8* dst, 
   const uint32_t units = ndw >> 2;
 #pragma unroll
   for (int i = 0; i < TR_UNITS; ++i) {
-    const uint32_t u = g + 16 * i;
+    const uint32_t u = g + TD_RL * i;
     if (u < units) *(lds_u32x4_t*)(dst + 16 * u) = s.t[i];
   }
   if (g < (ndw & 3)) ((lds_u32_t*)dst)[4 * units + g] = s.tail;
@@ -3763,7 +3800,7 @@ __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool eli
     const uint32_t invz = inv[z];  // x^(-8z) (loaded now, used after the decode)
     if (__builtin_amdgcn_ballot_w64(have && type == 1))  // uncompressed: copied forward to B[0, ulen) (in place: the
       // destination is below the source, and each byte is read before anything is stored at or above it)
-      for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += 16) B[k] = in[q + k];
+      for (uint32_t k = g; k < (have && type == 1 ? ulen : 0u); k += TD_RL) B[k] = in[q + k];
     const bool dec = have && type == 0;
     const uint32_t rd = row_snappy_decode(B, ib + q, ib + next, 0u, ulen, dec, g, TR_ROW - 4);
     const bool ok = !dec || rd == 0;
@@ -3856,44 +3893,30 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   TD_STAMP(3);
   const bool dec = !over && chunks;
   for (uint32_t i = threadIdx.x; i < 256 + 16; i += blockDim.x) bad[i] = 0;
-  if (dec)  // the LDS image (TDL_*): the table image's T0..T3, then its Z64..Z1024
+  if (dec)  // the LDS image (TDL_*): the table image's T0..T3, then its Z64 or Z128 .. Z1024
     for (uint32_t i = threadIdx.x; i < TDL_WORDS / 4; i += blockDim.x)
-      ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i < 256 ? i : i + (TAB_ZPIECE + 2 * 1024 - TDL_Z64) / 4];
+      ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i < 256 ? i : i + (TDL_ZSRC - 1024) / 4];
   __syncthreads();
   if (dec) {
-    // this tile's frames (the meta blocks excluded): four per wave at a time, one per row, over a static share of
-    // the tile's 64 groups of four -- eight each with eight waves, two a SIMD (round 5's six waves: waves 2 and 3 took
-    // 12, the others 10: the hardware puts a workgroup's waves on the SIMDs in order, so waves 0/4 and 1/5 shared a
-    // SIMD and 2 and 3 had one each). A frame the row cannot decode (bad[] = 2) then through the whole wave, in two
-    // waves' row areas; then the last workgroup's wave 0 the meta blocks.
+    // this tile's frames (the meta blocks excluded): TD_RPW per wave at a time, one per row, over a static share of
+    // the tile's 256 / TD_RPW groups -- eight groups each (round 5's six waves of four rows: waves 2 and 3 took 12, the
+    // others 10: the hardware puts a workgroup's waves on the SIMDs in order, so waves 0/4 and 1/5 shared a SIMD and 2
+    // and 3 had one each). A frame the row cannot decode (bad[] = 2) then through the whole wave, in its wave's row
+    // area (or two waves'); then the last workgroup's wave 0 the meta blocks.
     const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
-    const uint32_t r = lane >> 4, g = lane & 15;
-#ifndef LCRC_TD_SPLIT
-#if LCRC_TD_WAVES == 8
-#define LCRC_TD_SPLIT 8, 8, 8, 8, 8, 8, 8, 8
-#else
-#define LCRC_TD_SPLIT 10, 10, 12, 12, 10, 10  // (a probe build may try another share)
-#endif
-#endif
-    constexpr uint32_t gsplit[TD_WAVES] = {LCRC_TD_SPLIT};
-    static_assert([] {
-      uint32_t sum = 0;
-      for (uint32_t i = 0; i < TD_WAVES; ++i) sum += gsplit[i];
-      return sum == 64;
-    }(), "the waves' shares cover the tile's 64 groups of four frames");
-    uint32_t gbeg = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < TD_WAVES; ++i) gbeg += i < wv ? gsplit[i] : 0u;
-    const uint32_t gcnt = gsplit[wv];
+    const uint32_t r = lane / TD_RL, g = lane % TD_RL;
+    constexpr uint32_t GPW = 256 / TD_RPW / TD_WAVES;  // groups a wave
+    static_assert(GPW * TD_RPW <= 64, "a wave's groups: one descriptor a lane");
+    const uint32_t gbeg = GPW * wv, gcnt = GPW;
     lds_u8* const rb = (lds_u8*)(td_lds + TDL_WORDS * 4 + wv * TD_WAVE_LDS + r * TR_ROW);
     const uint32_t* const inv = tab_c + TAB_INV;
-    // the wave's frames lo + 4 (gbeg + k) + r (k < gcnt): their descriptors loaded at once, lane 4 k + r holding frame
-    // k's of row r; each group's frames staged through registers one group ahead (RowStage)
+    // the wave's frames lo + TD_RPW (gbeg + k) + r (k < gcnt): their descriptors loaded at once, lane TD_RPW k + r
+    // holding frame k's of row r; each group's frames staged through registers one group ahead (RowStage)
     uint64_t d_off = 0;
     uint32_t d_len = 0;
     {
-      const uint64_t f = lo + 4 * (gbeg + (lane >> 2)) + (lane & 3);
-      if ((lane >> 2) < gcnt && f < hi) {
+      const uint64_t f = lo + TD_RPW * (gbeg + lane / TD_RPW) + lane % TD_RPW;
+      if (lane / TD_RPW < gcnt && f < hi) {
         d_len = frames[f].length;
         d_off = frames[f].offset;
         if (fstatus[f]) d_len |= 0x80000000u;  // (a frame whose framing walk failed: not live)
@@ -3901,11 +3924,11 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     }
     auto group = [&](uint32_t k, uint32_t& len, bool& live, bool& elig, uint32_t& d, const uint32_t*& za,
                      uint32_t& ndw) {
-      const int src = (int)(4 * (k & 15) + r) * 4;
+      const int src = (int)(TD_RPW * (k % GPW) + r) * 4;
       const uint32_t lw = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)d_len);
       const uint64_t of = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)d_off) |
                           ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(d_off >> 32)) << 32);
-      const bool valid = k < gcnt && lo + 4 * (gbeg + k) + r < hi;
+      const bool valid = k < gcnt && lo + TD_RPW * (gbeg + k) + r < hi;
       len = valid ? lw & 0x7FFFFFFFu : 0u;
       live = len && !(lw >> 31);
       elig = live && len + 3 <= TR_IN - 16;
@@ -3920,7 +3943,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     const uint32_t* za;
     group(0, len, live, elig, d, za, ndw);
     row_stage_load(stg, za, ndw, g);
-    for (uint32_t k = 0; k < gcnt && lo + 4 * (gbeg + k) < hi; ++k) {
+    for (uint32_t k = 0; k < gcnt && lo + TD_RPW * (gbeg + k) < hi; ++k) {
       const uint32_t len_c = len, d_c = d;
       const bool live_c = live, elig_c = elig;
       // the frame staged at the row's end (16-aligned), the decoded chunk growing from the row's start towards it
@@ -3930,18 +3953,18 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
       row_stage_load(stg, za, ndw, g);  // (in flight while this group decodes)
       __builtin_amdgcn_wave_barrier();
       const uint32_t v = row_frame(d_c, len_c, elig_c, T, rb, ib, g, lane, inv);
-      if (live_c && g == 0) bad[4 * (gbeg + k) + r] = elig_c ? (uint8_t)v : 2;
+      if (live_c && g == 0) bad[TD_RPW * (gbeg + k) + r] = elig_c ? (uint8_t)v : 2;
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the next group's loads stay in flight
       __builtin_amdgcn_wave_barrier();  // (the next round overwrites the row staging)
     }
   }
-  __syncthreads();  // every row done: the whole-wave decoder takes two waves' row areas
+  __syncthreads();  // every row done: the whole-wave decoder takes one or two (TD_WW) waves' row areas
   if (dec) {
     const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
-    uint8_t* const lin = td_lds + TDL_WORDS * 4 + (wv & ~1u) * TD_WAVE_LDS;
+    uint8_t* const lin = td_lds + TDL_WORDS * 4 + (wv / TD_WW) * TD_WW * TD_WAVE_LDS;
     uint8_t* const lout = lin + TD_IN + SN_SLACK;
-    if ((wv & 1) == 0)
-      for (uint64_t f = lo + wv / 2; f < hi; f += TD_WAVES / 2)
+    if (wv % TD_WW == 0)
+      for (uint64_t f = lo + wv / TD_WW; f < hi; f += TD_WAVES / TD_WW)
         if (bad[f - lo] == 2) {
           const bool ok = td_frame(file + frames[f].offset, frames[f].length, T, tab_c, lin, lout, out, out_off[f] + before, lane);
           __builtin_amdgcn_s_waitcnt(0);
