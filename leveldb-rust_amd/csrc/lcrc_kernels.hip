@@ -1854,7 +1854,7 @@ static_assert(TR_ROW % 16 == 0 && TR_IN + 16 <= TR_ROW && TR_OUT >= 4096, "row s
 constexpr uint32_t TD_WW = TD_IN + SN_SLACK + TD_OUT <= TD_WAVE_LDS ? 1 : 2;
 static_assert(TD_WAVES % TD_WW == 0 && TD_IN + SN_SLACK + TD_OUT <= TD_WW * TD_WAVE_LDS,
               "the whole-wave decoder's staging is one or two waves' row areas");
-constexpr uint32_t TD_LDS = TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16;
+constexpr uint32_t TD_LDS = TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16 + 16;  // + the rows' zero piece
 static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish");
 
 // `slow`: the decoded bytes (16-aligned) of the compressed chunks too large for k_ts_decode's LDS staging (TD_IN
@@ -3666,57 +3666,68 @@ __device__ __forceinline__ uint32_t td_row_bcast0(uint32_t v, uint32_t lane) {
 
 // The CRC-32C of M = V[0, len) per row, walked as M || 0^z to whole 1 KiB passes (z = 1024 np - len, undone at the end
 // by one GF(2) multiply with invz = x^(-8z)), the init register already XORed into the first min(4, len) bytes of M by
-// the caller (the decoded bytes are not kept): per 1 KiB pass each lane walks 1024 / TD_RL B (slice-by-4), the row tree joins
-// the lanes with Z64, Z128, Z256, Z512 (8-lane rows: 128 B a lane, Z128 .. Z512), and the passes chain with Z1024 -- a
-// quarter of the passes (and of their tree and broadcast) of 16 B per lane. The zeros are not in the row (round 6): a
-// chunk's last pass masks the bytes at and past len as it reads them (16 B reads end at most at len rounded up to 16,
-// inside the row), so the row holds M only.
-__device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, uint32_t len, bool active,
-                                                  uint32_t g, uint32_t lane, uint32_t invz) {
+// the caller (the decoded bytes are not kept): per 1 KiB pass each lane walks 1024 / TD_RL B (slice-by-4), the row tree
+// joins the lanes with Z64, Z128, Z256, Z512 (8-lane rows: 128 B a lane, Z128 .. Z512), and the passes chain with
+// Z1024. The zeros are not in the row (round 6): the caller zeroes M's bytes up to the next 16 B boundary, and a piece
+// wholly past M is read from Z0, 16 zero bytes. A lane's walk over a pass is one dependent chain of LDS lookups (32 of
+// them for 128 B), so the passes -- independent until the Z1024 chaining -- are walked at once, TR_NP chains a lane,
+// when a row of the wave has that many (every chunk that fills a row: a 4 KiB block); else one pass after the other.
+constexpr uint32_t TR_NP = (TR_OUT + 1023) / 1024;  // a row chunk's passes at most
+__device__ __forceinline__ uint32_t row_tree(const uint32_t* T, uint32_t cv, uint32_t g, uint32_t lane) {
+  // level m joins lane g with g + 2^m, shifting the left part by (1024 / TD_RL) * 2^m bytes (Z64 .. Z512 for 16
+  // lanes, Z128 .. Z512 for 8)
+#pragma unroll
+  for (int m = 0; (1u << m) < TD_RL; ++m) {
+    const uint32_t pn = row_down(cv, m);
+    const int zt = TD_RL == 16 ? (m == 0 ? TDL_Z64 : m == 1 ? TDL_Z128 : m == 2 ? TDL_Z256 : TDL_Z512)
+                               : (m == 0 ? TDL_Z128 : m == 1 ? TDL_Z256 : TDL_Z512);
+    if ((g & ((2u << m) - 1)) == 0) cv = zl(T, zt, cv) ^ pn;
+  }
+  return td_row_bcast0(cv, lane);
+}
+__device__ __forceinline__ uint32_t row_chunk_crc(const uint32_t* T, const lds_u8* V, const lds_u8* Z0, uint32_t len,
+                                                  bool active, uint32_t g, uint32_t lane, uint32_t invz) {
   constexpr uint32_t LB = 1024 / TD_RL, SP = LB / 16;  // bytes a lane walks per pass, in 16 B pieces
   const uint32_t np = active ? (len + 1023) >> 10 : 0u;
   uint32_t acc = 0;
-  for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
-    const bool on = k < np;
-    uint32_t cv = 0;
-    if (__builtin_amdgcn_ballot_w64(on && 1024 * (k + 1) > len)) {  // some row's last, partial pass
+  if (__builtin_amdgcn_ballot_w64(np == TR_NP)) {
+    uint32_t cv[TR_NP];
+#pragma unroll
+    for (uint32_t j = 0; j < TR_NP; ++j) cv[j] = 0;
+#pragma unroll
+    for (uint32_t sp = 0; sp < SP; ++sp) {
+      u32x4 w[TR_NP];
+#pragma unroll
+      for (uint32_t j = 0; j < TR_NP; ++j) {
+        const uint32_t x0 = 1024 * j + LB * g + 16 * sp;
+        w[j] = *(lds_cu32x4*)(x0 < len ? V + x0 : Z0);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (uint32_t j = 0; j < TR_NP; ++j) cv[j] = step4(T, cv[j], w[j][d]);
+    }
+    uint32_t pass[TR_NP];
+#pragma unroll
+    for (uint32_t j = 0; j < TR_NP; ++j) pass[j] = row_tree(T, cv[j], g, lane);
+#pragma unroll
+    for (uint32_t j = 0; j < TR_NP; ++j)
+      if (j < np) acc = j ? zl(T, TDL_Z1024, acc) ^ pass[j] : pass[j];
+  } else {
+    for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < np); ++k) {
+      uint32_t cv = 0;
 #pragma unroll
       for (uint32_t sp = 0; sp < SP; ++sp) {
         const uint32_t x0 = 1024 * k + LB * g + 16 * sp;
-        u32x4 w = *(lds_cu32x4*)(V + (on && x0 < len ? x0 : 0u));
-        const int rem = (int)len - (int)x0;  // bytes of M from x0 on
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int rd = rem - 4 * d;
-          w[d] &= rd >= 4 ? ~0u : rd <= 0 ? 0u : (1u << (8 * rd)) - 1u;
-        }
+        const u32x4 w = *(lds_cu32x4*)(x0 < len ? V + x0 : Z0);
         cv = step4(T, cv, w.x);
         cv = step4(T, cv, w.y);
         cv = step4(T, cv, w.z);
         cv = step4(T, cv, w.w);
       }
-    } else {
-#pragma unroll
-      for (uint32_t sp = 0; sp < SP; ++sp) {
-        const uint32_t x0 = 1024 * k + LB * g + 16 * sp;
-        const u32x4 w = *(lds_cu32x4*)(V + (on ? x0 : 0u));
-        cv = step4(T, cv, w.x);
-        cv = step4(T, cv, w.y);
-        cv = step4(T, cv, w.z);
-        cv = step4(T, cv, w.w);
-      }
+      const uint32_t pass = row_tree(T, cv, g, lane);
+      if (k < np) acc = k ? zl(T, TDL_Z1024, acc) ^ pass : pass;
     }
-    // row tree over LB-byte pieces: level m joins lane g with g + 2^m, shifting the left part by LB * 2^m bytes
-    // (Z64 .. Z512 for 16 lanes, Z128 .. Z512 for 8)
-#pragma unroll
-    for (int m = 0; (1u << m) < TD_RL; ++m) {
-      const uint32_t pn = row_down(cv, m);
-      const int zt = TD_RL == 16 ? (m == 0 ? TDL_Z64 : m == 1 ? TDL_Z128 : m == 2 ? TDL_Z256 : TDL_Z512)
-                                 : (m == 0 ? TDL_Z128 : m == 1 ? TDL_Z256 : TDL_Z512);
-      if ((g & ((2u << m) - 1)) == 0) cv = zl(T, zt, cv) ^ pn;
-    }
-    const uint32_t pass = td_row_bcast0(cv, lane);
-    if (on) acc = k ? zl(T, TDL_Z1024, acc) ^ pass : pass;
   }
   // walk(M || 0^z) = Z_z(walk(M)), undone by x^(-8z)
   if (__builtin_amdgcn_ballot_w64(active && (len & 1023) != 0)) acc = (len & 1023) ? gf_mul(invz, acc, 0x82F63B78u) : acc;
@@ -3762,7 +3773,8 @@ __device__ __forceinline__ void row_stage_store(const RowStage& s, lds_u8* dst, 
 // checksummed. Returns 0 good, 1 bad, 2 deferred to the whole-wave decoder (a chunk over TR_OUT, or an in-place decode
 // that would reach unread input).
 __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool elig, const uint32_t* T, lds_u8* B,
-                                              uint32_t ib, uint32_t g, uint32_t lane, const uint32_t* __restrict__ inv) {
+                                              const lds_u8* Z0, uint32_t ib, uint32_t g, uint32_t lane,
+                                              const uint32_t* __restrict__ inv) {
   lds_u8* const in = B + ib;
   // the framing was validated by k_ts_finish: headers and lengths are in bounds, preambles are sane
   uint32_t pos = d, res = 0;
@@ -3791,7 +3803,9 @@ __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool eli
         snappy_preamble([&](uint32_t i) { return (uint32_t)in[q + i]; }, next - q, ulen, used);
         q += used;
       }
-      if (ulen > TR_OUT) {  // too large for the row: the whole wave
+      // too large for the row, or M's zeroed bytes up to the next 16 B boundary would reach a later chunk's input:
+      // the whole wave
+      if (ulen > TR_OUT || (next < end && ((ulen + 15) & ~15u) > ib + next)) {
         res = 2;
         have = false;
       }
@@ -3808,9 +3822,13 @@ __device__ __forceinline__ uint32_t row_frame(uint32_t d, uint32_t len, bool eli
       res = 2;  // given up in place: the whole wave decodes the frame from the file
       have = false;
     }
-    // the init register injected into M's first bytes (the CRC masks the bytes past M: nothing is zeroed)
+    // B[ulen, ulen rounded up to 16) zeroed (the CRC reads whole 16 B pieces up to there, Z0 past it), then the init
+    // register injected into M's first bytes
+    const uint32_t u4 = (ulen + 3) & ~3u, u16 = (ulen + 15) & ~15u;
+    if (have && ulen + g < u4) B[ulen + g] = 0;
+    if (have && u4 + 4 * g < u16) *(__attribute__((address_space(3))) uint32_t*)(B + u4 + 4 * g) = 0;
     if (have && g < (ulen < 4 ? ulen : 4u)) B[g] ^= 0xFFu;
-    const uint32_t crc = row_chunk_crc(T, B, ulen, have, g, lane, invz);
+    const uint32_t crc = row_chunk_crc(T, B, Z0, ulen, have, g, lane, invz);
     if (have) {
       if (!ok || mask32c(crc) != want) res = 1;
       pos = next;
@@ -3892,7 +3910,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   }
   TD_STAMP(3);
   const bool dec = !over && chunks;
-  for (uint32_t i = threadIdx.x; i < 256 + 16; i += blockDim.x) bad[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 256 + 16 + 16; i += blockDim.x) bad[i] = 0;  // (+ the zero piece)
   if (dec)  // the LDS image (TDL_*): the table image's T0..T3, then its Z64 or Z128 .. Z1024
     for (uint32_t i = threadIdx.x; i < TDL_WORDS / 4; i += blockDim.x)
       ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i < 256 ? i : i + (TDL_ZSRC - 1024) / 4];
@@ -3952,7 +3970,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
       group(k + 1, len, live, elig, d, za, ndw);
       row_stage_load(stg, za, ndw, g);  // (in flight while this group decodes)
       __builtin_amdgcn_wave_barrier();
-      const uint32_t v = row_frame(d_c, len_c, elig_c, T, rb, ib, g, lane, inv);
+      const uint32_t v = row_frame(d_c, len_c, elig_c, T, rb, (const lds_u8*)(bad + 256 + 16), ib, g, lane, inv);
       if (live_c && g == 0) bad[TD_RPW * (gbeg + k) + r] = elig_c ? (uint8_t)v : 2;
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the next group's loads stay in flight
       __builtin_amdgcn_wave_barrier();  // (the next round overwrites the row staging)
