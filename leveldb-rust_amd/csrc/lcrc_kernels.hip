@@ -1856,6 +1856,14 @@ static_assert(TD_WAVES % TD_WW == 0 && TD_IN + SN_SLACK + TD_OUT <= TD_WW * TD_W
               "the whole-wave decoder's staging is one or two waves' row areas");
 constexpr uint32_t TD_LDS = TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16 + 16;  // + the rows' zero piece
 static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish");
+// workgroups per 256-block tile of k_ts_finish: each takes TD_SUBN = 256 / TD_SUB frames (round 6: four, so that the
+// decode's work is dealt in ~100 us pieces -- with one workgroup a tile, all 256 resident at once, a CU held by the
+// other stream's index decode (k_ts_open2, ~210 us, a whole CU's LDS too) delayed its tile's whole decode by that much)
+#ifndef LCRC_TD_SUB
+#define LCRC_TD_SUB 4
+#endif
+constexpr uint32_t TD_SUB = LCRC_TD_SUB, TD_SUBN = 256 / TD_SUB;
+static_assert(TD_SUBN * TD_SUB == 256 && TD_SUBN % (TD_RPW * TD_WAVES) == 0, "whole groups a wave");
 
 // `slow`: the decoded bytes (16-aligned) of the compressed chunks too large for k_ts_decode's LDS staging (TD_IN
 // compressed, TD_OUT decoded), which it decodes lane-serially into the table scan's workspace
@@ -3848,30 +3856,33 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
                                                             uint64_t bound) {
   extern __shared__ __attribute__((aligned(16))) uint8_t td_lds[];
   uint32_t* const T = (uint32_t*)td_lds;
+  // workgroup b: sub-tile b % TD_SUB of tile t = b / TD_SUB, the frames lo .. lo + TD_SUBN
+  const uint64_t t = blockIdx.x / TD_SUB, lo = t * 256 + (blockIdx.x % TD_SUB) * TD_SUBN;
   // the content verdict's inputs for this thread's block, loaded with the state (bound: the arrays' length)
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t j = lo + threadIdx.x;
   uint8_t fs_j = 0;
   uint64_t off_j = 0, off_p = 0;
-  if (threadIdx.x < 256 && j < bound) {
+  if (threadIdx.x < TD_SUBN && j < bound) {
     fs_j = fstatus[j];
     off_j = blk[j].offset;
     off_p = j ? blk[j - 1].offset : 0;
   }
-  uint8_t* const bad = td_lds + TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // 256 tile flags + the meta blocks
+  uint8_t* const bad = td_lds + TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS;  // the sub-tile's flags (256) + the meta blocks
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
   // the block count from fields ts_final leaves alone (it may shrink n_total while later workgroups start)
   const bool live = st->status == TS_OK && !st->idx_only;
   const uint64_t n = live ? st->n_data + (st->has_filter ? 3 : 2) : 0;
-  // one workgroup per 256 data blocks; the meta blocks after them (filter, metaindex, index) are the last workgroup's
-  // (its wave 0, after the rows). A table of 65,536 data blocks is then 256 workgroups, all resident at once (one per
-  // CU), not 257; and a table without a filter keeps its last data block in the rows (as one of "the last three" it
-  // went through the whole-wave decoder alone, after the rows: ~35 us of the scan's tail)
-  const uint64_t tail = live ? st->n_data : 0, tiles = n ? (tail + 255) / 256 + (tail ? 0 : 1) : 0, t = blockIdx.x;
-  const bool last = n && t == tiles - 1;
-  if (t >= tiles && t != 0) return;  // (workgroup 0 runs ts_final when nothing is live)
-#ifdef LCRC_PROBE_CLOCK  // diagnostic build: phase stamps of workgroup t in lcrc_dbg_stamp row 2304 + t
+  // TD_SUB workgroups per 256 data blocks; the meta blocks after them (filter, metaindex, index) are the last
+  // workgroup's (its wave 0, after the rows): a table of 65,536 data blocks is 256 tiles, not 257; and a table without
+  // a filter keeps its last data block in the rows (as one of "the last three" it went through the whole-wave decoder
+  // alone, after the rows: ~35 us of the scan's tail)
+  const uint64_t tail = live ? st->n_data : 0, tiles = n ? (tail + 255) / 256 + (tail ? 0 : 1) : 0;
+  const bool last = n && t == tiles - 1 && blockIdx.x % TD_SUB == TD_SUB - 1;
+  // (workgroup 0 runs ts_final when nothing is live; a sub-tile past the data blocks has nothing else to do)
+  if ((t >= tiles || lo >= tail) && blockIdx.x != 0 && !last) return;
+#ifdef LCRC_PROBE_CLOCK  // diagnostic build: phase stamps of workgroup b in lcrc_dbg_stamp row 2304 + b
 #define TD_STAMP(k) \
-  if (threadIdx.x == 0 && t < 768) lcrc_dbg_stamp[(2304 + t) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+  if (threadIdx.x == 0 && blockIdx.x < 768) lcrc_dbg_stamp[(2304 + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define TD_STAMP(k)
 #endif
@@ -3902,7 +3913,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   // recorded by workgroup 0 and by the last tile's workgroup (the same values): the last one runs ts_final and is the
   // only one that changes st->status, so its `live` is always the scan's own; workgroup 0 may read a status the last
   // one has already set to TS_HOST (frames over the workspace) and skip the record
-  if (threadIdx.x == 0 && live && (t == 0 || last)) {
+  if (threadIdx.x == 0 && live && (blockIdx.x == 0 || last)) {
     st->need_out = total;
     st->need_chunks = chunks;
     st->gate = over ? 1u : chunks == 0 ? 2u : 0u;
@@ -3916,14 +3927,14 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
       ((u32x4*)T)[i] = ((const u32x4*)tab_c)[i < 256 ? i : i + (TDL_ZSRC - 1024) / 4];
   __syncthreads();
   if (dec) {
-    // this tile's frames (the meta blocks excluded): TD_RPW per wave at a time, one per row, over a static share of
-    // the tile's 256 / TD_RPW groups -- eight groups each (round 5's six waves of four rows: waves 2 and 3 took 12, the
-    // others 10: the hardware puts a workgroup's waves on the SIMDs in order, so waves 0/4 and 1/5 shared a SIMD and 2
-    // and 3 had one each). A frame the row cannot decode (bad[] = 2) then through the whole wave, in its wave's row
-    // area (or two waves'); then the last workgroup's wave 0 the meta blocks.
-    const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
+    // this sub-tile's frames (the meta blocks excluded): TD_RPW per wave at a time, one per row, over a static share of
+    // the sub-tile's TD_SUBN / TD_RPW groups, the same for every wave (round 5's six waves of four rows: waves 2 and 3
+    // took more, as the hardware puts a workgroup's waves on the SIMDs in order, so waves 0/4 and 1/5 shared a SIMD).
+    // A frame the row cannot decode (bad[] = 2) then through the whole wave, in its wave's row area (or two waves');
+    // then the last workgroup's wave 0 the meta blocks.
+    const uint64_t hi = lo + TD_SUBN < tail ? lo + TD_SUBN : tail;
     const uint32_t r = lane / TD_RL, g = lane % TD_RL;
-    constexpr uint32_t GPW = 256 / TD_RPW / TD_WAVES;  // groups a wave
+    constexpr uint32_t GPW = TD_SUBN / TD_RPW / TD_WAVES;  // groups a wave
     static_assert(GPW * TD_RPW <= 64, "a wave's groups: one descriptor a lane");
     const uint32_t gbeg = GPW * wv, gcnt = GPW;
     lds_u8* const rb = (lds_u8*)(td_lds + TDL_WORDS * 4 + wv * TD_WAVE_LDS + r * TR_ROW);
@@ -3978,7 +3989,7 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
   }
   __syncthreads();  // every row done: the whole-wave decoder takes one or two (TD_WW) waves' row areas
   if (dec) {
-    const uint64_t lo = t * 256, hi = lo + 256 < tail ? lo + 256 : tail;
+    const uint64_t hi = lo + TD_SUBN < tail ? lo + TD_SUBN : tail;
     uint8_t* const lin = td_lds + TDL_WORDS * 4 + (wv / TD_WW) * TD_WW * TD_WAVE_LDS;
     uint8_t* const lout = lin + TD_IN + SN_SLACK;
     if (wv % TD_WW == 0)
@@ -4012,12 +4023,12 @@ __global__ void __launch_bounds__(64 * TD_WAVES) k_ts_decode(const uint8_t* __re
     if (fstatus[j] || fb) blk[j].status = 3;  // LCRC_TBLK_BAD_CONTENT
     if (j > 0 && blk[j - 1].offset > blk[j].offset) st->unsorted = 1;
   };
-  if (threadIdx.x < 256 && j < tail) {  // (content() with the values loaded at the start)
+  if (threadIdx.x < TD_SUBN && j < tail && j < lo + TD_SUBN) {  // (content() with the values loaded at the start)
     if (fs_j || bad[threadIdx.x]) blk[j].status = 3;  // LCRC_TBLK_BAD_CONTENT
     if (j > 0 && off_p > off_j) st->unsorted = 1;
   }
   TD_STAMP(4);
-  if (threadIdx.x == 0 && (last || (n == 0 && t == 0))) {
+  if (threadIdx.x == 0 && (last || (n == 0 && blockIdx.x == 0))) {
     for (uint64_t k = tail; k < n; ++k) content(k, bad[256 + (k - tail)] != 0);
     if (over && st->status == TS_OK) st->status = TS_HOST;
     ts_final(st, blk, n_out, status_out);
@@ -4815,7 +4826,7 @@ hipError_t lcrc_launch_ts_decode(const uint8_t* file, const lcrc_desc_dev* frame
   static const hipError_t attr = hipFuncSetAttribute((const void*)lcrc_dev::k_ts_decode,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lcrc_dev::TD_LDS);
   if (attr != hipSuccess) return attr;
-  const uint64_t g = (bound + 255) / 256;
+  const uint64_t g = (bound + 255) / 256 * lcrc_dev::TD_SUB;
   LCRC_LAUNCH(lcrc_dev::k_ts_decode, dim3((unsigned)(g ? g : 1)), dim3(64 * lcrc_dev::TD_WAVES), lcrc_dev::TD_LDS, s,
               file, frames, out_off, out, fstatus, st, blk, tab_c, ts_out_cap, tparts, n_out, status_out, bound);
   return hipGetLastError();
