@@ -1856,11 +1856,12 @@ static_assert(TD_WAVES % TD_WW == 0 && TD_IN + SN_SLACK + TD_OUT <= TD_WW * TD_W
               "the whole-wave decoder's staging is one or two waves' row areas");
 constexpr uint32_t TD_LDS = TDL_WORDS * 4 + TD_WAVES * TD_WAVE_LDS + 256 + 16 + 16;  // + the rows' zero piece
 static_assert(TD_LDS + 4160 + 344 <= 163840, "k_ts_decode's LDS leaves room for k_ts_finish");
-// workgroups per 256-block tile of k_ts_finish: each takes TD_SUBN = 256 / TD_SUB frames (round 6: four, so that the
-// decode's work is dealt in ~100 us pieces -- with one workgroup a tile, all 256 resident at once, a CU held by the
-// other stream's index decode (k_ts_open2, ~210 us, a whole CU's LDS too) delayed its tile's whole decode by that much)
+// workgroups per 256-block tile of k_ts_finish: each takes TD_SUBN = 256 / TD_SUB frames (round 6: two, so that the
+// decode's work is dealt in ~200 us pieces -- with one workgroup a tile, all 256 resident at once, a CU held by the
+// other stream's index decode (k_ts_open2, ~210 us, a whole CU's LDS too) delayed its tile's whole decode by that
+// much; four sub-tiles cost 26 us more alone: each workgroup's table image, gate and slowest-wave barrier)
 #ifndef LCRC_TD_SUB
-#define LCRC_TD_SUB 4
+#define LCRC_TD_SUB 2
 #endif
 constexpr uint32_t TD_SUB = LCRC_TD_SUB, TD_SUBN = 256 / TD_SUB;
 static_assert(TD_SUBN * TD_SUB == 256 && TD_SUBN % (TD_RPW * TD_WAVES) == 0, "whole groups a wave");
