@@ -190,3 +190,50 @@ def test_row_decoder_elements(lcrc, orc, engines, seed):
     assert _expect_async(lcrc, eng, orc, f) == 0
     got, err = _scan(lcrc, eng, f)
     assert err is None and _as_tuples(got) == want
+
+
+def over_row_cases(orc, seed=31, count=24):
+    """Valid and corrupted frames whose chunk decodes to more than a row holds (ROW_OUT < size <= 5,200 B: the row path
+    of rounds 4-5, whose 5,136 B rows held them) but whose frame fits the row staging: k_ts_decode hands each to the
+    whole-wave decoder after the rows. Some with a wrong chunk CRC, some with output past the preamble's length."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    while len(cases) < count:
+        target = int(rng.integers(ROW_OUT + 1, 5200))
+        pay, dec = gen_stream(rng, target, lit_max=60)
+        if dec is None or not ROW_OUT < len(dec) <= 5200:
+            continue
+        fr = _frame(orc, pay, dec)
+        if len(fr) > 2701:
+            continue
+        r = rng.random()
+        if r < 0.15:
+            fr = bytearray(fr)
+            fr[len(STREAM) + 4] ^= 1
+            cases.append((bytes(fr), None))
+        elif r < 0.25:
+            cases.append((_frame(orc, pay, dec, ulen=len(dec) - 1), None))
+        else:
+            cases.append((fr, dec))
+    return cases
+
+
+def test_over_row_cases_match_oracle(orc, lcrc):
+    for fr, want in over_row_cases(orc):
+        assert orc.snappy_frame_decode(fr) == want
+        assert lcrc.snappy_frame_decode(fr) == want
+
+
+@pytest.mark.gpu
+def test_row_decoder_over_row(lcrc, orc, engines):
+    from test_table_scan import _scan
+    from test_table_scan_async import _expect_async
+    cases = over_row_cases(orc) + row_cases(orc, 41, 24)
+    f = frames_table(orc, [fr for fr, _ in cases])
+    want, werr = orc.table_scan_expect(f)
+    assert werr is None
+    assert [w[4] for w in want if w[2] == 0] == [0 if d is not None else 3 for _, d in cases]
+    eng = engines[lcrc.MODE_REF]
+    assert _expect_async(lcrc, eng, orc, f) == 0
+    got, err = _scan(lcrc, eng, f)
+    assert err is None and _as_tuples(got) == want
