@@ -680,3 +680,55 @@ def test_async_four_contexts_full_index_grid(lcrc, orc):
             s.close()
         for eng in engs:
             eng.close()
+
+
+def _bench_like_tables(lcrc, orc, sizes):
+    """Compressed tables of db_bench-style 4 KiB blocks (k_ts_decode's row path: 8 frames a wave, sub-tiles of 128
+    frames), written by the library's TableBuilder (synth.compressed_table); the last one with some data frames
+    corrupted and their block trailers re-sealed, so only the frames' chunk CRCs or decodes can tell."""
+    synth = __import__("leveldb_rust_amd.synth", fromlist=["x"])
+    out = []
+    for k, n in enumerate(sizes):
+        f, tb = synth.compressed_table(lcrc, n)
+        f = bytearray(f.tobytes())
+        blocks = [(int(b["offset"]), int(b["size"]), int(b["kind"])) for b in tb]
+        if k == len(sizes) - 1:
+            data = [b for b in blocks if b[2] == lcrc.TBLK_DATA and f[b[0] + b[1]] == 1]
+            for j in (0, 127, 128, 255, 256, len(data) // 2, len(data) - 1):
+                off, size, _ = data[j]
+                f[off + size // 2 + j % 7] ^= 0x20
+                f[off + size + 1:off + size + 5] = orc.crc(bytes(f[off:off + size + 1]), 0).to_bytes(4, "little")
+        out.append((bytes(f), blocks))
+    return out
+
+
+@pytest.mark.gpu
+def test_async_compressed_contexts_concurrent(lcrc, orc):
+    """Three contexts scanning compressed tables of 4 KiB blocks on their own streams at once, four rounds enqueued
+    back to back: the decode's workgroups of one launch share the CUs with the other launches' (a whole CU's LDS
+    each), and every result -- the corrupted frames' content verdicts included -- equals the oracle's
+    (format.rs:194-206 through read_block_from_file)."""
+    tables = _bench_like_tables(lcrc, orc, (700, 1300, 1500))
+    want = [orc.table_scan_expect(f)[0] for f, _b in tables]
+    assert sum(1 for w in want[2] if w[4] == 3) == 7 and all(w[4] == 0 for w in want[0] + want[1])
+    engs = [lcrc.Engine(0, lcrc.MODE_REF) for _ in tables]
+    scans = []
+    try:
+        for eng, (f, blocks) in zip(engs, tables):
+            eng.table_scan_reserve(len(f), len(blocks) + 4, 8 << 20)
+            scans.append(_Scan(lcrc, f, len(blocks) + 4))
+        for _ in range(4):
+            for s in scans:
+                s.blocks.zero()
+            for eng, s in zip(engs, scans):
+                eng.table_scan_async(s.file, s.n, s.blocks, s.cap, s.count, s.status, snappy_index=True)
+            for eng in engs:
+                eng.sync()
+            for k, (s, w) in enumerate(zip(scans, want)):
+                st, code, n, got = s.read()
+                assert st == OK and sorted(_as_tuples(got)) == w, k
+    finally:
+        for s in scans:
+            s.close()
+        for eng in engs:
+            eng.close()
