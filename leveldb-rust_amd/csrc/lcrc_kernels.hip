@@ -3397,17 +3397,18 @@ __global__ void __launch_bounds__(256) k_store_crc(uint8_t* __restrict__ base, u
 // decoded bytes' round trip through HBM: a chunk decoded in LDS is checksummed there and never written out
 // (format.rs:194-206; the snap crate's FrameDecoder checks each chunk's masked CRC-32C).
 //
-// One workgroup of TD_WAVES waves per 256-block tile of k_ts_finish (its in-tile scans of the frames' padded decoded
-// sizes give each frame's global-memory workspace for the lane-serial path; the workgroup adds the tiles before its
-// own once). A wave decodes four frames at a time, one per 16-lane row (row_frame); a frame the row staging cannot
-// hold goes through the whole wave (td_frame). The last three blocks (filter, metaindex, index: whatever ts_final may
-// move) are the last tile's.
+// TD_SUB workgroups of TD_WAVES waves per 256-block tile of k_ts_finish (its in-tile scans of the frames' padded
+// decoded sizes give each frame's global-memory workspace for the lane-serial path; each workgroup adds the tiles
+// before its own once). A wave decodes 64 / TD_RL frames at a time, one per TD_RL-lane row (row_frame); a frame the
+// row staging cannot hold goes through the whole wave (td_frame). The last three blocks (filter, metaindex, index:
+// whatever ts_final may move) are the last workgroup's.
 //
-// Chunk CRC (td_chunk_crc): the chunk M is read as V = 0^pad || M, |V| = 1024 np (leading zeros walked from register
-// 0 stay 0, so walk(0, V) = walk(0, M)); per 1 KiB pass each lane walks 16 B (slice-by-4), the 16-lane rows join with
-// Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- T0..T3 and Z64 or Z128 .. Z1024 from
-// k_ts_decode's LDS image (TDL_*), the shorter shifts (used by this path only) from the table image in global memory. The init register is
-// injected into the first min(4, |M|) bytes: walk(R, M) = walk(0, M ^ LE(R)) ^ (R >> 8 |M|) for |M| < 4.
+// Whole-wave chunk CRC (td_chunk_crc): the chunk M is read as V = 0^pad || M, |V| = 1024 np (leading zeros walked from
+// register 0 stay 0, so walk(0, V) = walk(0, M)); per 1 KiB pass each lane walks 16 B (slice-by-4), the 16-lane rows
+// join with Z16..Z128, the four rows with Z256 / Z512, the passes with Z1024 -- T0..T3 and Z64 or Z128 .. Z1024 from
+// k_ts_decode's LDS image (TDL_*), the shorter shifts (used by this path only) from the table image in global memory.
+// The init register is injected into the first min(4, |M|) bytes: walk(R, M) = walk(0, M ^ LE(R)) ^ (R >> 8 |M|) for
+// |M| < 4.
 // ---------------------------------------------------------------------------------------------------
 
 // the piece of pass k of lane `lane`: V[1024 k + 16 lane, +16), init injected into V[pad, pad + q)
