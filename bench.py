@@ -64,6 +64,8 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", choices=["fixed", "mixed", "wal", "table", "snappy", "seal"], default="fixed")
+    p.add_argument("--timer-read-inside", action="store_true",
+                   help="read the kernel-carried GPU clock before the wall clock stops (round 5's order; for A/B runs)")
     p.add_argument("--marker-timer", action="store_true",
                    help="fixed config: time the roofline with event markers after the first submission instead of "
                         "events carried by the launches")
@@ -196,7 +198,7 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False, kernels_per_step=1):
+def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False, kernels_per_step=1, read_inside=False):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides.
     `prepare(first, count)` returns the submissions for steps first .. first+count-1 as (submit, launches,
     steps[, engine]) tuples (argument marshalling done before the clock starts). The wall clock covers all K
@@ -208,6 +210,8 @@ def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False, ker
         submission the first engine's stream joins every other engine (lcrc_ctx_join) and an end event follows:
         first launch's start to the end of the last kernel of any engine.
       * otherwise: an event behind the first submission to the joined end event (steps 2..K).
+    With carried events the GPU clock is read after the wall clock stops (the events are complete once the engines
+    are synchronised: reading them is bookkeeping, not the steps' work); `read_inside` reads it before, as round 5.
     Returns (max-over-ranks wall seconds, this rank's wall seconds, GPU ms, launches and steps the GPU clock
     covers)."""
     mode = "marker" if not (engines and kernel_events) else "carried" if kernels_per_step == 1 else "start"
@@ -264,10 +268,16 @@ def timed_run(dist, prepare, steps, warmup, engines=(), kernel_events=False, ker
     dist.barrier()
     t0 = time.perf_counter()
     first, last = submit(subs)
-    gpu_ms = finish(first, last, len(subs))
-    for e in engines:
-        e.sync()
-    elapsed = time.perf_counter() - t0
+    if mode == "carried" and not read_inside:
+        for e in engines:
+            e.sync()
+        elapsed = time.perf_counter() - t0
+        gpu_ms = finish(first, last, len(subs))
+    else:  # (the end event is recorded by finish(): it must follow the last submission before the wait)
+        gpu_ms = finish(first, last, len(subs))
+        for e in engines:
+            e.sync()
+        elapsed = time.perf_counter() - t0
     dist.barrier()
     first = 1 if mode == "marker" else 0
     cov_launches = sum(sub[1] for sub in subs[first:])
@@ -912,7 +922,7 @@ def main(argv=None):
     fp = int(np.bitwise_xor.reduce(w.crcs())) if w.crcs is not None else 0
     elapsed_max, elapsed, gpu_ms, cov_launches, cov_steps = timed_run(
         dist, prepare, args.steps, args.warmup, timers, kernel_events=w.kernel_events,
-        kernels_per_step=w.cfg.get("kernels_per_step", 1))
+        kernels_per_step=w.cfg.get("kernels_per_step", 1), read_inside=args.timer_read_inside)
     value = aggregate_gibs(w.nbytes, args.steps, world, elapsed_max)
     # this rank's per-launch figure of the dominant kernel (its own HIP events; -1 when not timed on the GPU)
     launch_us = gpu_ms * 1e3 / cov_launches if (timers and gpu_ms and cov_launches) else -1.0
