@@ -237,3 +237,56 @@ def test_row_decoder_over_row(lcrc, orc, engines):
     assert _expect_async(lcrc, eng, orc, f) == 0
     got, err = _scan(lcrc, eng, f)
     assert err is None and _as_tuples(got) == want
+
+
+def boundary_cases(orc, seed=51):
+    """Frames whose chunk decodes to an exact size at the row decoder's edges: below one 16 B piece, at and around
+    whole 1 KiB CRC passes (no zero padding to undo), and at ROW_OUT and one past it (the whole-wave decoder), each
+    compressed enough for the row staging (64 literal bytes, then copies of them); plus uncompressed chunks up to the
+    staging's limit, and a few of each with a wrong chunk CRC."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    sizes = [1, 3, 4, 5, 15, 16, 17, 63, 64, 65, 1023, 1024, 1025, 2048, 3072, 4095, 4096, 4097,
+             ROW_OUT - 16, ROW_OUT - 15, ROW_OUT - 1, ROW_OUT, ROW_OUT + 1]
+    for n in sizes:
+        head = bytes(rng.integers(0, 256, min(n, 64), dtype=np.uint8))
+        pay = bytearray(_lit_el(head, 0 if len(head) <= 60 else 1))
+        dec = bytearray(head)
+        while len(dec) < n:
+            m = min(64, n - len(dec))
+            off = 64 if m >= 4 or len(dec) >= 64 else len(dec)
+            pay += _copy_el(off, m, 2)
+            for _ in range(m):
+                dec.append(dec[-off])
+        fr = _frame(orc, bytes(pay), bytes(dec))
+        assert len(fr) <= 2701
+        cases.append((fr, bytes(dec)))
+    for n in (1, 4, 16, 1024, 2048, 2683):
+        data = bytes(rng.integers(0, 256, n, dtype=np.uint8))
+        cases.append((STREAM + _chunk(orc, 1, data, data), data))
+    for k in (2, 9, 13, 19, 24):  # wrong chunk CRCs
+        fr = bytearray(cases[k][0])
+        fr[len(STREAM) + 4] ^= 0x80
+        cases.append((bytes(fr), None))
+    return cases
+
+
+def test_boundary_cases_match_oracle(orc, lcrc):
+    for fr, want in boundary_cases(orc):
+        assert orc.snappy_frame_decode(fr) == want
+        assert lcrc.snappy_frame_decode(fr) == want
+
+
+@pytest.mark.gpu
+def test_row_decoder_boundaries(lcrc, orc, engines):
+    from test_table_scan import _scan
+    from test_table_scan_async import _expect_async
+    cases = boundary_cases(orc)
+    f = frames_table(orc, [fr for fr, _ in cases])
+    want, werr = orc.table_scan_expect(f)
+    assert werr is None
+    assert [w[4] for w in want if w[2] == 0] == [0 if d is not None else 3 for _, d in cases]
+    eng = engines[lcrc.MODE_REF]
+    assert _expect_async(lcrc, eng, orc, f) == 0
+    got, err = _scan(lcrc, eng, f)
+    assert err is None and _as_tuples(got) == want
